@@ -1,0 +1,344 @@
+"""CPU oracle for the ST-CGAN hot path -- TEST INFRASTRUCTURE ONLY.
+
+A from-scratch, functional torch-CPU restatement of the reference algorithm:
+  * U-Net generator  (STCGAN/networks.py:31-143, odd-size pad/crop of
+    src/models/stcgan_g.py:120-132)
+  * PatchGAN discriminator (STCGAN/networks.py:147-192)
+  * DataLoss / AdversarialLoss (STCGAN/loss.py:14-26, 59-86)
+  * Adam (torch.optim.Adam as pinned by the reference, STCGAN/stcgan.py:60-65)
+  * one training / validation epoch (STCGAN/stcgan.py:186-330)
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / the timed CPU baseline.  The
+product path (shadow-removal-istd_amd/stcgan_amd) never imports it.
+
+Parity of this restatement is pinned against golden vectors produced by
+running the reference itself in the build container
+(tests/golden/make_goldens.py -> tests/golden/*.npz; checked by
+tests/test_oracle_golden.py).
+
+Networks are expressed over plain ``state`` dicts whose keys are exactly the
+reference ``state_dict`` keys, so reference checkpoints load unchanged.
+"""
+from collections import OrderedDict
+
+import torch
+import torch.nn.functional as F
+
+BN_EPS = 1e-5       # nn.BatchNorm2d default (STCGAN/networks.py:107,109)
+BN_MOMENTUM = 0.1   # nn.BatchNorm2d default
+LRELU = 0.2         # STCGAN/networks.py:102,158
+
+
+# --------------------------------------------------------------------------- keys
+def gen_block_prefix(level):
+    """Prefix of the UnetSkipConnectionBlock at ``level`` (0 = outermost)."""
+    if level == 0:
+        return "model.model."
+    return "model.model.1" + ".model.3" * (level - 1) + ".model."
+
+
+def _conv_shape(cout, cin):
+    return (cout, cin, 4, 4)
+
+
+def generator_state_template(in_channels, out_channels, ngf=64, num_downs=8):
+    """Keys/shapes of UnetGenerator.state_dict() in the reference order (STCGAN/networks.py:31-71)."""
+    # channel plan, outermost -> innermost: (outer_nc, inner_nc) per block
+    plan = [(out_channels, ngf), (ngf, ngf * 2), (ngf * 2, ngf * 4), (ngf * 4, ngf * 8)]
+    plan += [(ngf * 8, ngf * 8)] * (num_downs - 4)
+    st = OrderedDict()
+
+    def bn(prefix, c):
+        st[prefix + "weight"] = torch.zeros(c)
+        st[prefix + "bias"] = torch.zeros(c)
+        st[prefix + "running_mean"] = torch.zeros(c)
+        st[prefix + "running_var"] = torch.ones(c)
+        st[prefix + "num_batches_tracked"] = torch.zeros((), dtype=torch.long)
+
+    def block(level):
+        outer, inner = plan[level]
+        p = gen_block_prefix(level)
+        if level == 0:
+            st[p + "0.weight"] = torch.zeros(_conv_shape(inner, in_channels))
+            block(1)
+            st[p + "3.weight"] = torch.zeros((inner * 2, outer, 4, 4))
+            st[p + "3.bias"] = torch.zeros(outer)
+        elif level == num_downs - 1:
+            st[p + "1.weight"] = torch.zeros(_conv_shape(inner, outer))
+            st[p + "3.weight"] = torch.zeros((inner, outer, 4, 4))
+            bn(p + "4.", outer)
+        else:
+            st[p + "1.weight"] = torch.zeros(_conv_shape(inner, outer))
+            bn(p + "2.", inner)
+            block(level + 1)
+            st[p + "5.weight"] = torch.zeros((inner * 2, outer, 4, 4))
+            bn(p + "6.", outer)
+
+    block(0)
+    return st
+
+
+def discriminator_state_template(in_channels, ndf=64, n_layers=3):
+    """Keys/shapes of NLayerDiscriminator.state_dict() (STCGAN/networks.py:147-192)."""
+    st = OrderedDict()
+    st["model.0.weight"] = torch.zeros(_conv_shape(ndf, in_channels))
+    st["model.0.bias"] = torch.zeros(ndf)
+    idx = 2
+    mult = 1
+    for n in range(1, n_layers + 1):
+        prev, mult = mult, min(2 ** n, 8)
+        st[f"model.{idx}.weight"] = torch.zeros(_conv_shape(ndf * mult, ndf * prev))
+        for k in ["weight", "bias"]:
+            st[f"model.{idx + 1}.{k}"] = torch.zeros(ndf * mult)
+        st[f"model.{idx + 1}.running_mean"] = torch.zeros(ndf * mult)
+        st[f"model.{idx + 1}.running_var"] = torch.ones(ndf * mult)
+        st[f"model.{idx + 1}.num_batches_tracked"] = torch.zeros((), dtype=torch.long)
+        idx += 3
+    st[f"model.{idx}.weight"] = torch.zeros(_conv_shape(1, ndf * mult))
+    st[f"model.{idx}.bias"] = torch.zeros(1)
+    return st
+
+
+# --------------------------------------------------------------------------- layers
+def batch_norm(st, prefix, x, train):
+    """BatchNorm2d: batch stats (biased var) in train, running stats in eval;
+    running update uses the unbiased var and num_batches_tracked += 1."""
+    w, b = st[prefix + "weight"], st[prefix + "bias"]
+    rm, rv = st[prefix + "running_mean"], st[prefix + "running_var"]
+    if train:
+        n = x.numel() // x.shape[1]
+        mean = x.mean(dim=(0, 2, 3))
+        var = x.var(dim=(0, 2, 3), unbiased=False)
+        with torch.no_grad():
+            rm.mul_(1 - BN_MOMENTUM).add_(mean.detach() * BN_MOMENTUM)
+            rv.mul_(1 - BN_MOMENTUM).add_(var.detach() * (n / max(n - 1, 1)) * BN_MOMENTUM)
+            st[prefix + "num_batches_tracked"].add_(1)
+        xhat = (x - mean[None, :, None, None]) * torch.rsqrt(var + BN_EPS)[None, :, None, None]
+    else:
+        xhat = (x - rm[None, :, None, None]) * torch.rsqrt(rv + BN_EPS)[None, :, None, None]
+    return xhat * w[None, :, None, None] + b[None, :, None, None]
+
+
+def _gen_block(st, x, level, num_downs, train):
+    """UnetSkipConnectionBlock.forward for a non-outermost block.
+
+    The block's first op is an in-place LeakyReLU on its input, so at even sizes
+    the skip half of the concat is LeakyReLU(x) (STCGAN/networks.py:106,143);
+    at odd sizes the block pads a copy first and the skip is x itself
+    (src/models/stcgan_g.py:124-132).  ReLU(LeakyReLU(v)) == ReLU(v), so both
+    give the same parent input.
+    """
+    p = gen_block_prefix(level)
+    h, w = x.shape[2], x.shape[3]
+    odd = (h % 2) or (w % 2)
+    xin = F.pad(x, (0, w % 2, 0, h % 2)) if odd else x
+    a = F.leaky_relu(xin, LRELU)
+    skip = x if odd else a
+    d = F.conv2d(a, st[p + "1.weight"], None, 2, 1)
+    if level == num_downs - 1:  # innermost: no down-norm (STCGAN/networks.py:118-124)
+        u = F.conv_transpose2d(F.relu(d), st[p + "3.weight"], None, 2, 1)
+        u = batch_norm(st, p + "4.", u, train)
+    else:
+        d = batch_norm(st, p + "2.", d, train)
+        c = _gen_block(st, d, level + 1, num_downs, train)
+        u = F.conv_transpose2d(F.relu(c), st[p + "5.weight"], None, 2, 1)
+        u = batch_norm(st, p + "6.", u, train)
+    if odd:
+        u = u[:, :, :h, :w]
+    return torch.cat([skip, u], 1)
+
+
+def generator_forward(st, x, train=True, num_downs=8):
+    """UnetGenerator.forward (STCGAN/networks.py:74-76, outermost block :111-117)."""
+    p = gen_block_prefix(0)
+    h = F.conv2d(x, st[p + "0.weight"], None, 2, 1)
+    c = _gen_block(st, h, 1, num_downs, train)
+    y = F.conv_transpose2d(F.relu(c), st[p + "3.weight"], st[p + "3.bias"], 2, 1)
+    return torch.tanh(y)
+
+
+def discriminator_forward(st, x, train=True, n_layers=3):
+    """NLayerDiscriminator.forward (STCGAN/networks.py:147-192), use_sigmoid=False."""
+    h = F.leaky_relu(F.conv2d(x, st["model.0.weight"], st["model.0.bias"], 2, 1), LRELU)
+    idx = 2
+    for n in range(1, n_layers + 1):
+        stride = 2 if n < n_layers else 1
+        h = F.conv2d(h, st[f"model.{idx}.weight"], None, stride, 1)
+        h = F.leaky_relu(batch_norm(st, f"model.{idx + 1}.", h, train), LRELU)
+        idx += 3
+    return F.conv2d(h, st[f"model.{idx}.weight"], st[f"model.{idx}.bias"], 1, 1)
+
+
+# --------------------------------------------------------------------------- losses
+def data_loss(pred, target):
+    """DataLoss: F.l1_loss(..., 'mean') (STCGAN/loss.py:14-26)."""
+    return (pred - target).abs().mean()
+
+
+def adversarial_loss(d_out, is_real, ls=False):
+    """AdversarialLoss (STCGAN/loss.py:59-86).  ls=False -> labels 1/0, MSE;
+    ls=True -> labels 1/-1, BCE-with-logits (the branch the CLI never reaches)."""
+    if not ls:
+        t = 1.0 if is_real else 0.0
+        return ((d_out - t) ** 2).mean()
+    t = 1.0 if is_real else -1.0
+    # BCE with logits, numerically stable form: max(x,0) - x*t + log(1+exp(-|x|))
+    return (d_out.clamp(min=0) - d_out * t + torch.log1p(torch.exp(-d_out.abs()))).mean()
+
+
+# --------------------------------------------------------------------------- Adam
+class Adam:
+    """torch.optim.Adam (amsgrad=False, weight_decay=0, maximize=False) restated
+    element-wise: exp_avg.lerp_(g, 1-b1); exp_avg_sq = b2*v + (1-b2)*g*g;
+    p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)."""
+
+    def __init__(self, params, lr, betas=(0.5, 0.999), eps=1e-8):
+        self.params = list(params)
+        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+        self.state = [None] * len(self.params)
+        self.step_count = 0
+
+    def zero_grad(self):
+        for p in self.params:
+            p.grad = None
+
+    @torch.no_grad()
+    def step(self):
+        self.step_count += 1
+        bc1 = 1 - self.b1 ** self.step_count
+        bc2 = 1 - self.b2 ** self.step_count
+        step_size = self.lr / bc1
+        bc2_sqrt = bc2 ** 0.5
+        w = 1 - self.b1
+        for i, p in enumerate(self.params):
+            if p.grad is None:
+                continue
+            if self.state[i] is None:
+                self.state[i] = (torch.zeros_like(p), torch.zeros_like(p))
+            m, v = self.state[i]
+            g = p.grad
+            # torch.lerp: start + w*(end-start) if |w| < 0.5 else end - (end-start)*(1-w)
+            if abs(w) < 0.5:
+                m.add_(w * (g - m))
+            else:
+                m.copy_(g - (g - m) * (1 - w))
+            v.mul_(self.b2).add_((1 - self.b2) * g * g)
+            denom = v.sqrt() / bc2_sqrt + self.eps
+            p.add_(-step_size * (m / denom))
+
+
+# --------------------------------------------------------------------------- trainer
+class OracleSTCGAN:
+    """Functional restatement of STCGAN.run_epoch (STCGAN/stcgan.py:186-330)."""
+
+    def __init__(self, states, lr_G=5e-5, lr_D=2e-5, betas=(0.5, 0.999), loss_type="normal", ls=False):
+        self.st = states  # {"G1":…, "G2":…, "D1":…, "D2":…}; float tensors are leaf params
+        for s in self.st.values():
+            for k, v in s.items():
+                if v.is_floating_point() and not _is_buffer(k):
+                    v.requires_grad_(True)
+        self.optim_G = Adam(self._params("G1") + self._params("G2"), lr_G, betas)
+        self.optim_D = Adam(self._params("D1") + self._params("D2"), lr_D, betas)
+        self.loss_type = loss_type
+        self.ls = ls
+        self.lambda1, self.lambda2, self.lambda3 = 5, 0.1, 0.1  # STCGAN/stcgan.py:117-119
+
+    def _params(self, name):
+        return [v for k, v in self.st[name].items() if v.is_floating_point() and not _is_buffer(k)]
+
+    def G(self, name, x, train):
+        return generator_forward(self.st[name], x, train)
+
+    def D(self, name, x, train):
+        return discriminator_forward(self.st[name], x, train)
+
+    def adv(self, out, is_real):
+        return adversarial_loss(out, is_real, self.ls)
+
+    def d_losses(self, c1r, c1f, c2r, c2f):
+        adv, t = self.adv, self.loss_type
+        if t == "normal":
+            d1 = (adv(c1f, False) + adv(c1r, True)) * 0.5
+            d2 = (adv(c2f, False) + adv(c2r, True)) * 0.5
+        elif t == "rel":
+            d1 = adv(c1r - c1f, True)
+            d2 = adv(c2r - c2f, True)
+        else:
+            d1 = (adv(c1f - c1r.mean(dim=0), False) + adv(c1r - c1f.mean(dim=0), True)) * 0.5
+            d2 = (adv(c2f - c2r.mean(dim=0), False) + adv(c2r - c2f.mean(dim=0), True)) * 0.5
+        return d1, d2
+
+    def g_losses(self, c1r, c1f, c2r, c2f):
+        adv, t = self.adv, self.loss_type
+        if t == "normal":
+            return adv(c1f, True), adv(c2f, True)
+        if t == "rel":
+            return adv(c1f - c1r, True), adv(c2f - c2r, True)
+        g1 = (adv(c1f - c1r.mean(dim=0), True) + adv(c1r - c1f.mean(dim=0), False)) * 0.5
+        # the reference's rel_avg G2 loss uses the D1 outputs (STCGAN/stcgan.py:286-290)
+        g2 = (adv(c1f - c1r.mean(dim=0), True) + adv(c1r - c1f.mean(dim=0), False)) * 0.5
+        return g1, g2
+
+    def run_epoch(self, batches, training=True):
+        loss = dict.fromkeys(["G", "D", "D1", "D2", "G1", "G2", "data1", "data2"], 0.0)
+        d1_out = dict.fromkeys(["real", "fake"], 0.0)
+        d2_out = dict.fromkeys(["real", "fake"], 0.0)
+        tr = training
+        for (_, x, m, y) in batches:
+            self.optim_D.zero_grad()
+            self.optim_G.zero_grad()
+            with torch.set_grad_enabled(training):
+                c1r = self.D("D1", torch.cat((x, m), 1), tr)
+                m_pred = self.G("G1", x, tr)
+                c1f = self.D("D1", torch.cat((x, m_pred.detach()), 1), tr)
+                c2r = self.D("D2", torch.cat((x, m, y), 1), tr)
+                y_pred = self.G("G2", torch.cat((x, m_pred), 1), tr)
+                c2f = self.D("D2", torch.cat((x, m_pred.detach(), y_pred.detach()), 1), tr)
+                d1, d2 = self.d_losses(c1r, c1f, c2r, c2f)
+                d_loss = self.lambda2 * d1 + self.lambda3 * d2
+                if training:
+                    d_loss.backward()
+                    self.optim_D.step()
+                d1_out["real"] += float(c1r.detach().mean())
+                d1_out["fake"] += float(c1f.detach().mean())
+                d2_out["real"] += float(c2r.detach().mean())
+                d2_out["fake"] += float(c2f.detach().mean())
+                loss["D1"] += float(d1.detach())
+                loss["D2"] += float(d2.detach())
+                loss["D"] += float(d_loss.detach())
+                self.optim_G.zero_grad()
+                # D.requires_grad_(False): D param grads are not produced in the G step
+                for name in ("D1", "D2"):
+                    for p in self._params(name):
+                        p.requires_grad_(False)
+                if training:
+                    c1r = self.D("D1", torch.cat((x, m), 1), tr)
+                    c1f = self.D("D1", torch.cat((x, m_pred), 1), tr)
+                    c2r = self.D("D2", torch.cat((x, m, y), 1), tr)
+                    c2f = self.D("D2", torch.cat((x, m_pred, y_pred), 1), tr)
+                g1, g2 = self.g_losses(c1r, c1f, c2r, c2f)
+                data1 = data_loss(m_pred, m)
+                data2 = data_loss(y_pred, y)
+                g_loss = data1 + self.lambda1 * data2 + self.lambda2 * g1 + self.lambda3 * g2
+                if training:
+                    g_loss.backward()
+                    self.optim_G.step()
+                for name in ("D1", "D2"):
+                    for p in self._params(name):
+                        p.requires_grad_(True)
+                loss["G1"] += float(g1.detach())
+                loss["G2"] += float(g2.detach())
+                loss["data1"] += float(data1.detach())
+                loss["data2"] += float(data2.detach())
+                loss["G"] += float(g_loss.detach())
+        loss["total"] = loss["G"] * 0.8 + loss["D"] * 0.2
+        n = len(batches)
+        for dct in (loss, d1_out, d2_out):
+            for k in dct:
+                dct[k] /= n
+        return {"Loss": loss, "D1_out": d1_out, "D2_out": d2_out}
+
+
+def _is_buffer(key):
+    return key.endswith(("running_mean", "running_var", "num_batches_tracked"))

@@ -1,0 +1,164 @@
+"""Pin the CPU oracle (oracle/stcgan_ref.py) against golden vectors produced by
+running the reference itself (tests/golden/make_goldens.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from fixture_init import compare, fixture_state, normal, pm_one, state_checksum, uniform
+from oracle import stcgan_ref as ref
+
+NET_IN = {"G1": 3, "G2": 4, "D1": 4, "D2": 7}
+NET_SEED = {"G1": 11, "G2": 12, "D1": 13, "D2": 14}
+
+
+def template(name, ngf):
+    if name == "G1":
+        return ref.generator_state_template(3, 1, ngf)
+    if name == "G2":
+        return ref.generator_state_template(4, 3, ngf)
+    return ref.discriminator_state_template(NET_IN[name], ngf)
+
+
+def forward(name, st, x, train):
+    if name.startswith("G"):
+        return ref.generator_forward(st, x, train)
+    return ref.discriminator_forward(st, x, train)
+
+
+def test_state_templates_match_reference_keys(golden):
+    d = golden("run_epoch_ngf8.npz")
+    for name in ["G1", "G2", "D1", "D2"]:
+        keys = [k[len(f"normal/state/{name}/"):] for k in d if k.startswith(f"normal/state/{name}/")]
+        keys = sorted({k.split("::")[0] for k in keys})
+        assert keys == sorted(template(name, 8).keys())
+
+
+@pytest.mark.parametrize("name", ["G1", "G2", "D1", "D2"])
+def test_oracle_nets_ngf8(golden, name):
+    torch.set_num_threads(8)
+    d = golden("nets_ngf8.npz")
+    bs, hw = int(d["meta/bs"]), int(d["meta/hw"])
+    st = fixture_state(template(name, 8), NET_SEED[name], "one")
+    assert abs(state_checksum(st) - float(d[f"{name}/checksum"])) < 1e-6
+    params = {k: v.clone().requires_grad_(not ref._is_buffer(k) and v.is_floating_point())
+              for k, v in st.items()}
+    x = uniform((bs, NET_IN[name], hw, hw), 100 + NET_SEED[name]).requires_grad_(True)
+    out = forward(name, params, x, True)
+    r = normal(tuple(out.shape), 200 + NET_SEED[name])
+    (out * r).sum().backward()
+    compare(d, f"{name}/train_out", out, atol=2e-5)
+    compare(d, f"{name}/input_grad", x.grad, atol=1e-5, rtol=1e-3)
+    for k, p in params.items():
+        if p.requires_grad:
+            compare(d, f"{name}/grad/{k}", p.grad, atol=1e-4, rtol=1e-3)
+        else:
+            compare(d, f"{name}/buf_after_train/{k}", p, atol=1e-5)
+    st2 = fixture_state(template(name, 8), NET_SEED[name], "one")
+    with torch.no_grad():
+        compare(d, f"{name}/eval_out", forward(name, st2, x.detach(), False), atol=2e-5)
+
+
+def synth_batches(n, bs, hw, seed):
+    out = []
+    for i in range(n):
+        s = seed + 10 * i
+        out.append(([], uniform((bs, 3, hw, hw), s), pm_one((bs, 1, hw, hw), s + 1),
+                    uniform((bs, 3, hw, hw), s + 2)))
+    return out
+
+
+@pytest.mark.parametrize("loss_type", ["one_iter", "normal", "rel", "rel_avg"])
+def test_oracle_run_epoch(golden, loss_type):
+    """One iteration: post-Adam state within 1e-7.  Two iterations: Adam's
+    second step divides a near-cancelling first moment by sqrt(v), which
+    amplifies 1e-6-relative gradient differences into up to ~half an lr step
+    on a few percent of the elements, so state there is checked to 1 lr step
+    (lr_G = 5e-5) and the loss values to 1e-4 relative."""
+    torch.set_num_threads(8)
+    d = golden("run_epoch_ngf8.npz")
+    ngf, bs, hw = int(d["meta/ngf"]), int(d["meta/bs"]), int(d["meta/hw"])
+    batches = synth_batches(int(d["meta/n_iter"]), bs, hw, int(d["meta/batch_seed"]))
+    one = loss_type == "one_iter"
+    if one:
+        batches = batches[:1]
+    states = {n: fixture_state(template(n, ngf), NET_SEED[n], "ref") for n in ["G1", "G2", "D1", "D2"]}
+    tr = ref.OracleSTCGAN(states, loss_type="normal" if one else loss_type)
+    meas = tr.run_epoch(batches, training=True)
+    for grp, vals in meas.items():
+        for k, v in vals.items():
+            want = float(d[f"{loss_type}/measures/{grp}/{k}"])
+            assert abs(v - want) <= 1e-5 + 1e-4 * abs(want), (grp, k, v, want)
+    for n in ["G1", "G2", "D1", "D2"]:
+        for k, v in states[n].items():
+            if one:
+                compare(d, f"{loss_type}/state/{n}/{k}", v.detach(), atol=1e-7, rtol=1e-5)
+            else:
+                compare(d, f"{loss_type}/state/{n}/{k}", v.detach(), atol=5e-5, rtol=1e-4)
+    meas = tr.run_epoch(batches, training=False)
+    for grp, vals in meas.items():
+        for k, v in vals.items():
+            want = float(d[f"{loss_type}/valid_measures/{grp}/{k}"])
+            assert abs(v - want) <= 1e-5 + 1e-4 * abs(want), (grp, k, v, want)
+
+
+@pytest.mark.parametrize("name", ["G1", "G2"])
+def test_oracle_ngf64(golden, name):
+    torch.set_num_threads(8)
+    d = golden("g_ngf64.npz")
+    st = fixture_state(template(name, 64), NET_SEED[name], "one")
+    assert abs(state_checksum(st) - float(d[f"{name}/checksum"])) < 1e-6 * float(d[f"{name}/checksum"])
+    x = uniform((1, NET_IN[name], 256, 256), 300 + NET_SEED[name])
+    with torch.no_grad():
+        out = ref.generator_forward(st, x, True)
+        np.testing.assert_allclose(out.numpy(), d[f"{name}/train_out"], atol=2e-5)
+        st = fixture_state(template(name, 64), NET_SEED[name], "one")
+        out = ref.generator_forward(st, x, False)
+        np.testing.assert_allclose(out.numpy(), d[f"{name}/eval_out"], atol=2e-5)
+
+
+def istd_input(d):
+    f = d["shadow_bgr_u8"].astype(np.float32) / 255
+    f = (f - 0.5) * 2
+    return torch.from_numpy(np.ascontiguousarray(f.transpose(2, 0, 1)))[None]
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_oracle_istd_480x640(golden, train):
+    """Odd-size pad/crop semantics (src/models/stcgan_g.py:120-132) at native resolution."""
+    torch.set_num_threads(8)
+    d = golden("istd_114_5.npz")
+    x = istd_input(d)
+    g1 = fixture_state(template("G1", 64), NET_SEED["G1"], "one")
+    g2 = fixture_state(template("G2", 64), NET_SEED["G2"], "one")
+    with torch.no_grad():
+        m = ref.generator_forward(g1, x, train)
+        y = ref.generator_forward(g2, torch.cat((x, m), 1), train)
+    key = "full_train" if train else "full"
+    np.testing.assert_allclose(m.numpy(), d[f"{key}/m_pred"], atol=5e-5)
+    np.testing.assert_allclose(y.numpy(), d[f"{key}/y_pred"], atol=5e-5)
+
+
+def test_oracle_istd_crop(golden):
+    torch.set_num_threads(8)
+    d = golden("istd_114_5.npz")
+    r0, c0 = (int(v) for v in d["crop/r0c0"])
+    x = istd_input(d)[:, :, r0:r0 + 256, c0:c0 + 256].contiguous()
+    g1 = fixture_state(template("G1", 64), NET_SEED["G1"], "one")
+    g2 = fixture_state(template("G2", 64), NET_SEED["G2"], "one")
+    with torch.no_grad():
+        m = ref.generator_forward(g1, x, False)
+        y = ref.generator_forward(g2, torch.cat((x, m), 1), False)
+    np.testing.assert_allclose(m.numpy(), d["crop/m_pred"], atol=2e-5)
+    np.testing.assert_allclose(y.numpy(), d["crop/y_pred"], atol=2e-5)
+
+
+def test_oracle_losses_match_torch():
+    x = normal((2, 1, 30, 30), 1)
+    for is_real in (True, False):
+        t = torch.full_like(x, 1.0 if is_real else 0.0)
+        assert torch.allclose(ref.adversarial_loss(x, is_real), torch.nn.functional.mse_loss(x, t))
+        t = torch.full_like(x, 1.0 if is_real else -1.0)
+        assert torch.allclose(ref.adversarial_loss(x, is_real, ls=True),
+                              torch.nn.functional.binary_cross_entropy_with_logits(x, t), atol=1e-6)
+    y = normal((2, 3, 8, 8), 2)
+    assert torch.allclose(ref.data_loss(x[:, :, :8, :8], y[:, :1]), torch.nn.functional.l1_loss(x[:, :, :8, :8], y[:, :1]))
