@@ -1,0 +1,184 @@
+#!/usr/bin/env python
+"""ST-CGAN train-step benchmark on MI355X (BASELINE.json metric).
+
+A "step" is one full ST-CGAN training iteration (STCGAN.run_epoch body,
+STCGAN/stcgan.py:208-312): 6 network forwards + D backward + Adam(D), then 4
+discriminator forwards + G backward + Adam(G), on a resident synthetic batch of
+256x256 triplets (x, y ~ U(-1,1), m = +-1), batch 32 per GPU (BASELINE config 3/4).
+Multi-GPU: one process per GPU (torchrun), batch sharded (32 per rank, weak
+scaling), RCCL all-reduce of the G/D gradients.
+
+Prints ONE JSON line on rank 0 (see the driver contract in the task statement).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "shadow-removal-istd_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "ST-CGAN train images/s at 256×256 bs=32, 1/2/4/8 MI355X; G2 max-abs vs CPU"
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2516.0}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+
+
+def gen_fwd_flops(in_c, out_c, ngf, B, H, W, num_downs=8):
+    """Algorithmic FLOPs (2*MAC) of one U-Net generator forward (real channels, no padding)."""
+    co = [ngf * min(2 ** k, 8) for k in range(num_downs)]
+    S = [(H, W), (H // 2, W // 2)]
+    for _ in range(2, num_downs + 1):
+        S.append(((S[-1][0] + 1) // 2, (S[-1][1] + 1) // 2))
+    f = 0
+    for k in range(num_downs):
+        cin = in_c if k == 0 else co[k - 1]
+        f += 2 * B * S[k + 1][0] * S[k + 1][1] * co[k] * 16 * cin
+    for k in range(num_downs):
+        cin = co[k] if k == num_downs - 1 else 2 * co[k]
+        cout = out_c if k == 0 else co[k - 1]
+        f += 2 * B * (2 * S[k + 1][0]) * (2 * S[k + 1][1]) * cout * 4 * cin
+    return f
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="per-GPU batch")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--ngf", type=int, default=64)
+    ap.add_argument("--dtype", default=os.environ.get("STC_BENCH_DTYPE", "fp32"), choices=["fp32", "bf16"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-iters", type=int, default=2)
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The CPU oracle (oracle/stcgan_ref.py, a torch-CPU restatement of the reference
+    run_epoch, parity-pinned by tests/golden) timed on this host's cores."""
+    from oracle import stcgan_ref as ref
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from fixture_init import fixture_state, pm_one, uniform
+    try:
+        ncores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncores = os.cpu_count() or 1
+    threads = max(1, min(16, ncores))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    ngf, bs, s = args.ngf, args.cpu_batch, args.size
+    states = {
+        "G1": fixture_state(ref.generator_state_template(3, 1, ngf), 11, "ref"),
+        "G2": fixture_state(ref.generator_state_template(4, 3, ngf), 12, "ref"),
+        "D1": fixture_state(ref.discriminator_state_template(4, ngf), 13, "ref"),
+        "D2": fixture_state(ref.discriminator_state_template(7, ngf), 14, "ref"),
+    }
+    tr = ref.OracleSTCGAN(states)
+    batch = [([], uniform((bs, 3, s, s), 1), pm_one((bs, 1, s, s), 2), uniform((bs, 3, s, s), 3))]
+    tr.run_epoch(batch)  # warm-up iteration
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_iters):
+        tr.run_epoch(batch)
+    dt = time.perf_counter() - t0
+    torch.set_num_threads(prev)
+    return {"value": round(bs * args.cpu_iters / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle run_epoch (full D+G train step, fp32, ngf={ngf}) at batch {bs} {s}x{s}, "
+                      f"{args.cpu_iters} timed iterations after 1 warm-up ({dt:.1f} s)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import types
+    from stcgan_amd.stcgan import STCGAN
+
+    a = types.SimpleNamespace(devices=[f"cuda:{local}"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5,
+                              beta2=0.999, D_loss_fn="standard", D_loss_type="normal", ngf=args.ngf,
+                              dtype=args.dtype, load_weights_g1=None, load_weights_g2=None,
+                              load_weights_d1=None, load_weights_d2=None)
+    torch.manual_seed(1234 + rank)
+    tr = STCGAN(a)
+    dev = torch.device("cuda", local)
+    B, s = args.batch, args.size
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    x = torch.rand((B, 3, s, s), generator=g, device=dev) * 2 - 1
+    m = (torch.rand((B, 1, s, s), generator=g, device=dev) < 0.5).float() * 2 - 1
+    y = torch.rand((B, 3, s, s), generator=g, device=dev) * 2 - 1
+    for net in (tr.G1, tr.G2, tr.D1, tr.D2):
+        net.train()
+
+    for _ in range(args.warmup):
+        tr.train_step(x, m, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_step(x, m, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+
+    # ---- roofline of the north-star kernel set: G1+G2 forward (train-mode BN), HIP events on our stream
+    flops = gen_fwd_flops(3, 1, args.ngf, B, s, s) + gen_fwd_flops(4, 3, args.ngf, B, s, s)
+    with torch.no_grad():
+        for _ in range(2):
+            mp = tr.G1(x)
+            tr.G2([x, mp])
+        reps = 5
+        st = torch.cuda.current_stream()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(st)
+        for _ in range(reps):
+            mp = tr.G1(x)
+            tr.G2([x, mp])
+        ev1.record(st)
+        ev1.synchronize()
+        fwd_ms = ev0.elapsed_time(ev1) / reps
+    achieved = flops / (fwd_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel": f"G1+G2 forward (all conv/convT igemm + BN kernels), batch {B}, {flops / 1e9:.2f} GFLOP "
+                          f"per launch set, {fwd_ms:.3f} ms"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+               "data": "synthetic (x,y~U(-1,1), m=+-1; reference weights_init)",
+               "config": {"workload": "full ST-CGAN train step (G1,G2,D1,D2 fwd/bwd + MSE-cGAN/L1 + Adam), "
+                                      f"{s}x{s}", "global_batch": B * world, "per_gpu_batch": B,
+                          "image_size": s, "ngf": args.ngf, "parallelism": f"dp{world}"},
+               "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

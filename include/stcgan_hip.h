@@ -1,0 +1,188 @@
+/*
+ * stcgan_hip.h -- C-ABI of the MI355X (gfx950) ST-CGAN hot-path library
+ * (libstcgan_hip.so, built from the .hip sources in shadow-removal-istd_amd/csrc).
+ *
+ * The reference (nhchiu/Shadow-Removal-ISTD) has no native boundary: its hot
+ * path is torch.nn modules running on cuDNN/ATen.  Each entry
+ * point below replaces one implicit vendor kernel family on that path and
+ * names the reference call site it serves:
+ *
+ *   stc_conv_fwd     Conv2d 4x4 s2/s1 p1 forward     STCGAN/networks.py:104-105,156-157,167-169,176-178,183-184
+ *                    ConvTranspose2d 4x4 s2 p1 fwd   STCGAN/networks.py:112-114,119-121,126-128
+ *                    and both layers' input gradient (conv dgrad == convT fwd geometry and vice versa)
+ *   stc_conv_wgrad   weight gradient of both         (autograd of the same lines)
+ *   stc_pack_weight  torch weight layout -> GEMM operand layout (per-op packing)
+ *   stc_chan_stats / stc_bn_finalize               BatchNorm2d train/eval forward, STCGAN/networks.py:107,109,170,179
+ *   stc_bn_bwd_reduce / stc_bn_bwd_apply            BatchNorm2d backward fused with LeakyReLU/ReLU backward
+ *                    (with mean == NULL: LeakyReLU(0.2)/ReLU backward alone, networks.py:106,108,158)
+ *   stc_tanh_bias_bwd Tanh backward + outermost ConvT bias grad (networks.py:112-116)
+ *   stc_gather_nchw / stc_scatter_nchw              torch.cat input concat (stcgan.py:219-227,269-272) / its backward
+ *   stc_loss_fwd / stc_loss_bwd                     DataLoss (L1) and AdversarialLoss (MSE / BCE-with-logits), loss.py:14-26,59-86
+ *   stc_adam_step    torch.optim.Adam                STCGAN/stcgan.py:60-65
+ *
+ * Conventions
+ *   - Activations are NHWC ("view" = base pointer + explicit strides, so a
+ *     channel slice of a concat buffer is addressed in place, zero-copy).
+ *   - The library never allocates device memory; all workspace comes from the
+ *     caller.  Every call enqueues on the given hipStream_t only.
+ *   - Every call returns 0 on success, or a non-zero code; stc_last_error()
+ *     returns a thread-local message.  No C++ exception crosses the ABI.
+ *   - dtype: STC_F32 = 0, STC_BF16 = 1 (activation / operand storage type;
+ *     accumulation, BN statistics and optimizer state are always fp32).
+ */
+#ifndef STCGAN_HIP_H
+#define STCGAN_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { STC_F32 = 0, STC_BF16 = 1 };
+
+/* 4-D NHWC tensor view: element (b, y, x, c) lives at
+ *   p + b*bs + y*rs + x*ps + (co + c)*cs                                    */
+typedef struct {
+  void* p;
+  int32_t H, W;   /* logical extent (bounds for reads / reductions)        */
+  int64_t bs;     /* batch stride, elements                                */
+  int64_t rs;     /* row stride, elements                                  */
+  int32_t ps;     /* pixel stride, elements                                */
+  int32_t co;     /* channel offset                                        */
+  int32_t cs;     /* channel stride (1 for NHWC, H*W for NCHW)             */
+  int32_t pad_;
+} stc_view;
+
+/* ---- implicit-GEMM convolution -------------------------------------------
+ * kind:
+ *   STC_CONV_S2  : Conv2d k4 s2 p1 forward           (also ConvT dgrad)
+ *   STC_CONV_S1  : Conv2d k4 s1 p1 forward
+ *   STC_CONVT_S2 : ConvTranspose2d k4 s2 p1 forward  (also Conv-s2 dgrad), 4 phases
+ *   STC_CONV_S1_DGRAD : input gradient of Conv2d k4 s1 p1
+ * The packed weight comes from stc_pack_weight with the matching pack mode.
+ * prologue (applied to every in-bounds input element before the product,
+ * zero padding stays zero): v = v*scale[c] + shift[c] (if scale != NULL),
+ * then v = v > 0 ? v : v*slope (if pro_act != 0).
+ * epilogue: + bias[n] (if bias != NULL), tanh (if epi_tanh).                */
+enum { STC_CONV_S2 = 0, STC_CONV_S1 = 1, STC_CONVT_S2 = 2, STC_CONV_S1_DGRAD = 3 };
+
+int stc_conv_fwd(int dtype, int kind, int B,
+                 stc_view x, int Cin,
+                 const float* pro_scale, const float* pro_shift, int pro_act, float pro_slope,
+                 const void* w_packed, int Cout,
+                 stc_view y,
+                 const float* bias, int epi_tanh, int out_f32,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Workspace bytes stc_conv_fwd needs for this problem (split-K slabs). */
+int64_t stc_conv_fwd_workspace(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout);
+
+/* ---- weight gradient ---------------------------------------------------------
+ * dW[r][ci][kh][kw] = sum_{b,oy,ox} D[b,oy,ox,r] * G[b, oy*s+kh-1, ox*s+kw-1, ci]
+ *   Conv2d s2/s1 : D = dy (grid = output), G = x (input), s = stride
+ *   ConvT s2     : D = x (grid = input),  G = dy (output), s = 2
+ * D grid is D.H x D.W; prologues (optional) apply to D and G like stc_conv_fwd.
+ * dW is written in torch layout [R][Cg_out][4][4] (fp32), Cg_out <= Cg.          */
+int stc_conv_wgrad(int dtype, int B, int stride,
+                   stc_view D, int R,
+                   const float* d_scale, const float* d_shift, int d_act, float d_slope,
+                   stc_view G, int Cg, int Cg_out,
+                   const float* g_scale, const float* g_shift, int g_act, float g_slope,
+                   float* dW, void* workspace, int64_t workspace_bytes, void* stream);
+int64_t stc_conv_wgrad_workspace(int dtype, int B, int Hd, int Wd, int R, int Cg);
+
+/* ---- weight packing ----------------------------------------------------------
+ * W is a torch weight [P][Q][4][4] fp32.  out is [phases][N_pad][T][C_pad] of dtype.
+ *   STC_PACK_CONV_FWD    : conv  W[co][ci] -> n=co, c=ci, 16 taps          (P=Cout,Q=Cin)
+ *   STC_PACK_CONV_DGRAD  : conv  W[co][ci] -> n=ci, c=co, 4 phases x 4 taps (convT geometry)
+ *   STC_PACK_CONV_S1_DGRAD: conv W[co][ci] -> n=ci, c=co, 16 taps
+ *   STC_PACK_CONVT_FWD   : convT W[ci][co] -> n=co, c=ci, 4 phases x 4 taps (P=Cin,Q=Cout)
+ *   STC_PACK_CONVT_DGRAD : convT W[ci][co] -> n=ci, c=co, 16 taps (conv-s2 geometry)      */
+enum { STC_PACK_CONV_FWD = 0, STC_PACK_CONV_DGRAD = 1, STC_PACK_CONV_S1_DGRAD = 2,
+       STC_PACK_CONVT_FWD = 3, STC_PACK_CONVT_DGRAD = 4 };
+int stc_pack_weight(int dtype, int mode, const float* W, int P, int Q,
+                    void* out, int N_pad, int C_pad, void* stream);
+
+/* ---- batch norm -------------------------------------------------------------
+ * stc_chan_stats: per-channel partial statistics of x over pixel chunks:
+ *   part[chunk][c] = {count, shifted sum, shifted sum of squares, shift}.
+ * stc_bn_finalize: combines partials (fixed order -> deterministic), writes
+ *   mean/rstd (train), the affine table scale/shift used as a consumer prologue
+ *   (scale = gamma*rstd, shift = beta - mean*scale), and updates running stats
+ *   (momentum, unbiased var) + num_batches_tracked.  With part == NULL (eval)
+ *   the table is built from the running statistics.                         */
+int stc_chan_stats(int dtype, int B, stc_view x, int C, float* part, int nchunks, void* stream);
+int stc_chan_stats_chunks(int B, int H, int W);
+/* out[c] = sum over pixels of x[..., c] for c < Cout (conv bias gradient), fixed order.
+ * part needs nchunks*C floats.                                               */
+int stc_chan_sum(int dtype, int B, stc_view x, int C, int Cout, float* part, int nchunks, float* out, void* stream);
+int stc_bn_finalize(const float* part, int nchunks, int C,
+                    const float* gamma, const float* beta,
+                    float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                    float momentum, float eps,
+                    float* mean, float* rstd, float* scale, float* shift, void* stream);
+
+/* BN backward fused with the activation backward of its consumers:
+ *   n  = x*scale + shift (the BN output; scale/shift from stc_bn_finalize)
+ *   dn = g1 * act1'(n) + g2 * act2'(n)   (g1/g2 optional; act' = 1 if n>0 else slope)
+ *   reduce: part2[chunk][c] = {sum dn, sum dn*xhat}
+ *   apply : dx = gamma*rstd*(dn - sum(dn)/P - xhat*sum(dn*xhat)/P); dgamma, dbeta.
+ * With mean == NULL the BN is absent (identity affine): apply writes dx = dn. */
+int stc_bn_bwd_reduce(int dtype, int B, stc_view x, int C,
+                      const float* scale, const float* shift, const float* mean, const float* rstd,
+                      stc_view g1, float slope1, stc_view g2, float slope2,
+                      float* part2, int nchunks, void* stream);
+int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C,
+                     const float* scale, const float* shift, const float* mean, const float* rstd,
+                     const float* gamma,
+                     stc_view g1, float slope1, stc_view g2, float slope2,
+                     const float* part2, int nchunks,
+                     stc_view dx, float* dgamma, float* dbeta, void* stream);
+
+/* y = tanh(q) stored NCHW fp32 (the generator output).  dq = gy*(1-y^2) into NHWC
+ * view dq; dbias[c] = sum dq (deterministic).                               */
+int stc_tanh_bias_bwd(int dtype, int B, int C, int H, int W, const float* y, const float* gy,
+                      stc_view dq, float* dbias, float* part, int nchunks, void* stream);
+
+/* ---- layout -------------------------------------------------------------------
+ * Gather up to 4 NCHW fp32 sources (channels concatenated, like torch.cat dim=1)
+ * into an NHWC view with Cpad channels (extra channels zero).               */
+int stc_gather_nchw(int dtype, int B, int H, int W, int nsrc, const float* const* src,
+                    const int* src_c, stc_view dst, int Cpad, void* stream);
+/* Scatter channel ranges of an NHWC view back to NCHW fp32 tensors (backward of the gather);
+ * dst pointers may be NULL to skip a source.                                */
+int stc_scatter_nchw(int dtype, int B, int H, int W, stc_view src, int nsrc, float* const* dst,
+                     const int* dst_c, void* stream);
+
+/* ---- losses ---------------------------------------------------------------------
+ * kind: STC_LOSS_L1 (|p - t|, t tensor), STC_LOSS_MSE_CONST ((p - c)^2),
+ *       STC_LOSS_BCE_CONST (BCE-with-logits vs constant label c).
+ * fwd: out[0] = mean loss (deterministic two-level reduction, part >= stc_loss_parts(n) floats).
+ * bwd: grad = gout[0] * dloss/dp (gout is a device scalar).                  */
+enum { STC_LOSS_L1 = 0, STC_LOSS_MSE_CONST = 1, STC_LOSS_BCE_CONST = 2 };
+int stc_loss_parts(int64_t n);
+int stc_loss_fwd(int kind, const float* p, const float* t, float c, int64_t n,
+                 float* part, float* out, void* stream);
+int stc_loss_bwd(int kind, const float* p, const float* t, float c, int64_t n,
+                 const float* gout, float* grad, void* stream);
+
+/* ---- optimizer --------------------------------------------------------------------
+ * One launch over many tensors.  table: device array of ntensors records
+ * {param*, grad*, exp_avg*, exp_avg_sq*, numel, first_block} (6 x int64), where
+ * first_block is the prefix sum of ceil(numel / stc_adam_elems_per_block()) and
+ * total_blocks the grand total.  torch.optim.Adam semantics (amsgrad=False,
+ * weight_decay=0): exp_avg.lerp_(g, 1-b1); exp_avg_sq = b2*v + (1-b2)*g*g;
+ * p += -(lr/bc1) * exp_avg / (sqrt(exp_avg_sq)/sqrt(bc2) + eps).              */
+int stc_adam_step(const int64_t* table, int ntensors, int64_t total_blocks,
+                  float lr, float beta1, float beta2, float eps, int step, void* stream);
+int stc_adam_elems_per_block(void);
+
+/* ---- misc ------------------------------------------------------------------------ */
+const char* stc_last_error(void);
+int stc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STCGAN_HIP_H */

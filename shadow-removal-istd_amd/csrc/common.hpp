@@ -1,0 +1,104 @@
+// Shared device/host helpers for the gfx950 ST-CGAN kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <string>
+#include <cstdio>
+#include <cstdarg>
+
+#include "../../include/stcgan_hip.h"
+
+namespace stc {
+
+using bf16 = __hip_bfloat16;
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+
+#define STC_CHECK_LAUNCH()                                                     \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess)                                                      \
+      return ::stc::fail((int)e_, "%s: launch failed: %s", __func__,          \
+                         hipGetErrorString(e_));                               \
+  } while (0)
+
+#define STC_REQUIRE(cond, ...)                                                 \
+  do {                                                                         \
+    if (!(cond)) return ::stc::fail(-1, __VA_ARGS__);                          \
+  } while (0)
+
+// ---------------------------------------------------------------- bf16 helpers
+__device__ __forceinline__ float bf2f(unsigned short u) {
+  return __uint_as_float(((unsigned)u) << 16);
+}
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  // round-to-nearest-even; NaN kept NaN by the hardware convert
+  bf16 b = __float2bfloat16(f);
+  return *reinterpret_cast<unsigned short*>(&b);
+}
+
+// 4 consecutive elements <-> float4
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  __device__ __forceinline__ static float4 load(const float* p) {
+    return *reinterpret_cast<const float4*>(p);
+  }
+  __device__ __forceinline__ static void store(float* p, float4 v) {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+};
+template <> struct Vec4<bf16> {
+  __device__ __forceinline__ static float4 load(const bf16* p) {
+    uint2 u = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+  }
+  __device__ __forceinline__ static void store(bf16* p, float4 v) {
+    uint2 u;
+    u.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
+    u.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
+    *reinterpret_cast<uint2*>(p) = u;
+  }
+};
+
+template <typename T> __device__ __forceinline__ float ld1(const T* p);
+template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld1<bf16>(const bf16* p) {
+  return bf2f(*reinterpret_cast<const unsigned short*>(p));
+}
+template <typename T> __device__ __forceinline__ void st1(T* p, float v);
+template <> __device__ __forceinline__ void st1<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st1<bf16>(bf16* p, float v) {
+  *reinterpret_cast<unsigned short*>(p) = f2bf(v);
+}
+
+// ---------------------------------------------------------------- views
+struct View {  // device-side copy of stc_view
+  char* p;
+  int H, W;
+  long long bs, rs;
+  int ps, co, cs;
+};
+static inline View mkview(const stc_view& v) {
+  View r;
+  r.p = (char*)v.p; r.H = v.H; r.W = v.W; r.bs = v.bs; r.rs = v.rs;
+  r.ps = v.ps; r.co = v.co; r.cs = v.cs;
+  return r;
+}
+__device__ __forceinline__ long long vidx(const View& v, int b, int y, int x, int c) {
+  return (long long)b * v.bs + (long long)y * v.rs + (long long)x * v.ps + (long long)(v.co + c) * v.cs;
+}
+
+__device__ __forceinline__ float act(float v, float slope) { return v > 0.f ? v : v * slope; }
+__device__ __forceinline__ float dact(float n, float slope) { return n > 0.f ? 1.f : slope; }
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace stc

@@ -1,0 +1,277 @@
+// Layout edges, Tanh/bias backward, losses and the weight packer.
+//   gather/scatter : torch.cat((x, m, ...), 1) of the D/G inputs (STCGAN/stcgan.py:219-227,
+//                    269-272) fused with the NCHW->NHWC edge conversion (and its backward)
+//   tanh_bias_bwd  : outermost Tanh + ConvT bias (STCGAN/networks.py:112-116) backward
+//   losses         : DataLoss = F.l1_loss (STCGAN/loss.py:14-26); AdversarialLoss =
+//                    F.mse_loss vs 1/0 or BCE-with-logits vs 1/-1 (STCGAN/loss.py:59-86)
+//   pack_weight    : torch weight [P][Q][4][4] -> GEMM operand [phase][N][tap][C]
+#include "common.hpp"
+
+namespace stc {
+
+// ------------------------------------------------------------------ gather / scatter
+struct Src4 {
+  const float* p[4];
+  int c[4];
+};
+struct Dst4 {
+  float* p[4];
+  int c[4];
+};
+
+template <typename T>
+__global__ void gather_kernel(int B, int H, int W, int nsrc, Src4 s, View d, int Cpad) {
+  const long long HW = (long long)H * W, P = HW * B;
+  for (long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x; pix < P;
+       pix += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(pix / HW);
+    const long long hw = pix % HW;
+    const int y = (int)(hw / W), x = (int)(hw % W);
+    T* out = reinterpret_cast<T*>(d.p) + vidx(d, b, y, x, 0);
+    int c = 0;
+    for (int k = 0; k < nsrc; ++k) {
+      const float* src = s.p[k] + (long long)b * s.c[k] * HW + hw;
+      for (int j = 0; j < s.c[k]; ++j, ++c) st1<T>(out + (long long)c * d.cs, src[(long long)j * HW]);
+    }
+    for (; c < Cpad; ++c) st1<T>(out + (long long)c * d.cs, 0.f);
+  }
+}
+
+template <typename T>
+__global__ void scatter_kernel(int B, int H, int W, View s, int nsrc, Dst4 d) {
+  const long long HW = (long long)H * W, P = HW * B;
+  for (long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x; pix < P;
+       pix += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(pix / HW);
+    const long long hw = pix % HW;
+    const int y = (int)(hw / W), x = (int)(hw % W);
+    const T* in = reinterpret_cast<const T*>(s.p) + vidx(s, b, y, x, 0);
+    int c = 0;
+    for (int k = 0; k < nsrc; ++k) {
+      float* dst = d.p[k] ? d.p[k] + (long long)b * d.c[k] * HW + hw : nullptr;
+      for (int j = 0; j < d.c[k]; ++j, ++c)
+        if (dst) dst[(long long)j * HW] = ld1<T>(in + (long long)c * s.cs);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ tanh + bias backward
+// dq[b,y,x,c] = gy*(1-y^2) for c < C, 0 for C <= c < Cpad (dq view has Cpad channels);
+// part[chunk][c] = sum over the chunk's pixels of dq (c < C)
+template <typename T>
+__global__ void tanh_bwd_kernel(int B, int C, int H, int W, const float* y, const float* gy, View dq, int Cpad,
+                                float* part, int nchunks) {
+  const long long HW = (long long)H * W, P = HW * B;
+  const long long per = (P + nchunks - 1) / nchunks;
+  const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
+  float acc[4] = {0, 0, 0, 0};
+  for (long long pix = p0 + threadIdx.x; pix < p1; pix += blockDim.x) {
+    const int b = (int)(pix / HW);
+    const long long hw = pix % HW;
+    const int yy = (int)(hw / W), xx = (int)(hw % W);
+    T* out = reinterpret_cast<T*>(dq.p) + vidx(dq, b, yy, xx, 0);
+    for (int c = 0; c < Cpad; ++c) {
+      float v = 0.f;
+      if (c < C) {
+        const long long i = ((long long)b * C + c) * HW + hw;
+        const float t = y[i];
+        v = gy[i] * (1.f - t * t);
+        acc[c] += v;
+      }
+      st1<T>(out + (long long)c * dq.cs, v);
+    }
+  }
+  __shared__ float red[4][256];
+  for (int c = 0; c < 4; ++c) red[c][threadIdx.x] = acc[c];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s)
+      for (int c = 0; c < 4; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x < C) part[(long long)blockIdx.x * C + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void chunk_sum_kernel(const float* part, int nchunks, int C, float* out) {
+  const int c = blockIdx.x;
+  __shared__ double s[256];
+  double a = 0;
+  for (int k = threadIdx.x; k < nchunks; k += 256) a += part[(long long)k * C + c];
+  s[threadIdx.x] = a;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) s[threadIdx.x] += s[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[c] = (float)s[0];
+}
+
+// ------------------------------------------------------------------ losses
+constexpr int LOSS_BLOCK = 256, LOSS_PER_BLOCK = 256 * 16;
+
+__device__ __forceinline__ float loss_elem(int kind, float p, float t) {
+  if (kind == STC_LOSS_L1) return fabsf(p - t);
+  if (kind == STC_LOSS_MSE_CONST) { const float d = p - t; return d * d; }
+  // BCE with logits: max(x,0) - x*t + log1p(exp(-|x|))
+  return fmaxf(p, 0.f) - p * t + log1pf(expf(-fabsf(p)));
+}
+__device__ __forceinline__ float loss_grad(int kind, float p, float t) {
+  if (kind == STC_LOSS_L1) { const float d = p - t; return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
+  if (kind == STC_LOSS_MSE_CONST) return 2.f * (p - t);
+  const float s = 1.f / (1.f + expf(-p));
+  return s - t;
+}
+
+__global__ void loss_partial_kernel(int kind, const float* p, const float* t, float c, long long n, float* part) {
+  const long long b0 = (long long)blockIdx.x * LOSS_PER_BLOCK;
+  float acc = 0.f;
+  for (int k = 0; k < 16; ++k) {
+    const long long i = b0 + k * LOSS_BLOCK + threadIdx.x;
+    if (i < n) acc += loss_elem(kind, p[i], t ? t[i] : c);
+  }
+  __shared__ float red[LOSS_BLOCK];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = LOSS_BLOCK / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void loss_final_kernel(const float* part, int nparts, long long n, float* out) {
+  __shared__ double red[256];
+  double a = 0;
+  for (int k = threadIdx.x; k < nparts; k += 256) a += part[k];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)(red[0] / (double)n);
+}
+
+__global__ void loss_bwd_kernel(int kind, const float* p, const float* t, float c, long long n, const float* gout,
+                                float* grad) {
+  const float g = gout[0] / (float)n;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    grad[i] = g * loss_grad(kind, p[i], t ? t[i] : c);
+}
+
+// ------------------------------------------------------------------ weight packing
+template <typename T>
+__global__ void pack_kernel(int mode, const float* W, int P, int Q, T* out, int N_pad, int C_pad, int nph, int taps) {
+  const long long total = (long long)nph * N_pad * taps * C_pad;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % C_pad);
+    long long r = idx / C_pad;
+    const int t = (int)(r % taps);
+    r /= taps;
+    const int n = (int)(r % N_pad);
+    const int z = (int)(r / N_pad);
+    int kh, kw;
+    if (taps == 16) { kh = t >> 2; kw = t & 3; }
+    else { const int ph = z >> 1, pw = z & 1; kh = (1 - ph) + 2 * (t >> 1); kw = (1 - pw) + 2 * (t & 1); }
+    const bool n_is_p = (mode == STC_PACK_CONV_FWD || mode == STC_PACK_CONVT_DGRAD);
+    const int pi = n_is_p ? n : c, qi = n_is_p ? c : n;
+    float v = 0.f;
+    if (pi < P && qi < Q) v = W[(((long long)pi * Q + qi) * 4 + kh) * 4 + kw];
+    st1<T>(out + idx, v);
+  }
+}
+
+static int grid_for(long long work) { return (int)std::max<long long>(1, std::min<long long>((work + 255) / 256, 8192)); }
+
+}  // namespace stc
+
+using namespace stc;
+
+extern "C" int stc_gather_nchw(int dtype, int B, int H, int W, int nsrc, const float* const* src, const int* src_c,
+                               stc_view dst, int Cpad, void* stream) {
+  STC_REQUIRE(nsrc >= 1 && nsrc <= 4, "stc_gather_nchw: 1..4 sources");
+  Src4 s{};
+  int tot = 0;
+  for (int k = 0; k < nsrc; ++k) { s.p[k] = src[k]; s.c[k] = src_c[k]; tot += src_c[k]; }
+  STC_REQUIRE(tot <= Cpad, "stc_gather_nchw: %d channels > Cpad %d", tot, Cpad);
+  hipStream_t st = (hipStream_t)stream;
+  const long long P = (long long)B * H * W;
+  View d = mkview(dst);
+  if (dtype == STC_F32) hipLaunchKernelGGL(gather_kernel<float>, dim3(grid_for(P)), dim3(256), 0, st, B, H, W, nsrc, s, d, Cpad);
+  else hipLaunchKernelGGL(gather_kernel<bf16>, dim3(grid_for(P)), dim3(256), 0, st, B, H, W, nsrc, s, d, Cpad);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_scatter_nchw(int dtype, int B, int H, int W, stc_view src, int nsrc, float* const* dst,
+                                const int* dst_c, void* stream) {
+  STC_REQUIRE(nsrc >= 1 && nsrc <= 4, "stc_scatter_nchw: 1..4 destinations");
+  Dst4 d{};
+  for (int k = 0; k < nsrc; ++k) { d.p[k] = dst[k]; d.c[k] = dst_c[k]; }
+  hipStream_t st = (hipStream_t)stream;
+  const long long P = (long long)B * H * W;
+  View s = mkview(src);
+  if (dtype == STC_F32) hipLaunchKernelGGL(scatter_kernel<float>, dim3(grid_for(P)), dim3(256), 0, st, B, H, W, s, nsrc, d);
+  else hipLaunchKernelGGL(scatter_kernel<bf16>, dim3(grid_for(P)), dim3(256), 0, st, B, H, W, s, nsrc, d);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_tanh_bias_bwd(int dtype, int B, int C, int H, int W, const float* y, const float* gy, stc_view dq,
+                                 float* dbias, float* part, int nchunks, void* stream) {
+  STC_REQUIRE(C >= 1 && C <= 4, "stc_tanh_bias_bwd: C=%d", C);
+  hipStream_t st = (hipStream_t)stream;
+  const int Cpad = dtype == STC_F32 ? 4 : 8;
+  View d = mkview(dq);
+  if (dtype == STC_F32)
+    hipLaunchKernelGGL(tanh_bwd_kernel<float>, dim3(nchunks), dim3(256), 0, st, B, C, H, W, y, gy, d, Cpad, part, nchunks);
+  else
+    hipLaunchKernelGGL(tanh_bwd_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, B, C, H, W, y, gy, d, Cpad, part, nchunks);
+  STC_CHECK_LAUNCH();
+  if (dbias) {
+    hipLaunchKernelGGL(chunk_sum_kernel, dim3(C), dim3(256), 0, st, (const float*)part, nchunks, C, dbias);
+    STC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int stc_loss_parts(int64_t n) { return (int)((n + LOSS_PER_BLOCK - 1) / LOSS_PER_BLOCK); }
+
+extern "C" int stc_loss_fwd(int kind, const float* p, const float* t, float c, int64_t n, float* part, float* out,
+                            void* stream) {
+  STC_REQUIRE(kind >= 0 && kind <= 2, "stc_loss_fwd: bad kind");
+  STC_REQUIRE(n > 0, "stc_loss_fwd: empty input");
+  STC_REQUIRE(kind != STC_LOSS_L1 || t != nullptr, "stc_loss_fwd: L1 needs a target tensor");
+  hipStream_t st = (hipStream_t)stream;
+  const int np = stc_loss_parts(n);
+  hipLaunchKernelGGL(loss_partial_kernel, dim3(np), dim3(LOSS_BLOCK), 0, st, kind, p, t, c, (long long)n, part);
+  STC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, (const float*)part, np, (long long)n, out);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_loss_bwd(int kind, const float* p, const float* t, float c, int64_t n, const float* gout,
+                            float* grad, void* stream) {
+  STC_REQUIRE(kind >= 0 && kind <= 2, "stc_loss_bwd: bad kind");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, kind, p, t, c, (long long)n, gout, grad);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_pack_weight(int dtype, int mode, const float* W, int P, int Q, void* out, int N_pad, int C_pad,
+                               void* stream) {
+  STC_REQUIRE(mode >= 0 && mode <= 4, "stc_pack_weight: bad mode");
+  const bool phased = mode == STC_PACK_CONV_DGRAD || mode == STC_PACK_CONVT_FWD;
+  const int nph = phased ? 4 : 1, taps = phased ? 4 : 16;
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)nph * N_pad * taps * C_pad;
+  if (dtype == STC_F32)
+    hipLaunchKernelGGL(pack_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, mode, W, P, Q, (float*)out, N_pad, C_pad, nph, taps);
+  else
+    hipLaunchKernelGGL(pack_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, mode, W, P, Q, (bf16*)out, N_pad, C_pad, nph, taps);
+  STC_CHECK_LAUNCH();
+  return 0;
+}

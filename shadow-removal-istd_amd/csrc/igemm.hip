@@ -1,0 +1,495 @@
+// Implicit-GEMM 4x4 convolution family on gfx950 MFMA.
+//
+// One kernel template serves every forward product on the ST-CGAN path and
+// both input gradients:
+//   Conv2d k4 s2/s1 p1           : M = B*Ho*Wo, N = Cout, K = 16*Cin
+//   ConvTranspose2d k4 s2 p1     : 4 sub-pixel phases, each M = B*Hi*Wi, N = Cout, K = 4*Cin
+//   Conv-s2 dgrad == ConvT fwd geometry, ConvT dgrad == Conv-s2 geometry, Conv-s1 dgrad (flipped taps)
+// A (activations, NHWC) is gathered on the fly: row m -> (b, y, x), k -> (tap, ci);
+// tap offsets are affine in the tap index, so one parameter set describes every case.
+// A per-channel affine + leaky prologue applies BatchNorm-apply and LeakyReLU/ReLU of
+// the *producer* while loading (zero padding stays zero), so normalised activations
+// are never materialised in HBM.
+//
+// Tile: BM x BN x (128 bytes of K) per stage, 256 threads = 4 waves, each wave a
+// (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA blocks.  LDS rows are 128 B of K plus
+// 16 B of pad (144 B stride): the 16-lane groups of ds_read_b128 then hit 16
+// distinct 16-byte bank slots (conflict-free).  fp32 uses v_mfma_f32_32x32x2_f32
+// (4 MFMAs per 16-byte fragment, exact fp32 fmaf chains), bf16 uses
+// v_mfma_f32_32x32x16_bf16 (1 MFMA per fragment); both read the same LDS image.
+// Register-staged double buffer: the global loads of K-step s+1 are in flight
+// while step s runs on MFMA; one barrier per step.
+#include "common.hpp"
+
+namespace stc {
+
+struct ConvParams {
+  const char* a;
+  long long a_bs, a_rs;
+  int a_ps, a_co;
+  int IH, IW;
+  int lg_cin, lg_tw, in_stride;
+  int offy[4], offx[4];
+  int stepy, stepx;
+  const float* sc;
+  const float* sh;
+  int pro_act;
+  float slope;
+  int GH, GW, M, N, K;
+  int ksplit, kchunk;
+  const char* b;
+  long long b_phase_stride;
+  char* c;
+  long long c_bs, c_rs;
+  int c_ps, c_co, c_cs;
+  int os;
+  int oy0[4], ox0[4];
+  const float* bias;
+  int tanh_, out_f32;
+  float* ws;
+  int nphase;
+  int mtiles, ntiles;
+};
+
+constexpr int LDS_ROW = 144;  // 128 B of K + 16 B pad
+
+template <typename T>
+__device__ __forceinline__ uint4 prologue16(uint4 v, const float* sc, const float* sh, int ci,
+                                            int act_on, float slope) {
+  constexpr int VEC = 16 / sizeof(T);
+  float f[VEC];
+  if constexpr (sizeof(T) == 4) {
+    f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y);
+    f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+  } else {
+    unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f[2 * q] = __uint_as_float(w[q] << 16);
+      f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  }
+  if (sc) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) f[e] = fmaf(f[e], sc[ci + e], sh[ci + e]);
+  }
+  if (act_on) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) f[e] = f[e] > 0.f ? f[e] : f[e] * slope;
+  }
+  uint4 r;
+  if constexpr (sizeof(T) == 4) {
+    r.x = __float_as_uint(f[0]); r.y = __float_as_uint(f[1]);
+    r.z = __float_as_uint(f[2]); r.w = __float_as_uint(f[3]);
+  } else {
+    unsigned w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      w[q] = (unsigned)f2bf(f[2 * q]) | ((unsigned)f2bf(f[2 * q + 1]) << 16);
+    r.x = w[0]; r.y = w[1]; r.z = w[2]; r.w = w[3];
+  }
+  return r;
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256)
+igemm_kernel(const ConvParams p) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int BK = 128 / sizeof(T);
+  constexpr int AIT = BM / 32;  // 16-byte chunks per thread for A (8 chunks per row)
+  constexpr int BIT = BN / 32;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 32, FN = WTN / 32;
+  constexpr int STAGE = (BM + BN) * LDS_ROW;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(FM >= 1 && FN >= 1, "wave tile >= 32x32");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  long long* rowoff = reinterpret_cast<long long*>(smem + 2 * STAGE);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // XCD-aware bijective remap of the flat tile id: consecutive tiles (sharing A rows)
+  // land on the same XCD's L2.
+  const int nwg = p.mtiles * p.ntiles;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int mt = bid / p.ntiles, nt = bid % p.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int z = blockIdx.z;
+  const int ph = z / p.ksplit, split = z % p.ksplit;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nsteps = (kend - kbeg) / BK;
+  const int GHW = p.GH * p.GW;
+  const int offy = p.offy[ph], offx = p.offx[ph];
+  const int cin_mask = (1 << p.lg_cin) - 1;
+  const int tw_mask = (1 << p.lg_tw) - 1;
+
+  // ---- per-thread A row info
+  const int ca = tid & 7;
+  long long abase[AIT];
+  int ayy[AIT], axx[AIT];
+#pragma unroll
+  for (int i = 0; i < AIT; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    if (m < p.M) {
+      const int b = m / GHW, rem = m - b * GHW;
+      const int y = rem / p.GW, x = rem - y * p.GW;
+      abase[i] = (long long)b * p.a_bs + p.a_co;
+      ayy[i] = y * p.in_stride + offy;
+      axx[i] = x * p.in_stride + offx;
+    } else {
+      abase[i] = 0;
+      ayy[i] = -100000;  // always out of bounds
+      axx[i] = -100000;
+    }
+  }
+  // ---- per-thread B row info
+  const T* bptr[BIT];
+  bool bval[BIT];
+#pragma unroll
+  for (int j = 0; j < BIT; ++j) {
+    const int n = n0 + (tid >> 3) + 32 * j;
+    bval[j] = n < p.N;
+    bptr[j] = reinterpret_cast<const T*>(p.b) + p.b_phase_stride * ph + (long long)(bval[j] ? n : 0) * p.K + ca * VEC;
+  }
+  // ---- output row offsets (direct epilogue)
+  if (!p.ws) {
+    for (int r = tid; r < BM; r += 256) {
+      const int m = m0 + r;
+      long long off = -1;
+      if (m < p.M) {
+        const int b = m / GHW, rem = m - b * GHW;
+        const int y = rem / p.GW, x = rem - y * p.GW;
+        const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+        off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps;
+      }
+      rowoff[r] = off;
+    }
+  }
+
+  uint4 ra[AIT], rb[BIT];
+  const T* abase_ptr = reinterpret_cast<const T*>(p.a);
+  const bool has_pro = p.sc != nullptr || p.pro_act != 0;
+  unsigned amask = 0;  // which A chunks were in bounds (prologue must not touch padding)
+  int aci = 0;         // channel of this thread's chunk in the staged K-step
+
+  // Issue the global loads of one K-step; nothing consumes them until store_lds,
+  // so their latency hides under the MFMAs of the current step.
+  auto load_regs = [&](int k0) {
+    const int k = k0 + ca * VEC;
+    const int t = k >> p.lg_cin, ci = k & cin_mask;
+    const int dy = p.stepy * (t >> p.lg_tw), dx = p.stepx * (t & tw_mask);
+    aci = ci;
+    amask = 0;
+#pragma unroll
+    for (int i = 0; i < AIT; ++i) {
+      const int iy = ayy[i] + dy, ix = axx[i] + dx;
+      if ((unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) {
+        const T* src = abase_ptr + abase[i] + (long long)iy * p.a_rs + (long long)ix * p.a_ps + ci;
+        ra[i] = *reinterpret_cast<const uint4*>(src);
+        amask |= 1u << i;
+      } else {
+        ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BIT; ++j) {
+      rb[j] = bval[j] ? *reinterpret_cast<const uint4*>(bptr[j] + k0) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_lds = [&](int stage) {
+    char* sA = smem + stage * STAGE;
+    char* sB = sA + BM * LDS_ROW;
+#pragma unroll
+    for (int i = 0; i < AIT; ++i) {
+      uint4 v = ra[i];
+      if (has_pro && (amask >> i & 1u)) v = prologue16<T>(v, p.sc, p.sh, aci, p.pro_act, p.slope);
+      *reinterpret_cast<uint4*>(sA + ((tid >> 3) + 32 * i) * LDS_ROW + ca * 16) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < BIT; ++j)
+      *reinterpret_cast<uint4*>(sB + ((tid >> 3) + 32 * j) * LDS_ROW + ca * 16) = rb[j];
+  };
+
+  floatx16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (nsteps > 0) {
+    load_regs(kbeg);
+    store_lds(0);
+  }
+  __syncthreads();
+
+  const int lrow = lane & 31, lhalf = lane >> 5;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) load_regs(kbeg + (s + 1) * BK);
+    const char* sA = smem + cur * STAGE;
+    const char* sB = sA + BM * LDS_ROW;
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) {
+      const int coff = (2 * kc + lhalf) * 16;
+      uint4 fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        fa[i] = *reinterpret_cast<const uint4*>(sA + (wm * WTM + 32 * i + lrow) * LDS_ROW + coff);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        fb[j] = *reinterpret_cast<const uint4*>(sB + (wn * WTN + 32 * j + lrow) * LDS_ROW + coff);
+      if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const float av = __uint_as_float(e == 0 ? fa[i].x : e == 1 ? fa[i].y : e == 2 ? fa[i].z : fa[i].w);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              const float bv = __uint_as_float(e == 0 ? fb[j].x : e == 1 ? fb[j].y : e == 2 ? fb[j].z : fb[j].w);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+            }
+          }
+        }
+      } else {
+        typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const bf16x8 av = __builtin_bit_cast(bf16x8, fa[i]);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const bf16x8 bv = __builtin_bit_cast(bf16x8, fb[j]);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (s + 1 < nsteps) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue
+  if (p.ws) {
+    float* slab = p.ws + (long long)z * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WTN + 32 * j + lrow;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * WTM + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * lhalf;
+          if (m < p.M) slab[(long long)m * p.N + n] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WTN + 32 * j + lrow;
+    if (n >= p.N) continue;
+    const float bz = p.bias ? p.bias[n] : 0.f;
+    const long long coff = (long long)(p.c_co + n) * p.c_cs;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = wm * WTM + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * lhalf;
+        const long long ro = rowoff[r];
+        if (ro < 0) continue;
+        float v = acc[i][j][e] + bz;
+        if (p.tanh_) v = tanhf(v);
+        if (p.out_f32) reinterpret_cast<float*>(p.c)[ro + coff] = v;
+        else st1<T>(reinterpret_cast<T*>(p.c) + ro + coff, v);
+      }
+    }
+  }
+}
+
+// Split-K / raw-slab reduction with the epilogue: out[m, n] = epi(sum_s ws[ph][s][m][n])
+template <typename T>
+__global__ void splitk_reduce_kernel(const ConvParams p) {
+  const long long total = (long long)p.nphase * p.M * p.N;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(idx % p.N);
+    const long long pm = idx / p.N;
+    const int m = (int)(pm % p.M);
+    const int ph = (int)(pm / p.M);
+    const float* src = p.ws + ((long long)ph * p.ksplit * p.M + m) * p.N + n;
+    float v = 0.f;
+    for (int s = 0; s < p.ksplit; ++s) v += src[(long long)s * p.M * p.N];
+    if (p.bias) v += p.bias[n];
+    if (p.tanh_) v = tanhf(v);
+    const int GHW = p.GH * p.GW;
+    const int b = m / GHW, rem = m - b * GHW;
+    const int y = rem / p.GW, x = rem - y * p.GW;
+    const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+    const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps +
+                          (long long)(p.c_co + n) * p.c_cs;
+    if (p.out_f32) reinterpret_cast<float*>(p.c)[off] = v;
+    else st1<T>(reinterpret_cast<T*>(p.c) + off, v);
+  }
+}
+
+// ------------------------------------------------------------------------- host
+struct Geometry {
+  int taps_lg_tw;   // lg of taps per row (2 -> 4x4 taps, 1 -> 2x2 taps)
+  int in_stride, os, nphase;
+  int offy[4], offx[4];
+  int stepy, stepx;
+};
+
+static Geometry geometry(int kind) {
+  Geometry g{};
+  switch (kind) {
+    case STC_CONV_S2:
+    case STC_CONV_S1:
+      g.taps_lg_tw = 2; g.in_stride = kind == STC_CONV_S2 ? 2 : 1; g.os = 1; g.nphase = 1;
+      g.offy[0] = -1; g.offx[0] = -1; g.stepy = 1; g.stepx = 1;
+      break;
+    case STC_CONV_S1_DGRAD:  // dx[i] = sum_k dy[i + 1 - k] w[k]
+      g.taps_lg_tw = 2; g.in_stride = 1; g.os = 1; g.nphase = 1;
+      g.offy[0] = 1; g.offx[0] = 1; g.stepy = -1; g.stepx = -1;
+      break;
+    case STC_CONVT_S2:  // out(2y+ph) = sum_t in(y + ph - t) w[(1-ph) + 2t]
+      g.taps_lg_tw = 1; g.in_stride = 1; g.os = 2; g.nphase = 4;
+      for (int z = 0; z < 4; ++z) { g.offy[z] = z >> 1; g.offx[z] = z & 1; }
+      g.stepy = -1; g.stepx = -1;
+      break;
+  }
+  return g;
+}
+
+static int ilog2_exact(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+struct Plan {
+  int BM, BN, ksplit, kchunk, mtiles, ntiles;
+};
+
+static Plan plan_for(int dtype, int M, int N, int K, int nphase) {
+  const int BK = dtype == STC_F32 ? 32 : 64;
+  Plan pl{};
+  if (N <= 32) { pl.BM = 128; pl.BN = 32; }
+  else if (N <= 64) { pl.BM = 128; pl.BN = 64; }
+  else { pl.BM = 128; pl.BN = 128; }
+  if (M <= 64 && N >= 128) { pl.BM = 32; pl.BN = 128; }
+  else if (M <= 512 && N >= 64) { pl.BM = 64; pl.BN = 64; }
+  pl.mtiles = cdiv(M, pl.BM);
+  pl.ntiles = cdiv(N, pl.BN);
+  const long long tiles = (long long)pl.mtiles * pl.ntiles * nphase;
+  const int ksteps = K / BK;
+  int ks = 1;
+  // split K until the grid covers the chip (~2 waves of 256 CUs), keeping >= 4 K-steps per split
+  while (tiles * ks < 512 && ks * 2 <= 64 && ksteps / (ks * 2) >= 4) ks *= 2;
+  pl.ksplit = ks;
+  pl.kchunk = cdiv(ksteps, ks) * BK;
+  pl.ksplit = cdiv(K, pl.kchunk);
+  return pl;
+}
+
+static size_t lds_bytes(int BM, int BN) { return 2 * (size_t)(BM + BN) * LDS_ROW + BM * 8; }
+
+template <typename T>
+static int launch_igemm(const Plan& pl, ConvParams& p, hipStream_t st) {
+  dim3 grid(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
+  const size_t lds = lds_bytes(pl.BM, pl.BN);
+#define STC_L(BM_, BN_, WM_, WN_)                                                          \
+  if (pl.BM == BM_ && pl.BN == BN_) {                                                      \
+    hipLaunchKernelGGL((igemm_kernel<T, BM_, BN_, WM_, WN_>), grid, dim3(256), lds, st, p); \
+  } else
+  STC_L(128, 128, 2, 2)
+  STC_L(128, 64, 2, 2)
+  STC_L(128, 32, 4, 1)
+  STC_L(64, 64, 2, 2)
+  STC_L(32, 128, 1, 4)
+  { return fail(-1, "igemm: no kernel for tile %dx%d", pl.BM, pl.BN); }
+#undef STC_L
+  STC_CHECK_LAUNCH();
+  if (p.ws) {
+    const long long total = (long long)p.nphase * p.M * p.N;
+    const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(blocks), dim3(256), 0, st, p);
+    STC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // namespace stc
+
+using namespace stc;
+
+extern "C" int64_t stc_conv_fwd_workspace(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout) {
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  const int M = B * Hg * Wg, K = taps * Cin;
+  const Plan pl = plan_for(dtype, M, Cout, K, g.nphase);
+  if (pl.ksplit <= 1) return 0;
+  return (int64_t)g.nphase * pl.ksplit * (int64_t)M * Cout * 4;
+}
+
+extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
+                            const float* pro_scale, const float* pro_shift, int pro_act, float pro_slope,
+                            const void* w_packed, int Cout, stc_view y,
+                            const float* bias, int epi_tanh, int out_f32,
+                            void* workspace, int64_t workspace_bytes, void* stream) {
+  STC_REQUIRE(dtype == STC_F32 || dtype == STC_BF16, "stc_conv_fwd: bad dtype %d", dtype);
+  STC_REQUIRE(kind >= 0 && kind <= 3, "stc_conv_fwd: bad kind %d", kind);
+  const int VEC = dtype == STC_F32 ? 4 : 8;
+  const int BK = dtype == STC_F32 ? 32 : 64;
+  const int lg = ilog2_exact(Cin);
+  STC_REQUIRE(lg >= 0 && Cin >= VEC, "stc_conv_fwd: Cin=%d must be a power of two >= %d", Cin, VEC);
+  STC_REQUIRE(x.co % VEC == 0 && x.ps % VEC == 0 && x.cs == 1, "stc_conv_fwd: input view must be NHWC, 16-byte aligned channels");
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  const int K = taps * Cin;
+  STC_REQUIRE(K % BK == 0, "stc_conv_fwd: K=%d not a multiple of %d", K, BK);
+  // GEMM grid: conv kinds -> output grid; convT -> input grid
+  int GH, GW;
+  if (kind == STC_CONVT_S2) { GH = x.H; GW = x.W; }
+  else { GH = y.H; GW = y.W; }
+  ConvParams p{};
+  p.a = (const char*)x.p; p.a_bs = x.bs; p.a_rs = x.rs; p.a_ps = x.ps; p.a_co = x.co;
+  p.IH = x.H; p.IW = x.W;
+  p.lg_cin = lg; p.lg_tw = g.taps_lg_tw; p.in_stride = g.in_stride;
+  for (int i = 0; i < 4; ++i) { p.offy[i] = g.offy[i]; p.offx[i] = g.offx[i]; }
+  p.stepy = g.stepy; p.stepx = g.stepx;
+  p.sc = pro_scale; p.sh = pro_shift; p.pro_act = pro_act; p.slope = pro_slope;
+  STC_REQUIRE((pro_scale == nullptr) == (pro_shift == nullptr), "stc_conv_fwd: scale/shift must come together");
+  p.GH = GH; p.GW = GW; p.M = B * GH * GW; p.N = Cout; p.K = K;
+  p.b = (const char*)w_packed;
+  p.b_phase_stride = (long long)Cout * K;
+  p.c = (char*)y.p; p.c_bs = y.bs; p.c_rs = y.rs; p.c_ps = y.ps; p.c_co = y.co; p.c_cs = y.cs;
+  p.os = g.os;
+  for (int i = 0; i < 4; ++i) { p.oy0[i] = g.nphase == 4 ? (i >> 1) : 0; p.ox0[i] = g.nphase == 4 ? (i & 1) : 0; }
+  p.bias = bias; p.tanh_ = epi_tanh; p.out_f32 = out_f32 || dtype == STC_F32;
+  p.nphase = g.nphase;
+  if (p.M == 0 || Cout == 0) return 0;
+  const Plan pl = plan_for(dtype, p.M, Cout, K, g.nphase);
+  p.ksplit = pl.ksplit; p.kchunk = pl.kchunk; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles;
+  if (pl.ksplit > 1) {
+    const int64_t need = (int64_t)g.nphase * pl.ksplit * (int64_t)p.M * Cout * 4;
+    STC_REQUIRE(workspace && workspace_bytes >= need, "stc_conv_fwd: workspace %lld < %lld bytes",
+                (long long)workspace_bytes, (long long)need);
+    p.ws = (float*)workspace;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == STC_F32) return launch_igemm<float>(pl, p, st);
+  return launch_igemm<bf16>(pl, p, st);
+}

@@ -1,0 +1,115 @@
+"""ctypes binding of libstcgan_hip.so (C-ABI: include/stcgan_hip.h).
+
+The library is built in-tree (``shadow-removal-istd_amd/csrc/Makefile``) and
+loaded from this directory.  There is no fallback: if the library is missing
+or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libstcgan_hip.so")
+
+F32, BF16 = 0, 1
+CONV_S2, CONV_S1, CONVT_S2, CONV_S1_DGRAD = 0, 1, 2, 3
+PACK_CONV_FWD, PACK_CONV_DGRAD, PACK_CONV_S1_DGRAD, PACK_CONVT_FWD, PACK_CONVT_DGRAD = 0, 1, 2, 3, 4
+LOSS_L1, LOSS_MSE_CONST, LOSS_BCE_CONST = 0, 1, 2
+
+
+class View(ctypes.Structure):
+    """stc_view: element (b, y, x, c) at p + b*bs + y*rs + x*ps + (co + c)*cs."""
+    _fields_ = [("p", ctypes.c_void_p), ("H", ctypes.c_int32), ("W", ctypes.c_int32),
+                ("bs", ctypes.c_int64), ("rs", ctypes.c_int64), ("ps", ctypes.c_int32),
+                ("co", ctypes.c_int32), ("cs", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+NULL_VIEW = View(None, 0, 0, 0, 0, 0, 0, 1, 0)
+
+_vp, _i32, _i64, _f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+
+# name: (restype, argtypes)
+_SIGS = {
+    "stc_conv_fwd": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, _vp, _i32, View, _vp, _i32, _i32,
+                            _vp, _i64, _vp]),
+    "stc_conv_fwd_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32, _i32]),
+    "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
+                              _f32, _vp, _vp, _i64, _vp]),
+    "stc_conv_wgrad_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32]),
+    "stc_pack_weight": (_i32, [_i32, _i32, _vp, _i32, _i32, _vp, _i32, _i32, _vp]),
+    "stc_chan_stats": (_i32, [_i32, _i32, View, _i32, _vp, _i32, _vp]),
+    "stc_chan_stats_chunks": (_i32, [_i32, _i32, _i32]),
+    "stc_chan_sum": (_i32, [_i32, _i32, View, _i32, _i32, _vp, _i32, _vp, _vp]),
+    "stc_bn_finalize": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp]),
+    "stc_bn_bwd_reduce": (_i32, [_i32, _i32, View, _i32, _vp, _vp, _vp, _vp, View, _f32, View, _f32, _vp, _i32,
+                                 _vp]),
+    "stc_bn_bwd_apply": (_i32, [_i32, _i32, View, _i32, _vp, _vp, _vp, _vp, _vp, View, _f32, View, _f32, _vp, _i32,
+                                View, _vp, _vp, _vp]),
+    "stc_tanh_bias_bwd": (_i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, View, _vp, _vp, _i32, _vp]),
+    "stc_gather_nchw": (_i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, View, _i32, _vp]),
+    "stc_scatter_nchw": (_i32, [_i32, _i32, _i32, _i32, View, _i32, _vp, _vp, _vp]),
+    "stc_loss_parts": (_i32, [_i64]),
+    "stc_loss_fwd": (_i32, [_i32, _vp, _vp, _f32, _i64, _vp, _vp, _vp]),
+    "stc_loss_bwd": (_i32, [_i32, _vp, _vp, _f32, _i64, _vp, _vp, _vp]),
+    "stc_adam_step": (_i32, [_vp, _i32, _i64, _f32, _f32, _f32, _f32, _i32, _vp]),
+    "stc_adam_elems_per_block": (_i32, []),
+    "stc_last_error": (ctypes.c_char_p, []),
+    "stc_version": (_i32, []),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def lib():
+    """Load the library once; raise loudly if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"stcgan_amd: HIP library not built ({LIB_PATH}); run __graft_entry__.build()")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().stc_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (rc={rc}): {msg}")
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise ValueError(f"unsupported dtype {dt}")
+
+
+def nhwc_view(t, c0=0, H=None, W=None):
+    """View of a contiguous NHWC tensor [B, Ha, Wa, C] (channel offset c0, logical H x W)."""
+    assert t.dim() == 4 and t.is_contiguous()
+    _, Ha, Wa, C = t.shape
+    return View(t.data_ptr(), Ha if H is None else H, Wa if W is None else W,
+                Ha * Wa * C, Wa * C, C, c0, 1, 0)
+
+
+def nchw_view(t):
+    """View of a contiguous NCHW tensor [B, C, H, W]."""
+    assert t.dim() == 4 and t.is_contiguous()
+    _, C, H, W = t.shape
+    return View(t.data_ptr(), H, W, C * H * W, W, 1, 0, H * W, 0)

@@ -1,0 +1,207 @@
+"""Thin tensor-level wrappers over the C-ABI (include/stcgan_hip.h).
+
+Every function here enqueues HIP kernels of libstcgan_hip.so on torch's current
+stream; torch is used only for device memory (caching allocator) and streams.
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+from ._lib import check, lib, ptr, stream
+
+LRELU = 0.2
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+def vec(dt):
+    """Elements per 16-byte chunk for the activation dtype."""
+    return 4 if dt == torch.float32 else 8
+
+
+def pad_channels(c, dt):
+    """Smallest power of two >= max(c, vec(dt))."""
+    p = vec(dt)
+    while p < c:
+        p *= 2
+    return p
+
+
+def _ws(nbytes, device):
+    if nbytes <= 0:
+        return None, 0
+    return torch.empty(int(nbytes), dtype=torch.uint8, device=device), int(nbytes)
+
+
+def _pro(pro):
+    if pro is None:
+        return None, None
+    sc, sh = pro
+    return ptr(sc), ptr(sh)
+
+
+def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=None, tanh=False, out_f32=False,
+         grid_hw=None):
+    """Implicit-GEMM conv family (stc_conv_fwd).  ``grid_hw`` = GEMM grid (defaults from the views)."""
+    dev = w_packed.device
+    if kind == L.CONVT_S2:
+        gh, gw = xv.H, xv.W
+    else:
+        gh, gw = yv.H, yv.W
+    l = lib()
+    nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
+    ws, nb = _ws(nbytes, dev)
+    sc, sh = _pro(pro)
+    rc = l.stc_conv_fwd(L.dtype_code(dt), kind, B, xv, cin, sc, sh, 0 if slope is None else 1,
+                        0.0 if slope is None else float(slope), ptr(w_packed), cout, yv, ptr(bias), int(tanh),
+                        int(out_f32), ptr(ws), nb, stream())
+    check(rc, "stc_conv_fwd")
+
+
+def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None):
+    """Weight gradient [R][Cg_out][4][4] fp32 (stc_conv_wgrad)."""
+    l = lib()
+    nbytes = l.stc_conv_wgrad_workspace(L.dtype_code(dt), B, Dv.H, Dv.W, R, Cg)
+    ws, nb = _ws(nbytes, device)
+    dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)
+    dsc, dsh = _pro(dpro)
+    gsc, gsh = _pro(gpro)
+    rc = l.stc_conv_wgrad(L.dtype_code(dt), B, stride, Dv, R, dsc, dsh, 0 if dslope is None else 1,
+                          0.0 if dslope is None else float(dslope), Gv, Cg, Cg_out, gsc, gsh,
+                          0 if gslope is None else 1, 0.0 if gslope is None else float(gslope), ptr(dW), ptr(ws), nb,
+                          stream())
+    check(rc, "stc_conv_wgrad")
+    return dW
+
+
+_PHASED = {L.PACK_CONV_DGRAD, L.PACK_CONVT_FWD}
+
+
+def pack(mode, W, n_pad, c_pad, dt):
+    """Pack a torch weight [P][Q][4][4] into the GEMM operand layout [phases][n_pad][taps][c_pad]."""
+    P, Q = W.shape[0], W.shape[1]
+    nph, taps = (4, 4) if mode in _PHASED else (1, 16)
+    out = torch.empty((nph, n_pad, taps, c_pad), dtype=dt, device=W.device)
+    Wc = W.detach()
+    if not Wc.is_contiguous():
+        Wc = Wc.contiguous()
+    check(lib().stc_pack_weight(L.dtype_code(dt), mode, ptr(Wc), P, Q, ptr(out), n_pad, c_pad, stream()),
+          "stc_pack_weight")
+    return out
+
+
+# generation counter bumped by our optimizer (it updates parameters in place behind autograd's back)
+_GEN = {}
+
+
+def bump(params):
+    for p in params:
+        _GEN[id(p)] = _GEN.get(id(p), 0) + 1
+
+
+def packed(cache, W, mode, n_pad, c_pad, dt):
+    """Cached packed weight; repacked when the parameter changed (version or optimizer step)."""
+    key = (id(W), mode, n_pad, c_pad, dt)
+    ver = (W._version, _GEN.get(id(W), 0), W.data_ptr())
+    hit = cache.get(key)
+    if hit is not None and hit[0] == ver:
+        return hit[1]
+    t = pack(mode, W, n_pad, c_pad, dt)
+    cache[key] = (ver, t)
+    return t
+
+
+def stats_chunks(B, H, W):
+    return lib().stc_chan_stats_chunks(B, H, W)
+
+
+def bn_train_table(B, xv, C, dt, bn, scale_out, shift_out, update_running=True):
+    """Batch statistics of x (view, C channels) -> (mean, rstd); writes the prologue table
+    scale_out/shift_out (views of C floats) and updates bn's running statistics."""
+    dev = scale_out.device
+    nch = stats_chunks(B, xv.H, xv.W)
+    part = torch.empty((nch, C, 4), dtype=torch.float32, device=dev)
+    check(lib().stc_chan_stats(L.dtype_code(dt), B, xv, C, ptr(part), nch, stream()), "stc_chan_stats")
+    mean = torch.empty(C, dtype=torch.float32, device=dev)
+    rstd = torch.empty(C, dtype=torch.float32, device=dev)
+    rm = bn.running_mean if update_running else None
+    rv = bn.running_var if update_running else None
+    nbt = bn.num_batches_tracked if update_running else None
+    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+    check(lib().stc_bn_finalize(ptr(part), nch, C, ptr(bn.weight), ptr(bn.bias), ptr(rm), ptr(rv), ptr(nbt),
+                                float(mom), float(bn.eps), ptr(mean), ptr(rstd), ptr(scale_out), ptr(shift_out),
+                                stream()), "stc_bn_finalize")
+    return mean, rstd
+
+
+def bn_eval_table(C, bn, scale_out, shift_out):
+    check(lib().stc_bn_finalize(None, 0, C, ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
+                                ptr(bn.running_var), None, 0.0, float(bn.eps), None, None, ptr(scale_out),
+                                ptr(shift_out), stream()), "stc_bn_finalize(eval)")
+
+
+def bn_backward(B, xv, C, dt, dxv, g1=None, s1=0.0, g2=None, s2=0.0, bn_state=None):
+    """Fused activation + BatchNorm backward.  bn_state = (scale, shift, mean, rstd, gamma) or None
+    (no BN: dx = g1*act1'(x) + g2*act2'(x)).  Returns (dgamma, dbeta) or (None, None)."""
+    l = lib()
+    g1v = g1 if g1 is not None else L.NULL_VIEW
+    g2v = g2 if g2 is not None else L.NULL_VIEW
+    dev_t = None
+    if bn_state is None:
+        check(l.stc_bn_bwd_apply(L.dtype_code(dt), B, xv, C, None, None, None, None, None, g1v, float(s1), g2v,
+                                 float(s2), None, 0, dxv, None, None, stream()), "stc_bn_bwd_apply")
+        return None, None
+    scale, shift, mean, rstd, gamma = bn_state
+    dev_t = scale.device
+    nch = stats_chunks(B, xv.H, xv.W)
+    part = torch.empty((nch, C, 2), dtype=torch.float32, device=dev_t)
+    check(l.stc_bn_bwd_reduce(L.dtype_code(dt), B, xv, C, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), g1v,
+                              float(s1), g2v, float(s2), ptr(part), nch, stream()), "stc_bn_bwd_reduce")
+    dgamma = torch.empty(C, dtype=torch.float32, device=dev_t)
+    dbeta = torch.empty(C, dtype=torch.float32, device=dev_t)
+    check(l.stc_bn_bwd_apply(L.dtype_code(dt), B, xv, C, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), ptr(gamma),
+                             g1v, float(s1), g2v, float(s2), ptr(part), nch, dxv, ptr(dgamma), ptr(dbeta), stream()),
+          "stc_bn_bwd_apply")
+    return dgamma, dbeta
+
+
+def chan_sum(B, xv, C, Cout, dt, device):
+    nch = stats_chunks(B, xv.H, xv.W)
+    part = torch.empty((nch, C), dtype=torch.float32, device=device)
+    out = torch.empty(Cout, dtype=torch.float32, device=device)
+    check(lib().stc_chan_sum(L.dtype_code(dt), B, xv, C, Cout, ptr(part), nch, ptr(out), stream()), "stc_chan_sum")
+    return out
+
+
+def tanh_bias_bwd(y, gy, dqv, dt):
+    """dq = gy*(1-y^2) into the NHWC view dqv (padded channels zero); returns dbias [C]."""
+    B, C, H, W = y.shape
+    nch = stats_chunks(B, H, W)
+    part = torch.empty((nch, C), dtype=torch.float32, device=y.device)
+    dbias = torch.empty(C, dtype=torch.float32, device=y.device)
+    check(lib().stc_tanh_bias_bwd(L.dtype_code(dt), B, C, H, W, ptr(y), ptr(gy), dqv, ptr(dbias), ptr(part), nch,
+                                  stream()), "stc_tanh_bias_bwd")
+    return dbias
+
+
+def gather(sources, dst, dt):
+    """NCHW fp32 sources (channel concat) -> NHWC dst [B, H, W, Cpad] (extra channels zero)."""
+    B, H, W, cpad = dst.shape
+    n = len(sources)
+    arr = (ctypes.c_void_p * n)(*[s.data_ptr() for s in sources])
+    cs = (ctypes.c_int * n)(*[s.shape[1] for s in sources])
+    check(lib().stc_gather_nchw(L.dtype_code(dt), B, H, W, n, arr, cs, L.nhwc_view(dst), cpad, stream()),
+          "stc_gather_nchw")
+
+
+def scatter(src_nhwc, dsts, chans, dt, H=None, W=None):
+    """NHWC -> NCHW fp32 per channel range; dsts entries may be None (skipped)."""
+    B, Ha, Wa, _ = src_nhwc.shape
+    H = Ha if H is None else H
+    W = Wa if W is None else W
+    n = len(dsts)
+    arr = (ctypes.c_void_p * n)(*[None if d is None else d.data_ptr() for d in dsts])
+    cs = (ctypes.c_int * n)(*chans)
+    check(lib().stc_scatter_nchw(L.dtype_code(dt), B, H, W, L.nhwc_view(src_nhwc, 0, H, W), n, arr, cs, stream()),
+          "stc_scatter_nchw")

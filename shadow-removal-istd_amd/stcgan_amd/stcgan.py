@@ -1,0 +1,284 @@
+"""Drop-in replacement for the STCGAN trainer (STCGAN/stcgan.py:25-433) on MI355X.
+
+Public surface kept: ``STCGAN(args)``, ``train(epochs)``, ``run_epoch(training)``,
+``infer()``, ``save(weights, suffix)``, ``init_weight(...)``, the G1/G2/D1/D2,
+optim_G/optim_D, decay_G/decay_D, adv_loss/data_loss attributes, the losses
+dict returned by run_epoch and the ``{G1,G2,D1,D2}-{suffix}.pt`` checkpoints.
+
+Differences that do not change results:
+  * the per-iteration ``.item()`` / ``.cpu()`` syncs of the reference
+    (STCGAN/stcgan.py:256-262, 308-312) are replaced by on-device accumulators
+    read once per epoch;
+  * the input concatenations of the discriminators/generator are passed as
+    source lists (zero-copy: the first layer gathers the channels itself);
+  * multi-GPU is one process per GPU with an RCCL gradient all-reduce
+    (parallel.py) instead of nn.DataParallel.
+The data pipeline (ISTD folders + augmentation, STCGAN/dataset.py / transform.py)
+is outside this hot path: loaders are any iterable of (names, x, m, y) batches.
+"""
+import datetime
+import logging
+import os
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import networks
+from . import parallel
+from .loss import AdversarialLoss, DataLoss
+from .optim import Adam
+
+
+class SyntheticTriplets:
+    """Synthetic ISTD-shaped batches (x, y ~ U(-1,1), m = +-1), generated on the device."""
+
+    def __init__(self, n_batches, batch_size, size=256, seed=1234, device="cuda"):
+        self.n, self.bs, self.size, self.seed, self.device = n_batches, batch_size, size, seed, device
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        g = torch.Generator(device=self.device)
+        g.manual_seed(self.seed)
+        s = self.size
+        for i in range(self.n):
+            x = torch.rand((self.bs, 3, s, s), generator=g, device=self.device) * 2 - 1
+            m = (torch.rand((self.bs, 1, s, s), generator=g, device=self.device) < 0.5).float() * 2 - 1
+            y = torch.rand((self.bs, 3, s, s), generator=g, device=self.device) * 2 - 1
+            yield ([f"synthetic_{i}_{j}" for j in range(self.bs)], x, m, y)
+
+
+class STCGAN(object):
+
+    def __init__(self, args, train_loader=None, valid_loader=None):
+        self.logger = logging.getLogger(__name__)
+        if not torch.cuda.is_available():
+            raise RuntimeError("stcgan_amd.STCGAN needs a ROCm GPU")
+        dev = args.devices[0] if getattr(args, "devices", None) else "cuda"
+        self.device = torch.device(dev)
+        ngf = getattr(args, "ngf", 64)
+        self.G1 = networks.get_generator(in_channels=3, out_channels=1, ngf=ngf)
+        self.G2 = networks.get_generator(in_channels=3 + 1, out_channels=3, ngf=ngf)
+        self.D1 = networks.get_discriminator(in_channels=3 + 1, ndf=ngf, n_layers=3, use_sigmoid=False)
+        self.D2 = networks.get_discriminator(in_channels=3 + 3 + 1, ndf=ngf, n_layers=3, use_sigmoid=False)
+        tasks = getattr(args, "tasks", ["train"])
+        if "infer" in tasks and "train" not in tasks:
+            assert args.load_weights_g1 is not None
+            assert args.load_weights_g2 is not None
+        self.init_weight(g1_weights=getattr(args, "load_weights_g1", None),
+                         g2_weights=getattr(args, "load_weights_g2", None),
+                         d1_weights=getattr(args, "load_weights_d1", None),
+                         d2_weights=getattr(args, "load_weights_d2", None))
+        dtype = getattr(args, "dtype", "fp32")
+        for net in (self.G1, self.G2, self.D1, self.D2):
+            net.to(self.device)
+            net.set_compute_dtype(dtype)
+        self.optim_G = Adam(list(self.G1.parameters()) + list(self.G2.parameters()),
+                            lr=args.lr_G, betas=(args.beta1, args.beta2))
+        self.optim_D = Adam(list(self.D1.parameters()) + list(self.D2.parameters()),
+                            lr=args.lr_D, betas=(args.beta1, args.beta2))
+        self.decay_G = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_G, cooldown=10, min_lr=1e-7, factor=0.8)
+        self.decay_D = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_D, cooldown=10, min_lr=1e-7, factor=0.8)
+        self.sync_G = parallel.GradAllReduce(list(self.G1.parameters()) + list(self.G2.parameters()))
+        self.sync_D = parallel.GradAllReduce(list(self.D1.parameters()) + list(self.D2.parameters()))
+
+        self.train_loader = train_loader
+        self.valid_loader = valid_loader
+
+        if "train" in tasks:
+            self.d_loss_fn = getattr(args, "D_loss_fn", "standard")
+            self.d_loss_type = getattr(args, "D_loss_type", "normal")
+            # the reference compares against the misspelt "leastsqure" (STCGAN/stcgan.py:111-112):
+            # ls is therefore always False -> MSE with labels 1/0.  Kept as is.
+            self.adv_loss = AdversarialLoss(ls=(self.d_loss_fn == "leastsqure"))
+            self.adv_loss.to(self.device)
+            self.data_loss = DataLoss().to(self.device)
+            self.lambda1 = 5     # data2 loss
+            self.lambda2 = 0.1   # CGAN1 loss
+            self.lambda3 = 0.1   # CGAN2 loss
+            self.adapt = getattr(args, "softadapt", False)
+            self.weights_dir = getattr(args, "weights", None)
+            self.log_interval = getattr(args, "log_every", 3)
+            self.valid_interval = getattr(args, "valid_every", 10)
+        if "infer" in tasks:
+            self.inferd_dir = getattr(args, "infered", None)
+
+    # ------------------------------------------------------------------ training
+    def train(self, epochs=5000):
+        self.logger.info("Start training")
+        best_loss = 100000.0
+        start_time = time.time()
+        for epoch in range(epochs):
+            measures = self.run_epoch()
+            if epoch % self.log_interval == 0:
+                self.logger.info(f"epoch {epoch}: {measures['Loss']}")
+                if self.weights_dir:
+                    self.save(self.weights_dir, "latest")
+            if epoch % self.valid_interval == 0 and self.valid_loader is not None:
+                measures = self.run_epoch(training=False)
+                if measures["Loss"]["total"] < best_loss:
+                    best_loss = measures["Loss"]["total"]
+                    if self.weights_dir:
+                        self.save(self.weights_dir, "best")
+                    self.logger.info(f"Improvement after epoch {epoch}, error = {best_loss:4f}")
+        total_time = datetime.timedelta(seconds=(time.time() - start_time))
+        self.logger.info(f"Training time {total_time}")
+        self.logger.info(f"Best validation loss: {best_loss:.3f}")
+
+    def _d_losses(self, C1_real, C1_fake, C2_real, C2_fake):
+        adv = self.adv_loss
+        t = self.d_loss_type
+        if t == "normal":
+            D1_loss = (adv(C1_fake, is_real=False) + adv(C1_real, is_real=True)) * 0.5
+            D2_loss = (adv(C2_fake, is_real=False) + adv(C2_real, is_real=True)) * 0.5
+        elif t == "rel":
+            D1_loss = adv(C1_real - C1_fake, is_real=True)
+            D2_loss = adv(C2_real - C2_fake, is_real=True)
+        else:  # "rel_avg"
+            D1_loss = (adv(C1_fake - C1_real.mean(dim=0), is_real=False)
+                       + adv(C1_real - C1_fake.mean(dim=0), is_real=True)) * 0.5
+            D2_loss = (adv(C2_fake - C2_real.mean(dim=0), is_real=False)
+                       + adv(C2_real - C2_fake.mean(dim=0), is_real=True)) * 0.5
+        return D1_loss, D2_loss
+
+    def _g_losses(self, C1_real, C1_fake, C2_real, C2_fake):
+        adv = self.adv_loss
+        t = self.d_loss_type
+        if t == "normal":
+            return adv(C1_fake, is_real=True), adv(C2_fake, is_real=True)
+        if t == "rel":
+            return adv(C1_fake - C1_real, is_real=True), adv(C2_fake - C2_real, is_real=True)
+        G1_loss = (adv(C1_fake - C1_real.mean(dim=0), is_real=True)
+                   + adv(C1_real - C1_fake.mean(dim=0), is_real=False)) * 0.5
+        # as the reference: the rel_avg G2 loss is computed from the D1 outputs (STCGAN/stcgan.py:286-290)
+        G2_loss = (adv(C1_fake - C1_real.mean(dim=0), is_real=True)
+                   + adv(C1_real - C1_fake.mean(dim=0), is_real=False)) * 0.5
+        return G1_loss, G2_loss
+
+    def train_step(self, x, m, y, training=True, acc=None):
+        """One iteration of STCGAN.run_epoch (STCGAN/stcgan.py:208-312): D step then G step.
+        Returns the on-device loss scalars (no host sync)."""
+        self.optim_D.zero_grad()
+        self.optim_G.zero_grad()
+        with torch.set_grad_enabled(training):
+            self.optim_D.zero_grad()
+            self.D1.requires_grad_(True)
+            self.D2.requires_grad_(True)
+            C1_real = self.D1([x, m])
+            m_pred = self.G1(x)
+            C1_fake = self.D1([x, m_pred.detach()])
+            C2_real = self.D2([x, m, y])
+            y_pred = self.G2([x, m_pred])
+            C2_fake = self.D2([x, m_pred.detach(), y_pred.detach()])
+            D1_loss, D2_loss = self._d_losses(C1_real, C1_fake, C2_real, C2_fake)
+            D_loss = self.lambda2 * D1_loss + self.lambda3 * D2_loss
+            if training:
+                D_loss.backward()
+                self.sync_D()
+                self.optim_D.step()
+            d_out = (C1_real.detach(), C1_fake.detach(), C2_real.detach(), C2_fake.detach())
+
+            self.optim_G.zero_grad()
+            self.D1.requires_grad_(False)
+            self.D2.requires_grad_(False)
+            if training:  # D is not updated when validating
+                C1_real = self.D1([x, m])
+                C1_fake = self.D1([x, m_pred])
+                C2_real = self.D2([x, m, y])
+                C2_fake = self.D2([x, m_pred, y_pred])
+            G1_loss, G2_loss = self._g_losses(C1_real, C1_fake, C2_real, C2_fake)
+            data1_loss = self.data_loss(m_pred, m)
+            data2_loss = self.data_loss(y_pred, y)
+            G_loss = data1_loss + self.lambda1 * data2_loss + self.lambda2 * G1_loss + self.lambda3 * G2_loss
+            if training:
+                G_loss.backward()
+                self.sync_G()
+                self.optim_G.step()
+        vals = dict(D1=D1_loss.detach(), D2=D2_loss.detach(), D=D_loss.detach(), G1=G1_loss.detach(),
+                    G2=G2_loss.detach(), data1=data1_loss.detach(), data2=data2_loss.detach(), G=G_loss.detach())
+        if acc is not None:
+            for k, v in vals.items():
+                acc[k] = acc[k] + v
+            acc["D1_real"] = acc["D1_real"] + d_out[0].mean()
+            acc["D1_fake"] = acc["D1_fake"] + d_out[1].mean()
+            acc["D2_real"] = acc["D2_real"] + d_out[2].mean()
+            acc["D2_fake"] = acc["D2_fake"] + d_out[3].mean()
+        return vals
+
+    def run_epoch(self, training=True):
+        for net in (self.G1, self.G2, self.D1, self.D2):
+            net.train(training)
+        keys = ["G", "D", "D1", "D2", "G1", "G2", "data1", "data2"]
+        acc = {k: torch.zeros((), device=self.device) for k in keys + ["D1_real", "D1_fake", "D2_real", "D2_fake"]}
+        data_loader = self.train_loader if training else self.valid_loader
+        n_batches = 0
+        for (_, x, m, y) in data_loader:
+            x = x.to(self.device, non_blocking=True)
+            m = m.to(self.device, non_blocking=True)
+            y = y.to(self.device, non_blocking=True)
+            self.train_step(x, m, y, training=training, acc=acc)
+            n_batches += 1
+        host = {k: float(v) for k, v in acc.items()}  # the one host sync of the epoch
+        loss = {k: host[k] for k in keys}
+        if training:
+            self.decay_G.step(loss["G"])
+            self.decay_D.step(loss["D"])
+        loss["total"] = loss["G"] * 0.8 + loss["D"] * 0.2
+        n = max(n_batches, 1)
+        for k in loss:
+            loss[k] /= n
+        D1_out = {"real": host["D1_real"] / n, "fake": host["D1_fake"] / n}
+        D2_out = {"real": host["D2_real"] / n, "fake": host["D2_fake"] / n}
+        return {"Loss": loss, "D1_out": D1_out, "D2_out": D2_out}
+
+    # ------------------------------------------------------------------ inference
+    def infer(self):
+        """G1 -> G2 in eval mode over the validation loader (STCGAN/stcgan.py:332-381).
+        Writes ``{infered}/mask/<name>.npy`` and ``{infered}/shadowless/<name>.npy`` (values in [0,1],
+        the reference's ``x*0.5+0.5``); returns the list of (name, mask, shadowless) arrays."""
+        results = []
+        with torch.no_grad():
+            self.G1.eval()
+            self.G2.eval()
+            for (filenames, x, _, _) in self.valid_loader:
+                x = x.to(self.device, non_blocking=True)
+                m_pred = self.G1(x)
+                y_pred = self.G2([x, m_pred])
+                m_np = m_pred.cpu().numpy() * 0.5 + 0.5
+                y_np = y_pred.cpu().numpy() * 0.5 + 0.5
+                for i, name in enumerate(filenames):
+                    mk = m_np[i].transpose(1, 2, 0)
+                    sl = y_np[i].transpose(1, 2, 0)
+                    results.append((name, mk, sl))
+                    if self.inferd_dir:
+                        os.makedirs(os.path.join(self.inferd_dir, "mask"), exist_ok=True)
+                        os.makedirs(os.path.join(self.inferd_dir, "shadowless"), exist_ok=True)
+                        np.save(os.path.join(self.inferd_dir, "mask", name + ".npy"), mk)
+                        np.save(os.path.join(self.inferd_dir, "shadowless", name + ".npy"), sl)
+        return results
+
+    # ------------------------------------------------------------------ checkpoints
+    def save(self, weights=None, suffix="latest"):
+        # rank 0's BN running statistics are the reference's dev0 replica statistics
+        if parallel.rank() != 0:
+            return
+        if weights is None:
+            weights = self.weights_dir
+        os.makedirs(weights, exist_ok=True)
+        for name in ("G1", "G2", "D1", "D2"):
+            module = getattr(self, name)
+            module = module.module if isinstance(module, nn.DataParallel) else module
+            torch.save(module.state_dict(), os.path.join(weights, f"{name}-{suffix}.pt"))
+
+    def init_weight(self, g1_weights=None, g2_weights=None, d1_weights=None, d2_weights=None):
+        for name, path in (("G1", g1_weights), ("G2", g2_weights), ("D1", d1_weights), ("D2", d2_weights)):
+            net = getattr(self, name)
+            if path:
+                state_dict = torch.load(path, map_location="cpu", weights_only=True)
+                net.load_state_dict(state_dict)
+                self.logger.info(f"Loaded {name} weights: {path}")
+            else:
+                net.apply(networks.weights_init)
