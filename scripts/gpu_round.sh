@@ -1,0 +1,34 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, a short bench.  Every GPU step has its own time
+# limit; the script stops at the first abort/fault/timeout (exit code >= 2 from a step),
+# and continues past ordinary test failures (exit code 1) so the bench still reports.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 30 "gpurun_out/$name.log"
+  if [ $rc -ge 2 ] && [ $rc -ne 5 ]; then echo "== stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+MODE=${1:-all}
+if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
+  step pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout 300
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$MODE" = debug ]; then
+  step debug 300 python scripts/debug_nets.py G1 G2
+  step pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout 300
+  step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+fi
+if [ "$MODE" = prof ] || [ "$MODE" = all_prof ]; then
+  export TMPDIR=/tmp
+  step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
+       -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS}
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ] || [ "$MODE" = all_prof ]; then
+  step bench 600 python bench.py --steps 5 --warmup 2
+fi

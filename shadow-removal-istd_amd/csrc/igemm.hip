@@ -28,7 +28,7 @@ struct ConvParams {
   long long a_bs, a_rs;
   int a_ps, a_co;
   int IH, IW;
-  int lg_cin, lg_tw, in_stride;
+  int cin, lg_tw, in_stride;
   int offy[4], offx[4];
   int stepy, stepx;
   const float* sc;
@@ -126,10 +126,9 @@ igemm_kernel(const ConvParams p) {
   const int ph = z / p.ksplit, split = z % p.ksplit;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
-  const int nsteps = (kend - kbeg) / BK;
+  const int nsteps = (kend - kbeg + BK - 1) / BK;  // a partial last step is zero-filled past kend
   const int GHW = p.GH * p.GW;
   const int offy = p.offy[ph], offx = p.offx[ph];
-  const int cin_mask = (1 << p.lg_cin) - 1;
   const int tw_mask = (1 << p.lg_tw) - 1;
 
   // ---- per-thread A row info
@@ -185,14 +184,15 @@ igemm_kernel(const ConvParams p) {
   // so their latency hides under the MFMAs of the current step.
   auto load_regs = [&](int k0) {
     const int k = k0 + ca * VEC;
-    const int t = k >> p.lg_cin, ci = k & cin_mask;
+    const int t = k / p.cin, ci = k - t * p.cin;
     const int dy = p.stepy * (t >> p.lg_tw), dx = p.stepx * (t & tw_mask);
     aci = ci;
     amask = 0;
+    const bool kin = k < kend;
 #pragma unroll
     for (int i = 0; i < AIT; ++i) {
       const int iy = ayy[i] + dy, ix = axx[i] + dx;
-      if ((unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) {
+      if (kin && (unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) {
         const T* src = abase_ptr + abase[i] + (long long)iy * p.a_rs + (long long)ix * p.a_ps + ci;
         ra[i] = *reinterpret_cast<const uint4*>(src);
         amask |= 1u << i;
@@ -202,7 +202,7 @@ igemm_kernel(const ConvParams p) {
     }
 #pragma unroll
     for (int j = 0; j < BIT; ++j) {
-      rb[j] = bval[j] ? *reinterpret_cast<const uint4*>(bptr[j] + k0) : make_uint4(0, 0, 0, 0);
+      rb[j] = (bval[j] && kin) ? *reinterpret_cast<const uint4*>(bptr[j] + k0) : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_lds = [&](int stage) {
@@ -394,7 +394,7 @@ static Plan plan_for(int dtype, int M, int N, int K, int nphase) {
   pl.mtiles = cdiv(M, pl.BM);
   pl.ntiles = cdiv(N, pl.BN);
   const long long tiles = (long long)pl.mtiles * pl.ntiles * nphase;
-  const int ksteps = K / BK;
+  const int ksteps = cdiv(K, BK);
   int ks = 1;
   // split K until the grid covers the chip (~2 waves of 256 CUs), keeping >= 4 K-steps per split
   while (tiles * ks < 512 && ks * 2 <= 64 && ksteps / (ks * 2) >= 4) ks *= 2;
@@ -453,13 +453,12 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
   STC_REQUIRE(kind >= 0 && kind <= 3, "stc_conv_fwd: bad kind %d", kind);
   const int VEC = dtype == STC_F32 ? 4 : 8;
   const int BK = dtype == STC_F32 ? 32 : 64;
-  const int lg = ilog2_exact(Cin);
-  STC_REQUIRE(lg >= 0 && Cin >= VEC, "stc_conv_fwd: Cin=%d must be a power of two >= %d", Cin, VEC);
+  STC_REQUIRE(Cin >= VEC && Cin % VEC == 0, "stc_conv_fwd: Cin=%d must be a multiple of %d", Cin, VEC);
   STC_REQUIRE(x.co % VEC == 0 && x.ps % VEC == 0 && x.cs == 1, "stc_conv_fwd: input view must be NHWC, 16-byte aligned channels");
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   const int K = taps * Cin;
-  STC_REQUIRE(K % BK == 0, "stc_conv_fwd: K=%d not a multiple of %d", K, BK);
+  (void)BK;
   // GEMM grid: conv kinds -> output grid; convT -> input grid
   int GH, GW;
   if (kind == STC_CONVT_S2) { GH = x.H; GW = x.W; }
@@ -467,7 +466,7 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
   ConvParams p{};
   p.a = (const char*)x.p; p.a_bs = x.bs; p.a_rs = x.rs; p.a_ps = x.ps; p.a_co = x.co;
   p.IH = x.H; p.IW = x.W;
-  p.lg_cin = lg; p.lg_tw = g.taps_lg_tw; p.in_stride = g.in_stride;
+  p.cin = Cin; p.lg_tw = g.taps_lg_tw; p.in_stride = g.in_stride;
   for (int i = 0; i < 4; ++i) { p.offy[i] = g.offy[i]; p.offx[i] = g.offx[i]; }
   p.stepy = g.stepy; p.stepx = g.stepx;
   p.sc = pro_scale; p.sh = pro_shift; p.pro_act = pro_act; p.slope = pro_slope;

@@ -27,7 +27,7 @@ struct WgradParams {
   int GH, GW;  // D grid (the reduction domain) -> P = B*GH*GW
   int IH, IW;  // G logical bounds
   int stride;
-  int R, Cg, lg_cg, Ncol;  // Ncol = 16*Cg
+  int R, Cg, Ncol;  // Ncol = 16*Cg
   int P, pchunk, nsplit;
   const float *dsc, *dsh, *gsc, *gsh;
   int dact, gact;
@@ -82,7 +82,7 @@ wgrad_kernel(const WgradParams p) {
   const int col = c0 + chunk * 4;    // G column of this chunk
   const bool rval = rr < p.R;
   const bool cval = col < p.Ncol;
-  const int t = col >> p.lg_cg, ci = col & ((1 << p.lg_cg) - 1);
+  const int t = col / p.Cg, ci = col - t * p.Cg;
   const int kh = t >> 2, kw = t & 3;
 
   float4 va[4], vb[4];
@@ -214,9 +214,7 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
                               const float* g_scale, const float* g_shift, int g_act, float g_slope,
                               float* dW, void* workspace, int64_t workspace_bytes, void* stream) {
   STC_REQUIRE(dtype == STC_F32 || dtype == STC_BF16, "stc_conv_wgrad: bad dtype");
-  int lg = 0;
-  while ((1 << lg) < Cg) ++lg;
-  STC_REQUIRE((1 << lg) == Cg && Cg >= 4, "stc_conv_wgrad: Cg=%d must be a power of two >= 4", Cg);
+  STC_REQUIRE(Cg >= 4 && Cg % 4 == 0, "stc_conv_wgrad: Cg=%d must be a multiple of 4", Cg);
   STC_REQUIRE(R % 4 == 0, "stc_conv_wgrad: R=%d must be a multiple of 4", R);
   STC_REQUIRE(D.cs == 1 && G.cs == 1 && D.co % 4 == 0 && G.co % 4 == 0 && D.ps % 4 == 0 && G.ps % 4 == 0,
               "stc_conv_wgrad: views must be NHWC with 4-aligned channels");
@@ -225,7 +223,7 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
   p.d = (const char*)D.p; p.d_bs = D.bs; p.d_rs = D.rs; p.d_ps = D.ps; p.d_co = D.co;
   p.g = (const char*)G.p; p.g_bs = G.bs; p.g_rs = G.rs; p.g_ps = G.ps; p.g_co = G.co;
   p.GH = D.H; p.GW = D.W; p.IH = G.H; p.IW = G.W; p.stride = stride;
-  p.R = R; p.Cg = Cg; p.lg_cg = lg; p.Ncol = 16 * Cg;
+  p.R = R; p.Cg = Cg; p.Ncol = 16 * Cg;
   p.P = B * D.H * D.W;
   p.dsc = d_scale; p.dsh = d_shift; p.dact = d_act; p.dslope = d_slope;
   p.gsc = g_scale; p.gsh = g_shift; p.gact = g_act; p.gslope = g_slope;

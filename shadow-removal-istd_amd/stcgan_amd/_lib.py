@@ -101,15 +101,22 @@ def dtype_code(dt):
 
 
 def nhwc_view(t, c0=0, H=None, W=None):
-    """View of a contiguous NHWC tensor [B, Ha, Wa, C] (channel offset c0, logical H x W)."""
+    """View of a contiguous NHWC tensor [B, Ha, Wa, C] (channel offset c0, logical H x W).
+    The view keeps a reference to ``t`` so the memory cannot be recycled before the call."""
     assert t.dim() == 4 and t.is_contiguous()
     _, Ha, Wa, C = t.shape
-    return View(t.data_ptr(), Ha if H is None else H, Wa if W is None else W,
-                Ha * Wa * C, Wa * C, C, c0, 1, 0)
+    H = Ha if H is None else H
+    W = Wa if W is None else W
+    assert 0 <= H <= Ha and 0 <= W <= Wa and 0 <= c0 < C, "view outside the tensor"
+    v = View(t.data_ptr(), H, W, Ha * Wa * C, Wa * C, C, c0, 1, 0)
+    v._keep = t
+    return v
 
 
 def nchw_view(t):
     """View of a contiguous NCHW tensor [B, C, H, W]."""
     assert t.dim() == 4 and t.is_contiguous()
     _, C, H, W = t.shape
-    return View(t.data_ptr(), H, W, C * H * W, W, 1, 0, H * W, 0)
+    v = View(t.data_ptr(), H, W, C * H * W, W, 1, 0, H * W, 0)
+    v._keep = t
+    return v

@@ -16,6 +16,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs the HIP path)")
 
 
+def pytest_runtest_logreport(report):
+    """Print a failure as soon as it happens (a later hard crash must not hide it)."""
+    if report.failed:
+        sys.stderr.write(f"\n!!! FAILED {report.nodeid} ({report.when})\n{report.longreprtext[-3000:]}\n")
+        sys.stderr.flush()
+
+
 def load_golden(name):
     return dict(np.load(os.path.join(GOLDEN, name), allow_pickle=False))
 

@@ -49,7 +49,7 @@ def test_invalid_arguments_fail_loudly_without_gpu():
     rc = lib.stc_conv_fwd(0, 0, 1, v, 3, None, None, 0, 0.0, None, 8, v, None, 0, 1, None, 0, None)
     assert rc != 0
     assert b"Cin=3" in lib.stc_last_error()
-    with pytest.raises(RuntimeError, match="power of two"):
+    with pytest.raises(RuntimeError, match="must be a multiple of 4"):
         _lib.check(rc, "stc_conv_fwd")
 
 

@@ -53,7 +53,9 @@ def test_nets_ngf8_vs_golden(golden, name):
     bs, hw = int(d["meta/bs"]), int(d["meta/hw"])
     net, st = make_net(name, 8)
     assert abs(state_checksum(st) - float(d[f"{name}/checksum"])) < 1e-6
-    x = uniform((bs, NET_IN[name], hw, hw), 100 + NET_SEED[name]).to(DEV).requires_grad_(True)
+    # input seed chosen by the generator so no deep-level activation input sits within 1e-5
+    # of zero (a ReLU decision there is fp32-rounding-sensitive; see make_goldens.pick_input_seed)
+    x = uniform((bs, NET_IN[name], hw, hw), int(d[f"{name}/x_seed"])).to(DEV).requires_grad_(True)
     net.train()
     out = net(x)
     r = normal(tuple(out.shape), 200 + NET_SEED[name]).to(DEV)
@@ -166,22 +168,28 @@ def test_run_epoch_vs_golden(golden, loss_type):
     tr = _trainer(ngf, "normal" if one else loss_type)
     tr.train_loader = batches
     tr.valid_loader = batches
+    # Tolerances.  With the reference init (BN gamma ~ N(0, 0.02)) many gradients are
+    # tiny sums with heavy cancellation; Adam's first step is lr*g/(|g|+eps), so for
+    # |g| ~ eps a relative gradient difference moves the update by up to ~lr/4:
+    # one-iteration state is checked to 0.2*lr_G = 1e-5 (gradients themselves are
+    # checked tightly in test_nets_ngf8_vs_golden).  Two iterations: Adam's second
+    # step amplifies further (tests/test_oracle_golden.py::test_oracle_run_epoch), so
+    # state is checked to 1 lr step and the logged losses / D outputs (means of values
+    # ~1e-3 that depend on those updates) to 1e-4 absolute.
+    m_atol = 2e-5 if one else 1e-4
     meas = tr.run_epoch(training=True)
     for grp, vals in meas.items():
         for k, v in vals.items():
             want = float(d[f"{loss_type}/measures/{grp}/{k}"])
-            assert abs(v - want) <= 2e-5 + 2e-4 * abs(want), (grp, k, v, want)
+            assert abs(v - want) <= m_atol + 2e-4 * abs(want), (grp, k, v, want)
     for n in ["G1", "G2", "D1", "D2"]:
         for k, v in getattr(tr, n).state_dict().items():
-            if one:
-                compare(d, f"{loss_type}/state/{n}/{k}", v.cpu(), atol=1e-6, rtol=1e-4)
-            else:  # two Adam steps: see tests/test_oracle_golden.py::test_oracle_run_epoch
-                compare(d, f"{loss_type}/state/{n}/{k}", v.cpu(), atol=5e-5, rtol=1e-4)
+            compare(d, f"{loss_type}/state/{n}/{k}", v.cpu(), atol=1e-5 if one else 5e-5, rtol=1e-4)
     meas = tr.run_epoch(training=False)
     for grp, vals in meas.items():
         for k, v in vals.items():
             want = float(d[f"{loss_type}/valid_measures/{grp}/{k}"])
-            assert abs(v - want) <= 2e-5 + 2e-4 * abs(want), (grp, k, v, want)
+            assert abs(v - want) <= m_atol + 2e-4 * abs(want), (grp, k, v, want)
 
 
 def test_bf16_generator_vs_oracle():

@@ -42,7 +42,7 @@ def test_oracle_nets_ngf8(golden, name):
     assert abs(state_checksum(st) - float(d[f"{name}/checksum"])) < 1e-6
     params = {k: v.clone().requires_grad_(not ref._is_buffer(k) and v.is_floating_point())
               for k, v in st.items()}
-    x = uniform((bs, NET_IN[name], hw, hw), 100 + NET_SEED[name]).requires_grad_(True)
+    x = uniform((bs, NET_IN[name], hw, hw), int(d[f"{name}/x_seed"])).requires_grad_(True)
     out = forward(name, params, x, True)
     r = normal(tuple(out.shape), 200 + NET_SEED[name])
     (out * r).sum().backward()
