@@ -156,12 +156,34 @@ def main():
         ev1.record(st)
         ev1.synchronize()
         fwd_ms = ev0.elapsed_time(ev1) / reps
-    achieved = flops / (fwd_ms * 1e-3) / 1e12
+        # per-launch HIP events on our stream around every conv-family launch of one G1+G2 forward
+        from stcgan_amd import ops
+        ops._timer = []
+        mp = tr.G1(x)
+        tr.G2([x, mp])
+        torch.cuda.synchronize()
+        launches, ops._timer = ops._timer, None
+    per = {}
+    for name, fl, e0, e1 in launches:
+        t = e0.elapsed_time(e1)
+        a = per.setdefault(name, [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += fl
+        a[2] += t
+    dom = max(per, key=lambda k: per[k][2])
+    n_dom, fl_dom, ms_dom = per[dom]
+    achieved = fl_dom / (ms_dom * 1e-3) / 1e12
+    set_tf = flops / (fwd_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
+    tile = {"fp32": "float", "bf16": "__hip_bfloat16"}[args.dtype]
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": None,
-                "kernel": f"G1+G2 forward (all conv/convT igemm + BN kernels), batch {B}, {flops / 1e9:.2f} GFLOP "
-                          f"per launch set, {fwd_ms:.3f} ms"}
+                "kernel": f"igemm_kernel<{tile},{dom.split('_')[1].replace('x', ',')},...> ({dom}): {n_dom} launches "
+                          f"of one G1+G2 forward, {fl_dom / 1e9:.2f} GFLOP, {ms_dom:.3f} ms (HIP events)",
+                "per_tile": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 2), "ms": round(v[2], 3),
+                                 "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2)} for k, v in per.items()},
+                "g1g2_forward": {"gflop": round(flops / 1e9, 2), "ms": round(fwd_ms, 3),
+                                 "tflops": round(set_tf, 2), "frac": round(set_tf / peak, 4)}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

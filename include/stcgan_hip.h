@@ -75,8 +75,12 @@ int stc_conv_fwd(int dtype, int kind, int B,
                  const float* bias, int epi_tanh, int out_f32,
                  void* workspace, int64_t workspace_bytes, void* stream);
 
-/* Workspace bytes stc_conv_fwd needs for this problem (split-K slabs). */
+/* Workspace bytes stc_conv_fwd needs for this problem (split-K slabs).
+ * Hg x Wg = GEMM grid: the output grid for the conv kinds, the input grid for STC_CONVT_S2. */
 int64_t stc_conv_fwd_workspace(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout);
+/* Launch plan chosen for this problem: out[4] = {BM, BN, ksplit, narrow_n}; narrow_n = 1 means
+ * the N <= 8 wave-per-pixel kernel (HBM-bound layers) instead of an MFMA tile. */
+int stc_conv_fwd_plan(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int32_t* out);
 
 /* ---- weight gradient ---------------------------------------------------------
  * dW[r][ci][kh][kw] = sum_{b,oy,ox} D[b,oy,ox,r] * G[b, oy*s+kh-1, ox*s+kw-1, ci]

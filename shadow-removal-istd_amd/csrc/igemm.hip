@@ -344,6 +344,85 @@ __global__ void splitk_reduce_kernel(const ConvParams p) {
   }
 }
 
+// Narrow-N layers (N <= 8: the 1/3-channel generator output, the 1-channel PatchGAN
+// logits, first-layer input gradients).  An MFMA tile would waste >= 3/4 of its
+// columns, and these layers are HBM-bound (K*4 B read per output pixel for <= 8
+// outputs), so one wave computes one output pixel: its 64 lanes stride over the K
+// chunks with coalesced 16-byte loads (1 KiB per wave instruction), the weights sit
+// in LDS, and a wave shuffle reduces the N partial dots.
+template <typename T>
+__global__ void __launch_bounds__(256) smalln_kernel(const ConvParams p) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int NMAX = 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* wl = reinterpret_cast<T*>(smem);  // [N][K] of this phase
+  const int ph = blockIdx.y;
+  const T* wsrc = reinterpret_cast<const T*>(p.b) + p.b_phase_stride * ph;
+  const int NK = p.N * p.K;
+  for (int i = threadIdx.x * VEC; i < NK; i += 256 * VEC)
+    *reinterpret_cast<uint4*>(wl + i) = *reinterpret_cast<const uint4*>(wsrc + i);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nchunks = p.K / VEC;
+  const int GHW = p.GH * p.GW;
+  const int tw_mask = (1 << p.lg_tw) - 1;
+  const int offy = p.offy[ph], offx = p.offx[ph];
+  const T* A = reinterpret_cast<const T*>(p.a);
+  for (int m = blockIdx.x * 4 + wave; m < p.M; m += gridDim.x * 4) {
+    const int b = m / GHW, rem = m - b * GHW;
+    const int y = rem / p.GW, x = rem - y * p.GW;
+    const long long abase = (long long)b * p.a_bs + p.a_co;
+    float acc[NMAX];
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) acc[n] = 0.f;
+    for (int c = lane; c < nchunks; c += 64) {
+      const int k = c * VEC;
+      const int t = k / p.cin, ci = k - t * p.cin;
+      const int iy = y * p.in_stride + offy + p.stepy * (t >> p.lg_tw);
+      const int ix = x * p.in_stride + offx + p.stepx * (t & tw_mask);
+      if ((unsigned)iy >= (unsigned)p.IH || (unsigned)ix >= (unsigned)p.IW) continue;
+      uint4 v = *reinterpret_cast<const uint4*>(A + abase + (long long)iy * p.a_rs + (long long)ix * p.a_ps + ci);
+      if (p.sc || p.pro_act) v = prologue16<T>(v, p.sc, p.sh, ci, p.pro_act, p.slope);
+      float av[VEC];
+      if constexpr (sizeof(T) == 4) {
+        av[0] = __uint_as_float(v.x); av[1] = __uint_as_float(v.y);
+        av[2] = __uint_as_float(v.z); av[3] = __uint_as_float(v.w);
+      } else {
+        const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { av[2 * q] = __uint_as_float(w[q] << 16); av[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+      }
+#pragma unroll
+      for (int n = 0; n < NMAX; ++n) {
+        if (n >= p.N) break;
+        const T* wr = wl + n * p.K + k;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[n] = fmaf(av[e], ld1<T>(wr + e), acc[n]);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+      if (n >= p.N) break;
+      float s = acc[n];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      acc[n] = s;
+    }
+    if (lane < p.N) {
+      float v = 0.f;
+#pragma unroll
+      for (int n = 0; n < NMAX; ++n) if (n == lane) v = acc[n];
+      if (p.bias) v += p.bias[lane];
+      if (p.tanh_) v = tanhf(v);
+      const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+      const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps +
+                            (long long)(p.c_co + lane) * p.c_cs;
+      if (p.out_f32) reinterpret_cast<float*>(p.c)[off] = v;
+      else st1<T>(reinterpret_cast<T*>(p.c) + off, v);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- host
 struct Geometry {
   int taps_lg_tw;   // lg of taps per row (2 -> 4x4 taps, 1 -> 2x2 taps)
@@ -435,13 +514,35 @@ static int launch_igemm(const Plan& pl, ConvParams& p, hipStream_t st) {
 
 using namespace stc;
 
+static bool use_smalln(int dtype, int N, int K) {
+  const int esz = dtype == STC_F32 ? 4 : 2;
+  return N <= 8 && (long long)N * K * esz <= 64 * 1024;
+}
+
 extern "C" int64_t stc_conv_fwd_workspace(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout) {
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   const int M = B * Hg * Wg, K = taps * Cin;
+  if (use_smalln(dtype, Cout, K)) return 0;
   const Plan pl = plan_for(dtype, M, Cout, K, g.nphase);
   if (pl.ksplit <= 1) return 0;
   return (int64_t)g.nphase * pl.ksplit * (int64_t)M * Cout * 4;
+}
+
+// out[0..3] = {BM, BN, ksplit, narrow-N path}; Hg x Wg is the GEMM grid (output grid for
+// the conv kinds, input grid for STC_CONVT_S2).
+extern "C" int stc_conv_fwd_plan(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int32_t* out) {
+  STC_REQUIRE(kind >= 0 && kind <= 3 && out, "stc_conv_fwd_plan: bad arguments");
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  const int M = B * Hg * Wg, K = taps * Cin;
+  if (use_smalln(dtype, Cout, K)) {
+    out[0] = 1; out[1] = Cout; out[2] = 1; out[3] = 1;
+    return 0;
+  }
+  const Plan pl = plan_for(dtype, M, Cout, K, g.nphase);
+  out[0] = pl.BM; out[1] = pl.BN; out[2] = pl.ksplit; out[3] = 0;
+  return 0;
 }
 
 extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
@@ -480,6 +581,18 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
   p.bias = bias; p.tanh_ = epi_tanh; p.out_f32 = out_f32 || dtype == STC_F32;
   p.nphase = g.nphase;
   if (p.M == 0 || Cout == 0) return 0;
+  hipStream_t st0 = (hipStream_t)stream;
+  if (use_smalln(dtype, Cout, K)) {
+    p.mtiles = 1; p.ntiles = 1; p.ksplit = 1; p.kchunk = K;
+    const int esz = dtype == STC_F32 ? 4 : 2;
+    STC_REQUIRE(K % VEC == 0, "stc_conv_fwd: K=%d", K);
+    dim3 grid((unsigned)std::min(cdiv(p.M, 4), 4096), g.nphase);
+    const size_t lds = (size_t)Cout * K * esz;
+    if (dtype == STC_F32) hipLaunchKernelGGL(smalln_kernel<float>, grid, dim3(256), lds, st0, p);
+    else hipLaunchKernelGGL(smalln_kernel<bf16>, grid, dim3(256), lds, st0, p);
+    STC_CHECK_LAUNCH();
+    return 0;
+  }
   const Plan pl = plan_for(dtype, p.M, Cout, K, g.nphase);
   p.ksplit = pl.ksplit; p.kchunk = pl.kchunk; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles;
   if (pl.ksplit > 1) {

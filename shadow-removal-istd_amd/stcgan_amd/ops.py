@@ -41,9 +41,17 @@ def _pro(pro):
     return ptr(sc), ptr(sh)
 
 
-def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=None, tanh=False, out_f32=False,
-         grid_hw=None):
-    """Implicit-GEMM conv family (stc_conv_fwd).  ``grid_hw`` = GEMM grid (defaults from the views)."""
+_timer = None  # when a list: conv() appends (tile name, flops, start event, end event) per launch
+
+
+def plan_of(kind, B, gh, gw, cin, cout, dt):
+    out = (ctypes.c_int32 * 4)()
+    check(lib().stc_conv_fwd_plan(L.dtype_code(dt), kind, B, gh, gw, cin, cout, out), "stc_conv_fwd_plan")
+    return tuple(out)
+
+
+def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=None, tanh=False, out_f32=False):
+    """Implicit-GEMM conv family (stc_conv_fwd)."""
     dev = w_packed.device
     if kind == L.CONVT_S2:
         gh, gw = xv.H, xv.W
@@ -53,10 +61,22 @@ def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=No
     nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
     ws, nb = _ws(nbytes, dev)
     sc, sh = _pro(pro)
+    timer = _timer
+    if timer is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     rc = l.stc_conv_fwd(L.dtype_code(dt), kind, B, xv, cin, sc, sh, 0 if slope is None else 1,
                         0.0 if slope is None else float(slope), ptr(w_packed), cout, yv, ptr(bias), int(tanh),
                         int(out_f32), ptr(ws), nb, stream())
     check(rc, "stc_conv_fwd")
+    if timer is not None:
+        e1.record()
+        bm, bn, ks, narrow = plan_of(kind, B, gh, gw, cin, cout, dt)
+        tname = "smalln" if narrow else f"igemm_{bm}x{bn}" + (f"_splitk{ks}" if ks > 1 else "")
+        outs = B * gh * gw * (4 if kind == L.CONVT_S2 else 1)
+        taps = 4 if kind == L.CONVT_S2 else 16
+        timer.append((tname, 2.0 * outs * cout * taps * cin, e0, e1))
 
 
 def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None):
