@@ -175,11 +175,16 @@ def main():
     achieved = fl_dom / (ms_dom * 1e-3) / 1e12
     set_tf = flops / (fwd_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
-    tile = {"fp32": "float", "bf16": "__hip_bfloat16"}[args.dtype]
+    tname = {"fp32": "float", "bf16": "__hip_bfloat16"}[args.dtype]
+    if dom.startswith("igemm_"):
+        bm, bn = dom.split("_")[1].split("x")
+        kname = f"igemm_kernel<{tname},{bm},{bn},...>"
+    else:
+        kname = f"{dom}_kernel<{tname}>"
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": None,
-                "kernel": f"igemm_kernel<{tile},{dom.split('_')[1].replace('x', ',')},...> ({dom}): {n_dom} launches "
-                          f"of one G1+G2 forward, {fl_dom / 1e9:.2f} GFLOP, {ms_dom:.3f} ms (HIP events)",
+                "kernel": f"{kname} ({dom}): {n_dom} launches of one G1+G2 forward, {fl_dom / 1e9:.2f} GFLOP, "
+                          f"{ms_dom:.3f} ms (HIP events)",
                 "per_tile": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 2), "ms": round(v[2], 3),
                                  "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2)} for k, v in per.items()},
                 "g1g2_forward": {"gflop": round(flops / 1e9, 2), "ms": round(fwd_ms, 3),

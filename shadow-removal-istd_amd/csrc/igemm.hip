@@ -423,6 +423,161 @@ __global__ void __launch_bounds__(256) smalln_kernel(const ConvParams p) {
   }
 }
 
+// Spatially tiled narrow-N kernel (the fast path for N <= 8).  One thread owns one
+// GEMM-grid point (all 4 sub-pixel phases for the ConvT geometry); the block stages
+// the input halo region for one 128-byte channel chunk in LDS (pixel stride 144 B:
+// 16 lanes at consecutive pixels hit 16 distinct bank slots), so each input element
+// is read from L2/HBM once per tile instead of once per output.  Weights are indexed
+// only by loop counters (wave-uniform -> scalar / broadcast loads).
+//   GEOM 0: ConvT-s2 phased geometry (taps in {0,1}^2 per phase, 3x3 neighbourhood),
+//           TY x TX = 16 x 16 grid points, 256 threads.
+//   GEOM 1: Conv k4 s1 (16 taps, 4x4 neighbourhood), 8 x 8 points, 64 threads.
+template <typename T, int GEOM, int NMAX>
+__global__ void narrow_tiled_kernel(const ConvParams p, int tiles_x, int tiles_per_img) {
+  constexpr int TY = GEOM == 0 ? 16 : 8, TX = GEOM == 0 ? 16 : 8;
+  constexpr int NT = TY * TX;
+  constexpr int HALO = GEOM == 0 ? 2 : 3;  // region = (TY+HALO) x (TX+HALO), origin (-1,-1)
+  constexpr int RY = TY + HALO, RX = TX + HALO;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int CC = 128 / sizeof(T);  // channels per chunk
+  constexpr int PSTR = 144;            // LDS bytes per staged pixel
+  constexpr int NPH = GEOM == 0 ? 4 : 1;
+  __shared__ __attribute__((aligned(16))) char tile[RY * RX * PSTR];
+
+  const int tid = threadIdx.x;
+  const int img = blockIdx.x / tiles_per_img, tix = blockIdx.x % tiles_per_img;
+  const int y0 = (tix / tiles_x) * TY, x0 = (tix % tiles_x) * TX;
+  const int ty = tid / TX, tx = tid % TX;
+  const int gy = y0 + ty, gx = x0 + tx;
+  const T* A = reinterpret_cast<const T*>(p.a) + (long long)img * p.a_bs + p.a_co;
+  const T* Wt = reinterpret_cast<const T*>(p.b);
+  const int taps = GEOM == 0 ? 4 : 16;
+
+  float acc[NPH][NMAX];
+#pragma unroll
+  for (int q = 0; q < NPH; ++q)
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) acc[q][n] = 0.f;
+
+  for (int c0 = 0; c0 < p.cin; c0 += CC) {
+    // ---- stage the halo region (in-bounds pixels get the producer prologue)
+    for (int i = tid; i < RY * RX * 8; i += NT) {
+      const int pix = i >> 3, part = i & 7;
+      const int ry = pix / RX, rx = pix - ry * RX;
+      const int iy = y0 - 1 + ry, ix = x0 - 1 + rx;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if ((unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) {
+        const int ci = c0 + part * VEC;
+        v = *reinterpret_cast<const uint4*>(A + (long long)iy * p.a_rs + (long long)ix * p.a_ps + ci);
+        if (p.sc || p.pro_act) v = prologue16<T>(v, p.sc, p.sh, ci, p.pro_act, p.slope);
+      }
+      *reinterpret_cast<uint4*>(tile + pix * PSTR + part * 16) = v;
+    }
+    __syncthreads();
+    // ---- accumulate
+#pragma unroll
+    for (int part = 0; part < 8; ++part) {
+      const int cbase = c0 + part * VEC;
+      if constexpr (GEOM == 0) {
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) {
+            const uint4 v = *reinterpret_cast<const uint4*>(tile + ((ty + 1 + dy) * RX + (tx + 1 + dx)) * PSTR + part * 16);
+            float f[VEC];
+            if constexpr (sizeof(T) == 4) {
+              f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y); f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+            } else {
+              const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+              for (int q = 0; q < 4; ++q) { f[2 * q] = __uint_as_float(w[q] << 16); f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+            }
+#pragma unroll
+            for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+              for (int pw = 0; pw < 2; ++pw) {
+                const int th = ph - dy, tw = pw - dx;  // out(2y+ph) += in(y + ph - th) * w[tap th]
+                if (th < 0 || th > 1 || tw < 0 || tw > 1) continue;
+                const int phase = ph * 2 + pw, tap = th * 2 + tw;
+#pragma unroll
+                for (int n = 0; n < NMAX; ++n) {
+                  if (n >= p.N) break;
+                  const T* wr = Wt + p.b_phase_stride * phase + ((long long)n * taps + tap) * p.cin + cbase;
+                  float s = acc[phase][n];
+#pragma unroll
+                  for (int e = 0; e < VEC; ++e) s = fmaf(f[e], ld1<T>(wr + e), s);
+                  acc[phase][n] = s;
+                }
+              }
+          }
+      } else {
+#pragma unroll
+        for (int kh = 0; kh < 4; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 4; ++kw) {
+            const uint4 v = *reinterpret_cast<const uint4*>(tile + ((ty + kh) * RX + (tx + kw)) * PSTR + part * 16);
+            float f[VEC];
+            if constexpr (sizeof(T) == 4) {
+              f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y); f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+            } else {
+              const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+              for (int q = 0; q < 4; ++q) { f[2 * q] = __uint_as_float(w[q] << 16); f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+            }
+            const int tap = kh * 4 + kw;
+#pragma unroll
+            for (int n = 0; n < NMAX; ++n) {
+              if (n >= p.N) break;
+              const T* wr = Wt + ((long long)n * taps + tap) * p.cin + cbase;
+              float s = acc[0][n];
+#pragma unroll
+              for (int e = 0; e < VEC; ++e) s = fmaf(f[e], ld1<T>(wr + e), s);
+              acc[0][n] = s;
+            }
+          }
+      }
+    }
+    __syncthreads();
+  }
+  if (gy >= p.GH || gx >= p.GW) return;
+#pragma unroll
+  for (int q = 0; q < NPH; ++q) {
+    const int oy = gy * p.os + p.oy0[q], ox = gx * p.os + p.ox0[q];
+    const long long base = (long long)img * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps;
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+      if (n >= p.N) break;
+      float v = acc[q][n];
+      if (p.bias) v += p.bias[n];
+      if (p.tanh_) v = tanhf(v);
+      const long long off = base + (long long)(p.c_co + n) * p.c_cs;
+      if (p.out_f32) reinterpret_cast<float*>(p.c)[off] = v;
+      else st1<T>(reinterpret_cast<T*>(p.c) + off, v);
+    }
+  }
+}
+
+template <typename T>
+static bool launch_narrow_tiled(int kind, int B, ConvParams& p, hipStream_t st) {
+  const int CC = 128 / sizeof(T);
+  if (p.cin % CC != 0) return false;
+  const int geom = kind == STC_CONVT_S2 ? 0 : (kind == STC_CONV_S1 ? 1 : -1);
+  if (geom < 0) return false;
+  const int TY = geom == 0 ? 16 : 8, TX = geom == 0 ? 16 : 8;
+  const int tiles_x = cdiv(p.GW, TX), tiles_y = cdiv(p.GH, TY);
+  const int tpi = tiles_x * tiles_y;
+  dim3 grid((unsigned)(B * tpi));
+  const bool n4 = p.N <= 4;
+  if (geom == 0) {
+    if (n4) hipLaunchKernelGGL((narrow_tiled_kernel<T, 0, 4>), grid, dim3(256), 0, st, p, tiles_x, tpi);
+    else hipLaunchKernelGGL((narrow_tiled_kernel<T, 0, 8>), grid, dim3(256), 0, st, p, tiles_x, tpi);
+  } else {
+    if (n4) hipLaunchKernelGGL((narrow_tiled_kernel<T, 1, 4>), grid, dim3(64), 0, st, p, tiles_x, tpi);
+    else hipLaunchKernelGGL((narrow_tiled_kernel<T, 1, 8>), grid, dim3(64), 0, st, p, tiles_x, tpi);
+  }
+  return true;
+}
+
 // ------------------------------------------------------------------------- host
 struct Geometry {
   int taps_lg_tw;   // lg of taps per row (2 -> 4x4 taps, 1 -> 2x2 taps)
@@ -586,6 +741,12 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
     p.mtiles = 1; p.ntiles = 1; p.ksplit = 1; p.kchunk = K;
     const int esz = dtype == STC_F32 ? 4 : 2;
     STC_REQUIRE(K % VEC == 0, "stc_conv_fwd: K=%d", K);
+    const bool tiled = dtype == STC_F32 ? launch_narrow_tiled<float>(kind, B, p, st0)
+                                        : launch_narrow_tiled<bf16>(kind, B, p, st0);
+    if (tiled) {
+      STC_CHECK_LAUNCH();
+      return 0;
+    }
     dim3 grid((unsigned)std::min(cdiv(p.M, 4), 4096), g.nphase);
     const size_t lds = (size_t)Cout * K * esz;
     if (dtype == STC_F32) hipLaunchKernelGGL(smalln_kernel<float>, grid, dim3(256), lds, st0, p);

@@ -4,15 +4,20 @@
 //   Conv2d s2/s1 : D = dy (output grid), G = x       (SURVEY.md a4/a5 backward)
 //   ConvT  s2    : D = x  (input grid),  G = dy, s=2 (SURVEY.md a6 backward)
 //
-// GEMM view: C[R][16*Cg] = sum_p A[p][R]^T * Bcol[p][16*Cg]; both operands are
-// pixel-major in HBM (channels contiguous), so they are staged into LDS as
-// [pixel][channel] rows with 16-byte loads/stores and read by the f32 MFMA
-// (v_mfma_f32_32x32x2_f32: lane l feeds A[i=l&31][k=l>>5]) with conflict-free
-// ds_read_b32 across consecutive channels.  The pixel dimension is split over
-// blockIdx.z into fp32 slabs that a second kernel sums in a fixed order
-// (bitwise reproducible) while writing torch layout [R][Cg][4][4].
-// bf16 operands are widened to fp32 while staging (exact), so both dtypes share
-// the f32 MFMA path.
+// GEMM view: C[R][16*Cg] = sum_p D[p][R]^T * Gcol[p][16*Cg]; both operands are
+// pixel-major in HBM (channels contiguous), so each is staged into LDS as
+// [pixel][channel] rows with 16-byte loads and 16-byte LDS stores, no transpose.
+//   fp32: v_mfma_f32_32x32x2_f32 takes one k per lane half (lane l: A[i=l&31][k=l>>5]),
+//         i.e. a plain ds_read_b32 across consecutive channels (conflict-free).
+//   bf16: v_mfma_f32_32x32x16_bf16 needs 8 consecutive k (pixels) per lane: two
+//         ds_read_b64_tr_b16 (hardware 4x16 transpose per 16-lane group) build each
+//         operand from the [pixel][channel] image.  Rows are 320 B (256 B of data +
+//         64 B pad): 320/4 = 80 = 16 mod 64 banks, so the four rows of a transposed
+//         read land in disjoint 16-bank ranges (conflict-free per 32-lane half).
+// The global loads of K-step s+1 are issued before step s's MFMAs and only consumed
+// (prologue: BN affine + LeakyReLU/ReLU of the producer) when written to LDS.
+// The pixel dimension is split over blockIdx.z into fp32 slabs that a second kernel
+// sums in a fixed order (bitwise reproducible) while writing torch layout.
 #include "common.hpp"
 
 namespace stc {
@@ -37,29 +42,65 @@ struct WgradParams {
 };
 
 constexpr int WG_BM = 128, WG_BN = 128, WG_BK = 32;
-constexpr int WG_LDA = WG_BM + 4;  // floats; +4 keeps rows 16-byte aligned
+
+template <typename T> struct WgCfg;
+template <> struct WgCfg<float> {
+  static constexpr int ROWB = (WG_BM + 4) * 4;  // 528 B: 16-byte aligned rows
+};
+template <> struct WgCfg<bf16> {
+  static constexpr int ROWB = 320;  // 256 B data + 64 B pad (see header)
+};
 
 template <typename T>
-__device__ __forceinline__ float4 load4(const char* base, long long off) {
-  return Vec4<T>::load(reinterpret_cast<const T*>(base) + off);
-}
-
-__device__ __forceinline__ float4 pro4(float4 v, const float* sc, const float* sh, int c, int act_on, float slope) {
+__device__ __forceinline__ uint4 wg_pro(uint4 v, const float* sc, const float* sh, int act_on, float slope) {
+  // sc/sh already offset to the chunk's first channel
+  constexpr int VEC = 16 / sizeof(T);
+  float f[VEC];
+  if constexpr (sizeof(T) == 4) {
+    f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y); f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+  } else {
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { f[2 * q] = __uint_as_float(w[q] << 16); f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+  }
   if (sc) {
-    v.x = fmaf(v.x, sc[c], sh[c]); v.y = fmaf(v.y, sc[c + 1], sh[c + 1]);
-    v.z = fmaf(v.z, sc[c + 2], sh[c + 2]); v.w = fmaf(v.w, sc[c + 3], sh[c + 3]);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) f[e] = fmaf(f[e], sc[e], sh[e]);
   }
   if (act_on) {
-    v.x = act(v.x, slope); v.y = act(v.y, slope); v.z = act(v.z, slope); v.w = act(v.w, slope);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) f[e] = f[e] > 0.f ? f[e] : f[e] * slope;
   }
-  return v;
+  uint4 r;
+  if constexpr (sizeof(T) == 4) {
+    r.x = __float_as_uint(f[0]); r.y = __float_as_uint(f[1]); r.z = __float_as_uint(f[2]); r.w = __float_as_uint(f[3]);
+  } else {
+    unsigned w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = (unsigned)f2bf(f[2 * q]) | ((unsigned)f2bf(f[2 * q + 1]) << 16);
+    r.x = w[0]; r.y = w[1]; r.z = w[2]; r.w = w[3];
+  }
+  return r;
+}
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ v4i16 lds_tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(p));
 }
 
 template <typename T>
 __global__ void __launch_bounds__(256)
 wgrad_kernel(const WgradParams p) {
-  __shared__ __attribute__((aligned(16))) float sA[2][WG_BK][WG_LDA];
-  __shared__ __attribute__((aligned(16))) float sB[2][WG_BK][WG_LDA];
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int CPR = WG_BM * (int)sizeof(T) / 16;  // 16-byte chunks per staged row (32 fp32 / 16 bf16)
+  constexpr int RPP = 256 / CPR;                     // rows per pass
+  constexpr int NP = WG_BK / RPP;                    // passes per K-step (4 fp32 / 2 bf16)
+  constexpr int ROWB = WgCfg<T>::ROWB;
+  constexpr int TILEB = WG_BK * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILEB];  // [stage][A|B]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -76,43 +117,60 @@ wgrad_kernel(const WgradParams p) {
   const int pend = min(p.P, pbeg + p.pchunk);
   const int GHW = p.GH * p.GW;
 
-  // staging map: row (pixel) kp = tid/32 + 8*i, chunk (4 channels) = tid%32
-  const int chunk = tid & 31;
-  const int rr = r0 + chunk * 4;     // D channel of this chunk
-  const int col = c0 + chunk * 4;    // G column of this chunk
+  // staging map: row (pixel) kp = tid/CPR + RPP*i, chunk = tid%CPR (VEC channels)
+  const int chunk = tid % CPR;
+  const int rr = r0 + chunk * VEC;   // D channel of this chunk
+  const int col = c0 + chunk * VEC;  // G column of this chunk
   const bool rval = rr < p.R;
   const bool cval = col < p.Ncol;
   const int t = col / p.Cg, ci = col - t * p.Cg;
   const int kh = t >> 2, kw = t & 3;
+  const T* Dp = reinterpret_cast<const T*>(p.d);
+  const T* Gp = reinterpret_cast<const T*>(p.g);
+  const float* dsc = p.dsc ? p.dsc + rr : nullptr;
+  const float* dsh = p.dsh ? p.dsh + rr : nullptr;
+  const float* gsc = p.gsc ? p.gsc + ci : nullptr;
+  const float* gsh = p.gsh ? p.gsh + ci : nullptr;
+  const bool dpro = p.dsc != nullptr || p.dact;
+  const bool gpro = p.gsc != nullptr || p.gact;
 
-  float4 va[4], vb[4];
+  uint4 va[NP], vb[NP];
+  unsigned ma = 0, mb = 0;
   auto load = [&](int k0) {
+    ma = 0; mb = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int pix = k0 + (tid >> 5) + 8 * i;
-      va[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      vb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < NP; ++i) {
+      const int pix = k0 + tid / CPR + RPP * i;
+      va[i] = make_uint4(0, 0, 0, 0);
+      vb[i] = make_uint4(0, 0, 0, 0);
       if (pix < pend) {
         const int b = pix / GHW, rem = pix - b * GHW;
         const int oy = rem / p.GW, ox = rem - oy * p.GW;
         if (rval) {
-          float4 v = load4<T>(p.d, (long long)b * p.d_bs + (long long)oy * p.d_rs + (long long)ox * p.d_ps + p.d_co + rr);
-          va[i] = pro4(v, p.dsc ? p.dsc + rr : nullptr, p.dsh ? p.dsh + rr : nullptr, 0, p.dact, p.dslope);
+          va[i] = *reinterpret_cast<const uint4*>(Dp + (long long)b * p.d_bs + (long long)oy * p.d_rs +
+                                                  (long long)ox * p.d_ps + p.d_co + rr);
+          ma |= 1u << i;
         }
         const int iy = oy * p.stride + kh - 1, ix = ox * p.stride + kw - 1;
         if (cval && (unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) {
-          float4 v = load4<T>(p.g, (long long)b * p.g_bs + (long long)iy * p.g_rs + (long long)ix * p.g_ps + p.g_co + ci);
-          vb[i] = pro4(v, p.gsc ? p.gsc + ci : nullptr, p.gsh ? p.gsh + ci : nullptr, 0, p.gact, p.gslope);
+          vb[i] = *reinterpret_cast<const uint4*>(Gp + (long long)b * p.g_bs + (long long)iy * p.g_rs +
+                                                  (long long)ix * p.g_ps + p.g_co + ci);
+          mb |= 1u << i;
         }
       }
     }
   };
   auto store = [&](int st) {
+    char* sA = smem + st * 2 * TILEB;
+    char* sB = sA + TILEB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kp = (tid >> 5) + 8 * i;
-      *reinterpret_cast<float4*>(&sA[st][kp][chunk * 4]) = va[i];
-      *reinterpret_cast<float4*>(&sB[st][kp][chunk * 4]) = vb[i];
+    for (int i = 0; i < NP; ++i) {
+      const int kp = tid / CPR + RPP * i;
+      uint4 a = va[i], b = vb[i];
+      if (dpro && (ma >> i & 1u)) a = wg_pro<T>(a, dsc, dsh, p.dact, p.dslope);
+      if (gpro && (mb >> i & 1u)) b = wg_pro<T>(b, gsc, gsh, p.gact, p.gslope);
+      *reinterpret_cast<uint4*>(sA + kp * ROWB + chunk * 16) = a;
+      *reinterpret_cast<uint4*>(sB + kp * ROWB + chunk * 16) = b;
     }
   };
 
@@ -131,20 +189,50 @@ wgrad_kernel(const WgradParams p) {
   }
   __syncthreads();
   const int li = lane & 31, lh = lane >> 5;
+  // transposed-read addressing (bf16): 16-lane group g16, lane-in-group 4*trq + trp
+  const int g16 = lane >> 4, lig = lane & 15;
+  const int trq = lig >> 2, trp = lig & 3;
+  const int trh = g16 >> 1, trc = 16 * (g16 & 1) + 4 * trp;
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
     if (s + 1 < nsteps) load(pbeg + (s + 1) * WG_BK);
+    const char* sA = smem + cur * 2 * TILEB;
+    const char* sB = sA + TILEB;
+    if constexpr (sizeof(T) == 4) {
 #pragma unroll 4
-    for (int kk = 0; kk < WG_BK / 2; ++kk) {
-      const int k = 2 * kk + lh;
-      float a0 = sA[cur][k][wm * 64 + li];
-      float a1 = sA[cur][k][wm * 64 + 32 + li];
-      float b0 = sB[cur][k][wn * 64 + li];
-      float b1 = sB[cur][k][wn * 64 + 32 + li];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      for (int kk = 0; kk < WG_BK / 2; ++kk) {
+        const int k = 2 * kk + lh;
+        const float* ra = reinterpret_cast<const float*>(sA + k * ROWB);
+        const float* rb = reinterpret_cast<const float*>(sB + k * ROWB);
+        const float a0 = ra[wm * 64 + li], a1 = ra[wm * 64 + 32 + li];
+        const float b0 = rb[wn * 64 + li], b1 = rb[wn * 64 + 32 + li];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < WG_BK / 16; ++ks) {
+        bf16x8 fa[2], fb[2];
+        const int row = ks * 16 + 8 * trh + trq;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const char* pa = sA + row * ROWB + (wm * 64 + 32 * i + trc) * 2;
+          const char* pb = sB + row * ROWB + (wn * 64 + 32 * i + trc) * 2;
+          const v4i16 a_lo = lds_tr16(pa), a_hi = lds_tr16(pa + 4 * ROWB);
+          const v4i16 b_lo = lds_tr16(pb), b_hi = lds_tr16(pb + 4 * ROWB);
+          const v8i16 av = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
+          const v8i16 bv = {b_lo[0], b_lo[1], b_lo[2], b_lo[3], b_hi[0], b_hi[1], b_hi[2], b_hi[3]};
+          fa[i] = __builtin_bit_cast(bf16x8, av);
+          fb[i] = __builtin_bit_cast(bf16x8, bv);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
     }
     if (s + 1 < nsteps) store(cur ^ 1);
     __syncthreads();
@@ -214,10 +302,11 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
                               const float* g_scale, const float* g_shift, int g_act, float g_slope,
                               float* dW, void* workspace, int64_t workspace_bytes, void* stream) {
   STC_REQUIRE(dtype == STC_F32 || dtype == STC_BF16, "stc_conv_wgrad: bad dtype");
-  STC_REQUIRE(Cg >= 4 && Cg % 4 == 0, "stc_conv_wgrad: Cg=%d must be a multiple of 4", Cg);
-  STC_REQUIRE(R % 4 == 0, "stc_conv_wgrad: R=%d must be a multiple of 4", R);
-  STC_REQUIRE(D.cs == 1 && G.cs == 1 && D.co % 4 == 0 && G.co % 4 == 0 && D.ps % 4 == 0 && G.ps % 4 == 0,
-              "stc_conv_wgrad: views must be NHWC with 4-aligned channels");
+  const int VEC = dtype == STC_F32 ? 4 : 8;
+  STC_REQUIRE(Cg >= VEC && Cg % VEC == 0, "stc_conv_wgrad: Cg=%d must be a multiple of %d", Cg, VEC);
+  STC_REQUIRE(R % VEC == 0, "stc_conv_wgrad: R=%d must be a multiple of %d", R, VEC);
+  STC_REQUIRE(D.cs == 1 && G.cs == 1 && D.co % VEC == 0 && G.co % VEC == 0 && D.ps % VEC == 0 && G.ps % VEC == 0,
+              "stc_conv_wgrad: views must be NHWC with %d-aligned channels", VEC);
   STC_REQUIRE(Cg_out <= Cg, "stc_conv_wgrad: Cg_out > Cg");
   WgradParams p{};
   p.d = (const char*)D.p; p.d_bs = D.bs; p.d_rs = D.rs; p.d_ps = D.ps; p.d_co = D.co;

@@ -94,6 +94,51 @@ def test_convT_fwd(case, dt):
     close(nchw(y), ref, tol=3e-2 if dt == torch.bfloat16 else 2e-5, what="convT fwd")
 
 
+NARROW_CASES = [  # kind, B, Cin, N, H, W  (GEMM grid = input grid for convT, output grid for conv s1)
+    ("convT", 2, 128, 3, 20, 24),   # G output layer geometry (partial 16x16 tiles)
+    ("convT", 2, 128, 1, 16, 16),
+    ("convT", 1, 64, 8, 9, 13),     # first-layer input-gradient geometry, N = 8
+    ("convT", 2, 64, 4, 32, 32),
+    ("conv_s1", 2, 512, 1, 31, 31),  # PatchGAN logits: 31x31 -> 30x30
+    ("conv_s1", 1, 256, 2, 12, 10),
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", NARROW_CASES)
+def test_narrow_n_paths(case, dt):
+    kind, B, Cin, N, H, W = case
+    x = rnd(B, Cin, H, W, seed=17)
+    sc = torch.rand(Cin, generator=torch.Generator().manual_seed(18)) + 0.5
+    sh = rnd(Cin, seed=19, scale=0.2)
+    b = rnd(N, seed=20)
+    xa = F.relu(x * sc[None, :, None, None] + sh[None, :, None, None])
+    xg = nhwc(x).to(DEV, dt)
+    if dt == torch.bfloat16:
+        xa = F.relu(nchw(xg.float().cpu()) * sc[None, :, None, None] + sh[None, :, None, None])
+        xa = xa.to(torch.bfloat16).float()
+    if kind == "convT":
+        w = rnd(Cin, N, 4, 4, seed=21, scale=0.05)
+        wq = w.to(torch.bfloat16).float() if dt == torch.bfloat16 else w
+        ref = torch.tanh(F.conv_transpose2d(xa, wq, b, 2, 1))
+        wp = ops.pack(L.PACK_CONVT_FWD, w.to(DEV), N, Cin, dt)
+        y = torch.empty((B, N, 2 * H, 2 * W), device=DEV)
+        ops.conv(L.CONVT_S2, B, L.nhwc_view(xg), Cin, wp, N, L.nchw_view(y), dt, pro=(sc.to(DEV), sh.to(DEV)),
+                 slope=0.0, bias=b.to(DEV), tanh=True, out_f32=True)
+    else:
+        w = rnd(N, Cin, 4, 4, seed=22, scale=0.05)
+        wq = w.to(torch.bfloat16).float() if dt == torch.bfloat16 else w
+        ref = torch.tanh(F.conv2d(xa, wq, b, 1, 1))
+        wp = ops.pack(L.PACK_CONV_FWD, w.to(DEV), N, Cin, dt)
+        y = torch.empty((B, N, H - 1, W - 1), device=DEV)
+        ops.conv(L.CONV_S1, B, L.nhwc_view(xg), Cin, wp, N, L.nchw_view(y), dt, pro=(sc.to(DEV), sh.to(DEV)),
+                 slope=0.0, bias=b.to(DEV), tanh=True, out_f32=True)
+    assert ops.plan_of(L.CONVT_S2 if kind == "convT" else L.CONV_S1, B, H if kind == "convT" else H - 1,
+                       W if kind == "convT" else W - 1, Cin, N, dt)[3] == 1
+    # fp32: one serial fmaf chain per output over K = 16*Cin (8192 terms for the logits layer)
+    close(y, ref, tol=3e-5 if dt == torch.float32 else 1e-3, what=f"narrow {kind}")
+
+
 def test_convT_tanh_bias_nchw_out():
     B, Cin, Cout, H, W = 2, 32, 3, 8, 8
     x = rnd(B, Cin, H, W, seed=21)
@@ -152,8 +197,8 @@ def test_convT_dgrad(case):
 @pytest.mark.parametrize("stride", [2, 1])
 def test_conv_wgrad(case, stride, dt):
     B, Cin, Cout, H, W = case
-    if Cin < 4:
-        pytest.skip()
+    if Cin < ops.vec(dt) or Cout % ops.vec(dt):
+        pytest.skip("channels below the vector width (padded at the model edge)")
     x = rnd(B, Cin, H, W, seed=51)
     w = rnd(Cout, Cin, 4, 4, seed=52, scale=0.05).requires_grad_(True)
     sc = torch.rand(Cin, generator=torch.Generator().manual_seed(53)) + 0.5
@@ -172,7 +217,25 @@ def test_conv_wgrad(case, stride, dt):
         (gw,) = torch.autograd.grad(y, w2, nchw(dyg.float().cpu()))
     dW = ops.wgrad(B, stride, L.nhwc_view(dyg), Cout, L.nhwc_view(xg), Cin, Cin, dt,
                    gpro=(sc.to(DEV), sh.to(DEV)), gslope=0.2, device=DEV)
-    close(dW, gw, tol=1e-3 if dt == torch.bfloat16 else 2e-5, what="conv wgrad")
+    # bf16: operands (incl. the prologue output) are bf16-rounded before the MFMA
+    close(dW, gw, tol=1e-2 if dt == torch.bfloat16 else 2e-5, what="conv wgrad")
+
+
+@pytest.mark.parametrize("case", CONV_CASES[1:6])
+def test_convT_wgrad_bf16(case):
+    B, Cin, Cout, H, W = case
+    if Cout % 8:
+        pytest.skip()
+    dt = torch.bfloat16
+    x = rnd(B, Cin, H, W, seed=64)
+    dy = rnd(B, Cout, 2 * H, 2 * W, seed=65)
+    xg, dyg = nhwc(x).to(DEV, dt), nhwc(dy).to(DEV, dt)
+    xb = F.relu(nchw(xg.float().cpu())).to(torch.bfloat16).float()
+    w = torch.zeros(Cin, Cout, 4, 4, requires_grad=True)
+    y = F.conv_transpose2d(xb, w, None, 2, 1)
+    (gw,) = torch.autograd.grad(y, w, nchw(dyg.float().cpu()))
+    dW = ops.wgrad(B, 2, L.nhwc_view(xg), Cin, L.nhwc_view(dyg), Cout, Cout, dt, dslope=0.0, device=DEV)
+    close(dW, gw, tol=2e-5, what="convT wgrad bf16")  # exact bf16 products, fp32 sums
 
 
 @pytest.mark.parametrize("case", CONV_CASES[1:6])
