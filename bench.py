@@ -97,9 +97,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # STC_DIST_BACKEND=gloo: rehearse the multi-rank path on fewer GPUs than ranks
+    backend = os.environ.get("STC_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    local = local % max(ndev, 1) if backend != "nccl" else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     import types
     from stcgan_amd.stcgan import STCGAN
 

@@ -127,6 +127,13 @@ int stc_bn_finalize(const float* part, int nchunks, int C,
                     float momentum, float eps,
                     float* mean, float* rstd, float* scale, float* shift, void* stream);
 
+/* Activation materialisation (BatchNorm apply + LeakyReLU/ReLU, STCGAN/networks.py:106-109,
+ * 158, 170-171, 179-180): n = x*scale + shift (identity if scale == NULL), y1 = act(n, slope1),
+ * y2 = act(n, slope2) if y2.p != NULL; act(v, s) = v > 0 ? v : s*v (s = 0 ReLU, 0.2 LeakyReLU,
+ * 1 identity).  One pass per BN'd tensor; the consuming GEMMs then stage plain operands. */
+int stc_bn_apply(int dtype, int B, stc_view x, int C, const float* scale, const float* shift,
+                 stc_view y1, float slope1, stc_view y2, float slope2, void* stream);
+
 /* BN backward fused with the activation backward of its consumers:
  *   n  = x*scale + shift (the BN output; scale/shift from stc_bn_finalize)
  *   dn = g1 * act1'(n) + g2 * act2'(n)   (g1/g2 optional; act' = 1 if n>0 else slope)

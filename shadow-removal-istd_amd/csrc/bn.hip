@@ -261,6 +261,37 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, int B, int C,
   }
 }
 
+// Activation materialisation: n = x*scale + shift (identity without a table), then
+// y1 = act(n, slope1) and optionally y2 = act(n, slope2) (slope 0 = ReLU, 0.2 = the
+// LeakyReLU of the reference, 1 = identity).  Applied once per element, so the GEMMs
+// that consume y1/y2 (each input element is re-read 4-16x by the im2col) stage plain
+// operands with no per-load transform.
+template <typename T>
+__global__ void __launch_bounds__(256) bn_apply_kernel(View x, int B, int C, const float* scale, const float* shift,
+                                                       View y1, float s1, View y2, float s2, int has2) {
+  const int cq = C >> 2;
+  const long long HW = (long long)x.H * x.W, total = HW * B * cq;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(idx % cq);
+    const long long pix = idx / cq;
+    const int b = (int)(pix / HW), rem = (int)(pix % HW);
+    const int yy = rem / x.W, xx = rem % x.W;
+    const int c = 4 * q;
+    float4 v = vload<T>(x, b, yy, xx, c);
+    if (scale) {
+      const float4 sc = *reinterpret_cast<const float4*>(scale + c);
+      const float4 sh = *reinterpret_cast<const float4*>(shift + c);
+      v = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z), fmaf(v.w, sc.w, sh.w));
+    }
+    Vec4<T>::store(reinterpret_cast<T*>(y1.p) + vidx(y1, b, yy, xx, c),
+                   make_float4(act(v.x, s1), act(v.y, s1), act(v.z, s1), act(v.w, s1)));
+    if (has2)
+      Vec4<T>::store(reinterpret_cast<T*>(y2.p) + vidx(y2, b, yy, xx, c),
+                     make_float4(act(v.x, s2), act(v.y, s2), act(v.z, s2), act(v.w, s2)));
+  }
+}
+
 // part[chunk][c] = sum over the chunk's pixels of x (conv bias gradients)
 template <typename T>
 __global__ void __launch_bounds__(256) chan_sum_kernel(View x, int B, int C, float* part, int nchunks) {
@@ -327,6 +358,23 @@ extern "C" int stc_chan_stats(int dtype, int B, stc_view x, int C, float* part, 
   View v = mkview(x);
   if (dtype == STC_F32) hipLaunchKernelGGL(chan_stats_kernel<float>, dim3(nchunks), dim3(256), 0, st, v, B, C, part, nchunks);
   else hipLaunchKernelGGL(chan_stats_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, v, B, C, part, nchunks);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_bn_apply(int dtype, int B, stc_view x, int C, const float* scale, const float* shift, stc_view y1,
+                            float slope1, stc_view y2, float slope2, void* stream) {
+  STC_REQUIRE(C % 4 == 0, "stc_bn_apply: C=%d must be a multiple of 4", C);
+  STC_REQUIRE((scale == nullptr) == (shift == nullptr), "stc_bn_apply: scale/shift must come together");
+  STC_REQUIRE(x.cs == 1 && y1.cs == 1 && y1.p, "stc_bn_apply: NHWC views required");
+  hipStream_t st = (hipStream_t)stream;
+  View v = mkview(x), o1 = mkview(y1), o2 = y2.p ? mkview(y2) : mkview(y1);
+  const long long work = (long long)B * x.H * x.W * (C / 4);
+  const int blocks = grid_for(work);
+  if (dtype == STC_F32)
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(blocks), dim3(256), 0, st, v, B, C, scale, shift, o1, slope1, o2, slope2, y2.p != nullptr ? 1 : 0);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(blocks), dim3(256), 0, st, v, B, C, scale, shift, o1, slope1, o2, slope2, y2.p != nullptr ? 1 : 0);
   STC_CHECK_LAUNCH();
   return 0;
 }

@@ -160,25 +160,44 @@ __global__ void loss_bwd_kernel(int kind, const float* p, const float* t, float 
 }
 
 // ------------------------------------------------------------------ weight packing
+// One thread per (n, c) pair: reads the 16 contiguous taps W[p][q][0..15] (64 B) once and
+// writes them to their 16 (phase, tap) slots; consecutive threads take consecutive c, so
+// every output write is coalesced along the operand's contiguous K dimension.
 template <typename T>
 __global__ void pack_kernel(int mode, const float* W, int P, int Q, T* out, int N_pad, int C_pad, int nph, int taps) {
-  const long long total = (long long)nph * N_pad * taps * C_pad;
+  const long long total = (long long)N_pad * C_pad;
+  const bool n_is_p = (mode == STC_PACK_CONV_FWD || mode == STC_PACK_CONVT_DGRAD);
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(idx % C_pad);
-    long long r = idx / C_pad;
-    const int t = (int)(r % taps);
-    r /= taps;
-    const int n = (int)(r % N_pad);
-    const int z = (int)(r / N_pad);
-    int kh, kw;
-    if (taps == 16) { kh = t >> 2; kw = t & 3; }
-    else { const int ph = z >> 1, pw = z & 1; kh = (1 - ph) + 2 * (t >> 1); kw = (1 - pw) + 2 * (t & 1); }
-    const bool n_is_p = (mode == STC_PACK_CONV_FWD || mode == STC_PACK_CONVT_DGRAD);
+    const int n = (int)(idx / C_pad);
     const int pi = n_is_p ? n : c, qi = n_is_p ? c : n;
-    float v = 0.f;
-    if (pi < P && qi < Q) v = W[(((long long)pi * Q + qi) * 4 + kh) * 4 + kw];
-    st1<T>(out + idx, v);
+    float w[16];
+    if (pi < P && qi < Q) {
+      const float4* src = reinterpret_cast<const float4*>(W + ((long long)pi * Q + qi) * 16);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float4 f = src[v];
+        w[4 * v] = f.x; w[4 * v + 1] = f.y; w[4 * v + 2] = f.z; w[4 * v + 3] = f.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) w[t] = 0.f;
+    }
+    if (taps == 16) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) st1<T>(out + ((long long)n * 16 + t) * C_pad + c, w[t]);
+    } else {
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int ph = z >> 1, pw = z & 1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int kh = (1 - ph) + 2 * (t >> 1), kw = (1 - pw) + 2 * (t & 1);
+          st1<T>(out + (((long long)z * N_pad + n) * 4 + t) * C_pad + c, w[kh * 4 + kw]);
+        }
+      }
+    }
   }
 }
 
@@ -267,7 +286,7 @@ extern "C" int stc_pack_weight(int dtype, int mode, const float* W, int P, int Q
   const bool phased = mode == STC_PACK_CONV_DGRAD || mode == STC_PACK_CONVT_FWD;
   const int nph = phased ? 4 : 1, taps = phased ? 4 : 16;
   hipStream_t st = (hipStream_t)stream;
-  const long long total = (long long)nph * N_pad * taps * C_pad;
+  const long long total = (long long)N_pad * C_pad;  // one thread per (n, c)
   if (dtype == STC_F32)
     hipLaunchKernelGGL(pack_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, mode, W, P, Q, (float*)out, N_pad, C_pad, nph, taps);
   else

@@ -91,8 +91,8 @@ __device__ __forceinline__ uint4 prologue16(uint4 v, const float* sc, const floa
   return r;
 }
 
-template <typename T, int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256)
+template <typename T, int BM, int BN, int WM, int WN, bool PRO>
+__global__ void __launch_bounds__(256, 2)
 igemm_kernel(const ConvParams p) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int BK = 128 / sizeof(T);
@@ -174,49 +174,53 @@ igemm_kernel(const ConvParams p) {
     }
   }
 
-  uint4 ra[AIT], rb[BIT];
+  // Two register staging sets (ping-pong): the global loads of K-step s+2 are issued at
+  // step s and written to LDS at the end of step s+1, so two steps of MFMA work cover
+  // their latency (a bf16 K-step is only 16 MFMAs per wave).
+  struct Regs {
+    uint4 ra[AIT], rb[BIT];
+    unsigned amask;  // which A chunks were in bounds (prologue must not touch padding)
+    int aci;         // channel of this thread's chunk in the staged K-step
+  };
+  Regs r0, r1;
   const T* abase_ptr = reinterpret_cast<const T*>(p.a);
-  const bool has_pro = p.sc != nullptr || p.pro_act != 0;
-  unsigned amask = 0;  // which A chunks were in bounds (prologue must not touch padding)
-  int aci = 0;         // channel of this thread's chunk in the staged K-step
+  constexpr bool has_pro = PRO;  // the engine materialises activations: PRO=false on its hot path
 
-  // Issue the global loads of one K-step; nothing consumes them until store_lds,
-  // so their latency hides under the MFMAs of the current step.
-  auto load_regs = [&](int k0) {
+  auto load_regs = [&](Regs& R, int k0) {
     const int k = k0 + ca * VEC;
     const int t = k / p.cin, ci = k - t * p.cin;
     const int dy = p.stepy * (t >> p.lg_tw), dx = p.stepx * (t & tw_mask);
-    aci = ci;
-    amask = 0;
+    R.aci = ci;
+    R.amask = 0;
     const bool kin = k < kend;
 #pragma unroll
     for (int i = 0; i < AIT; ++i) {
       const int iy = ayy[i] + dy, ix = axx[i] + dx;
       if (kin && (unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) {
         const T* src = abase_ptr + abase[i] + (long long)iy * p.a_rs + (long long)ix * p.a_ps + ci;
-        ra[i] = *reinterpret_cast<const uint4*>(src);
-        amask |= 1u << i;
+        R.ra[i] = *reinterpret_cast<const uint4*>(src);
+        R.amask |= 1u << i;
       } else {
-        ra[i] = make_uint4(0, 0, 0, 0);
+        R.ra[i] = make_uint4(0, 0, 0, 0);
       }
     }
 #pragma unroll
     for (int j = 0; j < BIT; ++j) {
-      rb[j] = (bval[j] && kin) ? *reinterpret_cast<const uint4*>(bptr[j] + k0) : make_uint4(0, 0, 0, 0);
+      R.rb[j] = (bval[j] && kin) ? *reinterpret_cast<const uint4*>(bptr[j] + k0) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store_lds = [&](int stage) {
+  auto store_lds = [&](Regs& R, int stage) {
     char* sA = smem + stage * STAGE;
     char* sB = sA + BM * LDS_ROW;
 #pragma unroll
     for (int i = 0; i < AIT; ++i) {
-      uint4 v = ra[i];
-      if (has_pro && (amask >> i & 1u)) v = prologue16<T>(v, p.sc, p.sh, aci, p.pro_act, p.slope);
+      uint4 v = R.ra[i];
+      if (has_pro && (R.amask >> i & 1u)) v = prologue16<T>(v, p.sc, p.sh, R.aci, p.pro_act, p.slope);
       *reinterpret_cast<uint4*>(sA + ((tid >> 3) + 32 * i) * LDS_ROW + ca * 16) = v;
     }
 #pragma unroll
     for (int j = 0; j < BIT; ++j)
-      *reinterpret_cast<uint4*>(sB + ((tid >> 3) + 32 * j) * LDS_ROW + ca * 16) = rb[j];
+      *reinterpret_cast<uint4*>(sB + ((tid >> 3) + 32 * j) * LDS_ROW + ca * 16) = R.rb[j];
   };
 
   floatx16 acc[FM][FN];
@@ -227,16 +231,8 @@ igemm_kernel(const ConvParams p) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  if (nsteps > 0) {
-    load_regs(kbeg);
-    store_lds(0);
-  }
-  __syncthreads();
-
   const int lrow = lane & 31, lhalf = lane >> 5;
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    if (s + 1 < nsteps) load_regs(kbeg + (s + 1) * BK);
+  auto compute = [&](int cur) {
     const char* sA = smem + cur * STAGE;
     const char* sB = sA + BM * LDS_ROW;
 #pragma unroll
@@ -275,7 +271,24 @@ igemm_kernel(const ConvParams p) {
         }
       }
     }
-    if (s + 1 < nsteps) store_lds(cur ^ 1);
+  };
+
+  if (nsteps > 0) {
+    load_regs(r0, kbeg);
+    store_lds(r0, 0);
+  }
+  if (nsteps > 1) load_regs(r1, kbeg + BK);
+  __syncthreads();
+  // step s: set (s&1) held step s (already in LDS stage s&1); set ((s+1)&1) holds step s+1
+  for (int s = 0; s < nsteps; s += 2) {
+    if (s + 2 < nsteps) load_regs(r0, kbeg + (s + 2) * BK);
+    compute(0);
+    if (s + 1 < nsteps) store_lds(r1, 1);
+    __syncthreads();
+    if (s + 1 >= nsteps) break;
+    if (s + 3 < nsteps) load_regs(r1, kbeg + (s + 3) * BK);
+    compute(1);
+    if (s + 2 < nsteps) store_lds(r0, 0);
     __syncthreads();
   }
 
@@ -644,9 +657,11 @@ template <typename T>
 static int launch_igemm(const Plan& pl, ConvParams& p, hipStream_t st) {
   dim3 grid(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
   const size_t lds = lds_bytes(pl.BM, pl.BN);
-#define STC_L(BM_, BN_, WM_, WN_)                                                          \
-  if (pl.BM == BM_ && pl.BN == BN_) {                                                      \
-    hipLaunchKernelGGL((igemm_kernel<T, BM_, BN_, WM_, WN_>), grid, dim3(256), lds, st, p); \
+  const bool pro = p.sc != nullptr || p.pro_act != 0;
+#define STC_L(BM_, BN_, WM_, WN_)                                                                  \
+  if (pl.BM == BM_ && pl.BN == BN_) {                                                              \
+    if (pro) hipLaunchKernelGGL((igemm_kernel<T, BM_, BN_, WM_, WN_, true>), grid, dim3(256), lds, st, p); \
+    else hipLaunchKernelGGL((igemm_kernel<T, BM_, BN_, WM_, WN_, false>), grid, dim3(256), lds, st, p);    \
   } else
   STC_L(128, 128, 2, 2)
   STC_L(128, 64, 2, 2)

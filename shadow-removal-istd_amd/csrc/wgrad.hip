@@ -38,6 +38,8 @@ struct WgradParams {
   int dact, gact;
   float dslope, gslope;
   float* ws;  // [nsplit][R][Ncol]
+  float* dW;  // direct output when nsplit == 1 (torch layout), else nullptr
+  int Cg_out;
   int mtiles, ntiles;
 };
 
@@ -238,6 +240,22 @@ wgrad_kernel(const WgradParams p) {
     __syncthreads();
   }
 
+  if (p.dW) {  // single pixel split: write torch layout dW[r][ci][kh][kw] directly
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = c0 + wn * 64 + 32 * j + li;
+      const int tt = n / p.Cg, cc = n - tt * p.Cg;
+      if (n >= p.Ncol || cc >= p.Cg_out) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = r0 + wm * 64 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          if (m < p.R) p.dW[((long long)m * p.Cg_out + cc) * 16 + tt] = acc[i][j][e];
+        }
+    }
+    return;
+  }
   float* slab = p.ws + (long long)split * p.R * p.Ncol;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -293,6 +311,7 @@ using namespace stc;
 extern "C" int64_t stc_conv_wgrad_workspace(int dtype, int B, int Hd, int Wd, int R, int Cg) {
   (void)dtype;
   const WgPlan pl = wg_plan(B * Hd * Wd, R, Cg);
+  if (pl.nsplit <= 1) return 0;  // written straight into dW
   return (int64_t)pl.nsplit * R * 16LL * Cg * 4;
 }
 
@@ -324,11 +343,19 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
   }
   const WgPlan pl = wg_plan(p.P, R, Cg);
   p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.nsplit = pl.nsplit; p.pchunk = pl.pchunk;
+  p.Cg_out = Cg_out;
+  dim3 grid(pl.mtiles * pl.ntiles, 1, pl.nsplit);
+  if (pl.nsplit <= 1) {
+    p.dW = dW;
+    if (dtype == STC_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, p);
+    STC_CHECK_LAUNCH();
+    return 0;
+  }
   const int64_t need = (int64_t)pl.nsplit * R * 16LL * Cg * 4;
   STC_REQUIRE(workspace && workspace_bytes >= need, "stc_conv_wgrad: workspace %lld < %lld",
               (long long)workspace_bytes, (long long)need);
   p.ws = (float*)workspace;
-  dim3 grid(pl.mtiles * pl.ntiles, 1, pl.nsplit);
   if (dtype == STC_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, p);
   STC_CHECK_LAUNCH();

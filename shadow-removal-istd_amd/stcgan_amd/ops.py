@@ -42,6 +42,7 @@ def _pro(pro):
 
 
 _timer = None  # when a list: conv() appends (tile name, flops, start event, end event) per launch
+_DEBUG_NO_PROLOGUE = False
 
 
 def plan_of(kind, B, gh, gw, cin, cout, dt):
@@ -60,6 +61,8 @@ def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=No
     l = lib()
     nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
     ws, nb = _ws(nbytes, dev)
+    if _DEBUG_NO_PROLOGUE:  # timing experiments only (wrong numerics); never set in tests/bench
+        pro, slope = None, None
     sc, sh = _pro(pro)
     timer = _timer
     if timer is not None:
@@ -159,6 +162,13 @@ def bn_eval_table(C, bn, scale_out, shift_out):
     check(lib().stc_bn_finalize(None, 0, C, ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
                                 ptr(bn.running_var), None, 0.0, float(bn.eps), None, None, ptr(scale_out),
                                 ptr(shift_out), stream()), "stc_bn_finalize(eval)")
+
+
+def bn_apply(B, xv, C, dt, table, y1, s1, y2=None, s2=1.0):
+    """y1 = act(x*scale+shift, s1) [, y2 = act(.., s2)]; table = (scale, shift) or None (identity)."""
+    sc, sh = _pro(table)
+    check(lib().stc_bn_apply(L.dtype_code(dt), B, xv, C, sc, sh, y1, float(s1),
+                             y2 if y2 is not None else L.NULL_VIEW, float(s2), stream()), "stc_bn_apply")
 
 
 def bn_backward(B, xv, C, dt, dxv, g1=None, s1=0.0, g2=None, s2=0.0, bn_state=None):

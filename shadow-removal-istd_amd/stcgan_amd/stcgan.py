@@ -82,8 +82,12 @@ class STCGAN(object):
                             lr=args.lr_D, betas=(args.beta1, args.beta2))
         self.decay_G = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_G, cooldown=10, min_lr=1e-7, factor=0.8)
         self.decay_D = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_D, cooldown=10, min_lr=1e-7, factor=0.8)
-        self.sync_G = parallel.GradAllReduce(list(self.G1.parameters()) + list(self.G2.parameters()))
-        self.sync_D = parallel.GradAllReduce(list(self.D1.parameters()) + list(self.D2.parameters()))
+        # one gradient exchange per network, launched from the backward as soon as that
+        # network's gradients are complete (one backward per step: STCGAN/stcgan.py:227,292)
+        self.sync_G = parallel.GradAllReduce([list(self.G2.parameters()), list(self.G1.parameters())])
+        self.sync_D = parallel.GradAllReduce([list(self.D2.parameters()), list(self.D1.parameters())])
+        self.sync_G.enable_overlap()
+        self.sync_D.enable_overlap()
 
         self.train_loader = train_loader
         self.valid_loader = valid_loader

@@ -37,14 +37,22 @@ def _worker(rank, world, port, out):
     st = fixture_state(ref.discriminator_state_template(4, 8), 13, "one")
     params = {k: v.clone().requires_grad_(not ref._is_buffer(k)) for k, v in st.items()}
     x = uniform((4, 4, 64, 64), 7)  # global batch 4, shard by rank
-    xs = x[rank * 2:(rank + 1) * 2]
-    out_t = ref.discriminator_forward(params, xs, True)
-    loss = ((out_t - 1.0) ** 2).mean()
-    loss.backward()
+    z = uniform((4, 4, 64, 64), 8)
     plist = [v for k, v in params.items() if v.requires_grad]
-    sync = parallel.GradAllReduce(plist, bucket_mb=0.01)  # several buckets
-    assert len(sync.buckets) > 1
+    half = len(plist) // 2
+    # two groups; the net is used twice in the graph (real + fake) but autograd sums the
+    # uses before accumulating, so each parameter's hook fires once per backward
+    sync = parallel.GradAllReduce([plist[:half], plist[half:]], bucket_mb=0.002)
+    assert all(len(b) > 1 for b in sync.buckets)  # several buckets per group
+    sync.enable_overlap()
+    sl = slice(rank * 2, (rank + 1) * 2)
+    out_a = ref.discriminator_forward(params, x[sl], True)
+    out_b = ref.discriminator_forward(params, z[sl], True)
+    loss = (((out_a - 1.0) ** 2).mean() + (out_b ** 2).mean()) * 0.5
+    loss.backward()
+    assert all(w is not None for w in sync.works)  # launched from the backward hooks
     sync()
+    assert sync.works == [None, None] and sync.count == [0, 0]
     if rank == 0:
         out.put([p.grad.clone() for p in plist])
     dist.barrier()
@@ -64,7 +72,14 @@ def test_grad_allreduce_matches_global_batch():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=300)
+    import queue
+    import time
+    got, t0 = None, time.time()
+    while got is None and time.time() - t0 < 300:
+        try:
+            got = q.get(timeout=1)
+        except queue.Empty:
+            assert all(p.exitcode in (None, 0) for p in procs), [p.exitcode for p in procs]
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
@@ -72,8 +87,13 @@ def test_grad_allreduce_matches_global_batch():
     st = fixture_state(ref.discriminator_state_template(4, 8), 13, "one")
     params = {k: v.clone().requires_grad_(not ref._is_buffer(k)) for k, v in st.items()}
     x = uniform((4, 4, 64, 64), 7)
-    outs = [ref.discriminator_forward(params, x[i * 2:(i + 1) * 2], True) for i in range(2)]
-    loss = sum(((o - 1.0) ** 2).mean() for o in outs) / 2
+    z = uniform((4, 4, 64, 64), 8)
+    loss = 0
+    for i in range(2):
+        sl = slice(i * 2, (i + 1) * 2)
+        out_a = ref.discriminator_forward(params, x[sl], True)
+        out_b = ref.discriminator_forward(params, z[sl], True)
+        loss = loss + (((out_a - 1.0) ** 2).mean() + (out_b ** 2).mean()) * 0.5 / 2
     loss.backward()
     want = [v.grad for k, v in params.items() if v.requires_grad]
     for g, w in zip(got, want):
