@@ -82,6 +82,22 @@ int64_t stc_conv_fwd_workspace(int dtype, int kind, int B, int Hg, int Wg, int C
  * the N <= 8 wave-per-pixel kernel (HBM-bound layers) instead of an MFMA tile. */
 int stc_conv_fwd_plan(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int32_t* out);
 
+/* Conv forward with the BatchNorm batch statistics of its output fused in (the reference's
+ * Conv2d/ConvTranspose2d -> BatchNorm2d pairs, STCGAN/networks.py:104-109,112-121,167-170,176-179).
+ * stats_part (optional): [stats_chunks][Cout][4] partials in stc_chan_stats format, merged by
+ * stc_bn_finalize.  bf16 operands run on the LDS-DMA MFMA kernel, which computes the partials
+ * in its epilogue (or in the split-K reduction); other cases run stc_conv_fwd + stc_chan_stats.
+ * force_plan (optional, tuning/tests): {tile config, ksplit} for the bf16 kernel.
+ * stc_conv_fwd_query returns the workspace bytes, the number of partial-stat chunks and the
+ * plan {BM, BN, ksplit, narrow_n, tile config} for the same arguments.                       */
+int stc_conv_fwd_query(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_f32,
+                       const int32_t* force_plan, int64_t* workspace_bytes, int32_t* stats_chunks,
+                       int32_t* plan_out);
+int stc_conv_fwd_ex(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
+                    stc_view y, const float* bias, int epi_tanh, int out_f32,
+                    float* stats_part, int stats_chunks, const int32_t* force_plan,
+                    void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---- weight gradient ---------------------------------------------------------
  * dW[r][ci][kh][kw] = sum_{b,oy,ox} D[b,oy,ox,r] * G[b, oy*s+kh-1, ox*s+kw-1, ci]
  *   Conv2d s2/s1 : D = dy (grid = output), G = x (input), s = stride

@@ -16,12 +16,12 @@ step() {  # step <name> <seconds> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout 300
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = debug ]; then
   step debug 300 python scripts/debug_nets.py G1 G2
-  step pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout 300
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
   step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
 fi
 if [ "$MODE" = prof ] || [ "$MODE" = all_prof ]; then
@@ -29,6 +29,16 @@ if [ "$MODE" = prof ] || [ "$MODE" = all_prof ]; then
   step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
        -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS}
 fi
+if [ "$MODE" = pmc ] || [ "$MODE" = all_prof ]; then
+  export TMPDIR=/tmp
+  PDT=${PMC_DTYPE:-bf16}
+  step pmc_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o g \
+       -- python scripts/g1g2_fwd.py --dtype $PDT
+  step pmc_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o g \
+       -- python scripts/g1g2_fwd.py --dtype $PDT
+  python scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic.json
+fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ] || [ "$MODE" = all_prof ]; then
   step bench 600 python bench.py --steps 5 --warmup 2
+  step bench_bf16 600 python bench.py --steps 5 --warmup 2 --dtype bf16 --no-cpu-baseline
 fi

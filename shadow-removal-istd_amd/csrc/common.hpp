@@ -101,4 +101,34 @@ __device__ __forceinline__ float dact(float n, float slope) { return n > 0.f ? 1
 
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// Implicit-GEMM geometry of each conv kind (tap offsets are affine in the tap index).
+struct Geometry {
+  int taps_lg_tw;   // lg of taps per row (2 -> 4x4 taps, 1 -> 2x2 taps)
+  int in_stride, os, nphase;
+  int offy[4], offx[4];
+  int stepy, stepx;
+};
+
+static inline Geometry geometry(int kind) {
+  Geometry g{};
+  switch (kind) {
+    case STC_CONV_S2:
+    case STC_CONV_S1:
+      g.taps_lg_tw = 2; g.in_stride = kind == STC_CONV_S2 ? 2 : 1; g.os = 1; g.nphase = 1;
+      g.offy[0] = -1; g.offx[0] = -1; g.stepy = 1; g.stepx = 1;
+      break;
+    case STC_CONV_S1_DGRAD:  // dx[i] = sum_k dy[i + 1 - k] w[k]
+      g.taps_lg_tw = 2; g.in_stride = 1; g.os = 1; g.nphase = 1;
+      g.offy[0] = 1; g.offx[0] = 1; g.stepy = -1; g.stepx = -1;
+      break;
+    case STC_CONVT_S2:  // out(2y+ph) = sum_t in(y + ph - t) w[(1-ph) + 2t]
+      g.taps_lg_tw = 1; g.in_stride = 1; g.os = 2; g.nphase = 4;
+      for (int z = 0; z < 4; ++z) { g.offy[z] = z >> 1; g.offx[z] = z & 1; }
+      g.stepy = -1; g.stepx = -1;
+      break;
+  }
+  return g;
+}
+
+
 }  // namespace stc

@@ -592,34 +592,6 @@ static bool launch_narrow_tiled(int kind, int B, ConvParams& p, hipStream_t st) 
 }
 
 // ------------------------------------------------------------------------- host
-struct Geometry {
-  int taps_lg_tw;   // lg of taps per row (2 -> 4x4 taps, 1 -> 2x2 taps)
-  int in_stride, os, nphase;
-  int offy[4], offx[4];
-  int stepy, stepx;
-};
-
-static Geometry geometry(int kind) {
-  Geometry g{};
-  switch (kind) {
-    case STC_CONV_S2:
-    case STC_CONV_S1:
-      g.taps_lg_tw = 2; g.in_stride = kind == STC_CONV_S2 ? 2 : 1; g.os = 1; g.nphase = 1;
-      g.offy[0] = -1; g.offx[0] = -1; g.stepy = 1; g.stepx = 1;
-      break;
-    case STC_CONV_S1_DGRAD:  // dx[i] = sum_k dy[i + 1 - k] w[k]
-      g.taps_lg_tw = 2; g.in_stride = 1; g.os = 1; g.nphase = 1;
-      g.offy[0] = 1; g.offx[0] = 1; g.stepy = -1; g.stepx = -1;
-      break;
-    case STC_CONVT_S2:  // out(2y+ph) = sum_t in(y + ph - t) w[(1-ph) + 2t]
-      g.taps_lg_tw = 1; g.in_stride = 1; g.os = 2; g.nphase = 4;
-      for (int z = 0; z < 4; ++z) { g.offy[z] = z >> 1; g.offx[z] = z & 1; }
-      g.stepy = -1; g.stepx = -1;
-      break;
-  }
-  return g;
-}
-
 static int ilog2_exact(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -689,14 +661,40 @@ static bool use_smalln(int dtype, int N, int K) {
   return N <= 8 && (long long)N * K * esz <= 64 * 1024;
 }
 
+namespace stc {
+bool bf16_conv_eligible(int kind, int B, const stc_view& x, int Cin, int Cout);
+int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_f32, const int32_t* force,
+                    int64_t* ws_bytes, int32_t* stats_chunks, int32_t* plan_out);
+int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
+                  const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
+                  const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st);
+bool bf16_narrow_eligible(int kind, int Cin, int Cout);
+int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout);
+int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
+                    const float* bias, int epi_tanh, int out_f32, void* ws, int64_t ws_bytes, hipStream_t st);
+}  // namespace stc
+
+// bf16 operands on the LDS-DMA kernel (igemm_bf16.hip) whenever the shape allows (no prologue,
+// N >= 16, 16-byte channel alignment); the query mirrors that decision for an NHWC input view.
+static bool bf16_path(int dtype, int kind, int Cin, int Cout) {
+  if (dtype != STC_BF16) return false;
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  return Cin % 8 == 0 && Cout >= 16 && Cout % 8 == 0 && Cout <= 2048 && !use_smalln(dtype, Cout, taps * Cin);
+}
+
 extern "C" int64_t stc_conv_fwd_workspace(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout) {
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   const int M = B * Hg * Wg, K = taps * Cin;
-  if (use_smalln(dtype, Cout, K)) return 0;
+  if (use_smalln(dtype, Cout, K))
+    return dtype == STC_BF16 && bf16_narrow_eligible(kind, Cin, Cout) ? bf16_narrow_workspace(kind, B, Hg, Wg, Cin, Cout) : 0;
+  int64_t ws_new = 0;
+  if (bf16_path(dtype, kind, Cin, Cout))  // the prologue form still runs the register-staged kernel: max of both
+    bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, &ws_new, nullptr, nullptr);
   const Plan pl = plan_for(dtype, M, Cout, K, g.nphase);
-  if (pl.ksplit <= 1) return 0;
-  return (int64_t)g.nphase * pl.ksplit * (int64_t)M * Cout * 4;
+  const int64_t ws_old = pl.ksplit <= 1 ? 0 : (int64_t)g.nphase * pl.ksplit * (int64_t)M * Cout * 4;
+  return std::max(ws_old, ws_new);
 }
 
 // out[0..3] = {BM, BN, ksplit, narrow-N path}; Hg x Wg is the GEMM grid (output grid for
@@ -710,9 +708,53 @@ extern "C" int stc_conv_fwd_plan(int dtype, int kind, int B, int Hg, int Wg, int
     out[0] = 1; out[1] = Cout; out[2] = 1; out[3] = 1;
     return 0;
   }
+  if (bf16_path(dtype, kind, Cin, Cout)) {
+    int32_t po[5];
+    bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, nullptr, po);
+    for (int i = 0; i < 4; ++i) out[i] = po[i];
+    return 0;
+  }
   const Plan pl = plan_for(dtype, M, Cout, K, g.nphase);
   out[0] = pl.BM; out[1] = pl.BN; out[2] = pl.ksplit; out[3] = 0;
   return 0;
+}
+
+// Forward conv with fused BatchNorm output statistics and an optional forced plan
+// {tile config, ksplit} (bf16 LDS-DMA kernel only; tuning / tests).  stats_part: [chunks][Cout][4]
+// in stc_chan_stats format (merged by stc_bn_finalize).  plan_out[5] = {BM, BN, ksplit, narrow, cfg}.
+extern "C" int stc_conv_fwd_query(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_f32,
+                                  const int32_t* force_plan, int64_t* workspace_bytes, int32_t* stats_chunks,
+                                  int32_t* plan_out) {
+  STC_REQUIRE(kind >= 0 && kind <= 3, "stc_conv_fwd_query: bad kind %d", kind);
+  const Geometry g = geometry(kind);
+  if (bf16_path(dtype, kind, Cin, Cout))
+    return bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, out_f32, force_plan, workspace_bytes, stats_chunks, plan_out);
+  const long long P = (long long)B * Hg * Wg * (g.nphase == 4 ? 4 : 1);
+  if (workspace_bytes) *workspace_bytes = stc_conv_fwd_workspace(dtype, kind, B, Hg, Wg, Cin, Cout);
+  if (stats_chunks) *stats_chunks = stc_chan_stats_chunks(1, 1, (int)std::min<long long>(P, 1 << 30));
+  if (plan_out) {
+    int32_t o[4];
+    stc_conv_fwd_plan(dtype, kind, B, Hg, Wg, Cin, Cout, o);
+    for (int i = 0; i < 4; ++i) plan_out[i] = o[i];
+    plan_out[4] = -1;
+  }
+  return 0;
+}
+
+extern "C" int stc_conv_fwd_ex(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
+                               stc_view y, const float* bias, int epi_tanh, int out_f32, float* stats_part,
+                               int stats_chunks, const int32_t* force_plan, void* workspace, int64_t workspace_bytes,
+                               void* stream) {
+  STC_REQUIRE(kind >= 0 && kind <= 3, "stc_conv_fwd_ex: bad kind %d", kind);
+  hipStream_t st = (hipStream_t)stream;
+  if (bf16_path(dtype, kind, Cin, Cout) && bf16_conv_eligible(kind, B, x, Cin, Cout))
+    return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, epi_tanh, out_f32, stats_part, stats_chunks,
+                         force_plan, workspace, workspace_bytes, st);
+  const int rc = stc_conv_fwd(dtype, kind, B, x, Cin, nullptr, nullptr, 0, 0.f, w_packed, Cout, y, bias, epi_tanh,
+                              out_f32, workspace, workspace_bytes, stream);
+  if (rc != 0 || stats_part == nullptr) return rc;
+  STC_REQUIRE(!out_f32 || dtype == STC_F32, "stc_conv_fwd_ex: stats of a non-activation output");
+  return stc_chan_stats(dtype, B, y, Cout, stats_part, stats_chunks, stream);
 }
 
 extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
@@ -753,6 +795,9 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
   if (p.M == 0 || Cout == 0) return 0;
   hipStream_t st0 = (hipStream_t)stream;
   if (use_smalln(dtype, Cout, K)) {
+    if (dtype == STC_BF16 && p.sc == nullptr && pro_act == 0 && bf16_narrow_eligible(kind, Cin, Cout))
+      return bf16_narrow_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, epi_tanh, out_f32, workspace, workspace_bytes,
+                             st0);
     p.mtiles = 1; p.ntiles = 1; p.ksplit = 1; p.kchunk = K;
     const int esz = dtype == STC_F32 ? 4 : 2;
     STC_REQUIRE(K % VEC == 0, "stc_conv_fwd: K=%d", K);
@@ -769,6 +814,9 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
     STC_CHECK_LAUNCH();
     return 0;
   }
+  if (dtype == STC_BF16 && p.sc == nullptr && pro_act == 0 && bf16_conv_eligible(kind, B, x, Cin, Cout))
+    return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, epi_tanh, out_f32, nullptr, 0, nullptr,
+                         workspace, workspace_bytes, st0);
   const Plan pl = plan_for(dtype, p.M, Cout, K, g.nphase);
   p.ksplit = pl.ksplit; p.kchunk = pl.kchunk; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles;
   if (pl.ksplit > 1) {

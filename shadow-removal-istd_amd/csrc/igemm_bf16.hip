@@ -1,0 +1,684 @@
+// bf16 implicit-GEMM 4x4 convolution on gfx950 MFMA, staged by LDS-DMA.
+//
+// Same problem family as igemm.hip (Conv2d k4 s2/s1, ConvTranspose2d k4 s2 as 4 phases,
+// and both input gradients), bf16 operands / fp32 accumulation:
+//   * operands move HBM/L2 -> LDS with buffer_load_dwordx4 ... lds (one 1 KiB wave
+//     instruction = 8 rows x 128 B of K), no VGPR round trip and no ds_write pass.
+//     Zero padding / K tails / rows past M come for free: their byte offset is put
+//     out of the buffer range, and the range check delivers zeros.
+//   * LDS image per stage: [rows][128 B] with the 16-byte chunk index XOR-swizzled by
+//     (row & 7) on the *source* side (the DMA image is lane-linear), so every
+//     ds_read_b128 lane group hits 16 distinct bank slots.
+//   * v_mfma_f32_16x16x32_bf16, wave tile (BM/WM) x (BN/WN); 2-stage ring, BK = 64:
+//     the DMA of K-step s+1 is in flight under the MFMAs of step s, one barrier per step.
+//   * epilogue: either fp32 split-K slabs, or + bias -> bf16 through an LDS tile and
+//     16-byte row stores (NHWC rows are contiguous channels), with the BatchNorm batch
+//     statistics of the tile fused in (two-pass: tile mean, then centred sum of
+//     squares, in fp32 from the accumulators) -> part[tile][n] = {count, 0, M2, mean},
+//     the format stc_bn_finalize merges (Chan's parallel variance).
+#include "common.hpp"
+
+namespace stc {
+
+struct GParams {
+  const char* a;
+  unsigned a_bytes;
+  int a_bs, a_rs, a_ps, a_co;  // elements (a_bytes < 2^31, so 32-bit offsets suffice)
+  int IH, IW, cin, lg_tw, in_stride;
+  int offy[4], offx[4];
+  int stepy, stepx;
+  int GH, GW, M, N, K;
+  int ksplit, kchunk;
+  const char* b;
+  unsigned b_bytes;
+  int b_phase_stride;
+  char* c;
+  long long c_bs, c_rs;
+  int c_ps, c_co, c_cs;
+  int os;
+  int oy0[4], ox0[4];
+  const float* bias;
+  int tanh_, vec_out, out_f32;
+  float* ws;
+  float* stats;
+  int nphase, mtiles, ntiles;
+};
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+using lds_vptr = __attribute__((address_space(3))) void*;
+
+constexpr unsigned OOB = 0x80000000u;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)lds_dst, 16, voff, 0, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN, int NST>
+__global__ void __launch_bounds__(64 * WM * WN)
+igemm_bf16_kernel(const GParams p) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int AG = BM / (8 * NW), BG = BN / (8 * NW);  // 1 KiB DMA pieces per wave per K-step
+  constexpr int STAGE = (BM + BN) * 128;
+  static_assert(AG * 8 * NW == BM && BG * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
+  static_assert(FM >= 1 && FN >= 1, "wave tile >= 16x16");
+  static_assert(NST == 2 || NST == 3, "2- or 3-stage ring");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int nwg = p.mtiles * p.ntiles;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int mt = bid / p.ntiles, nt = bid % p.ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int z = blockIdx.z;
+  const int ph = z / p.ksplit, split = z % p.ksplit;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nsteps = (kend - kbeg + 63) / 64;
+  const int GHW = p.GH * p.GW;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, (int)p.b_bytes, 0x00020000);
+
+  // ---- DMA lane roles: lane -> (row in its 8-row piece, source chunk) ; LDS slot = lane & 7
+  // Every offset is computed unconditionally and pushed out of range by OR-ing bit 31 where the
+  // element is padding (any offset >= 2^31 > num_records reads zeros): no divergent branches
+  // around the DMA instructions.
+  const int prow = lane >> 3;
+  const int schunk = (lane & 7) ^ prow;
+  int a_base[AG], a_y[AG], a_x[AG];
+#pragma unroll
+  for (int g = 0; g < AG; ++g) {
+    const int m = m0 + (wave * AG + g) * 8 + prow;
+    const int mm = m < p.M ? m : 0;
+    const int b = mm / GHW, rem = mm - b * GHW;
+    const int y = rem / p.GW, x = rem - y * p.GW;
+    a_base[g] = b * p.a_bs + p.a_co;
+    a_y[g] = m < p.M ? y * p.in_stride + p.offy[ph] : -(1 << 20);
+    a_x[g] = x * p.in_stride + p.offx[ph];
+  }
+  int b_row[BG];
+#pragma unroll
+  for (int g = 0; g < BG; ++g) {
+    const int n = n0 + (wave * BG + g) * 8 + prow;
+    b_row[g] = n < p.N ? ph * p.b_phase_stride + n * p.K : (1 << 30);
+  }
+  const int tw_mask = (1 << p.lg_tw) - 1;
+
+  auto issue = [&](int s, int stage) {
+    char* sA = smem + stage * STAGE;
+    char* sB = sA + BM * 128;
+    const int k = kbeg + s * 64 + schunk * 8;
+    const unsigned kpen = k < kend ? 0u : OOB;
+    const int t = k / p.cin, ci = k - t * p.cin;
+    const int dy = p.stepy * (t >> p.lg_tw), dx = p.stepx * (t & tw_mask);
+#pragma unroll
+    for (int g = 0; g < AG; ++g) {
+      const int iy = a_y[g] + dy, ix = a_x[g] + dx;
+      const unsigned pen = ((unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) ? kpen : OOB;
+      const unsigned off = (((unsigned)a_base[g] + (unsigned)iy * (unsigned)p.a_rs + (unsigned)ix * (unsigned)p.a_ps +
+                             (unsigned)ci) * 2u) | pen;
+      dma16(ra, sA + (wave * AG + g) * 1024, off);
+    }
+#pragma unroll
+    for (int g = 0; g < BG; ++g) {
+      const unsigned off = (((unsigned)b_row[g] + (unsigned)k) * 2u) | kpen;
+      dma16(rb, sB + (wave * BG + g) * 1024, off);
+    }
+  };
+
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets: row (l & 15), chunk 4*kk + (l >> 4), slot = chunk ^ (row & 7)
+  const int frow = lane & 15;
+  int rd_off[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) rd_off[kk] = frow * 128 + (((4 * kk + (lane >> 4)) ^ (frow & 7)) * 16);
+
+  auto compute = [&](int stage) {
+    const char* sA = smem + stage * STAGE + (wm * TM) * 128;
+    const char* sB = smem + stage * STAGE + BM * 128 + (wn * TN) * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + i * 16 * 128 + rd_off[kk]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sB + j * 16 * 128 + rd_off[kk]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if constexpr (NST == 2) {
+    // DMA of step s+1 lands under the MFMAs of step s; vmcnt(0) + barrier per step.
+    if (nsteps > 0) issue(0, 0);
+    for (int s = 0; s < nsteps; ++s) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+      compute(s & 1);
+    }
+  } else {
+    // 3-stage ring: two K-steps in flight; at step s wait only for step s's pieces (the
+    // AG+BG youngest, step s+1's, stay in flight across the raw barrier), then refill the
+    // stage that step s-1 read (every wave has passed the barrier, so those reads are done).
+    constexpr int P = AG + BG;
+    if (nsteps > 0) issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+    int cur = 0, nxt = 2;
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(P) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (s + 2 < nsteps) issue(s + 2, nxt);
+      compute(cur);
+      cur = cur == 2 ? 0 : cur + 1;
+      nxt = nxt == 2 ? 0 : nxt + 1;
+    }
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // accumulator element (i, j, r): row wm*TM + 16i + 4*(lane>>4) + r, column wn*TN + 16j + (lane&15)
+  const int rq = 4 * (lane >> 4), cl = lane & 15;
+  if (p.ws) {  // split-K / raw fp32 slab [z][M][N]
+    float* slab = p.ws + (long long)z * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * TN + 16 * j + cl;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * TM + 16 * i + rq + r;
+          if (m < p.M) slab[(long long)m * p.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+
+  float bz[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * TN + 16 * j + cl;
+    bz[j] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[i][j][r] + bz[j];
+        if (p.tanh_) v = tanhf(v);
+        acc[i][j][r] = v;
+      }
+
+  __syncthreads();  // every wave is done with the stage buffers
+  float* red = reinterpret_cast<float*>(smem);  // [WM][BN] partials, then [BN] column means
+  if (p.stats) {
+    const int mrem = p.M - m0;
+    const int nvalid = mrem < BM ? mrem : BM;
+    float s1[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + 16 * i + rq + r;
+          s += row < nvalid ? acc[i][j][r] : 0.f;
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      s1[j] = s;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + 16 * j + lane] = s1[j];
+    }
+    __syncthreads();
+    float* cmean = red + WM * BN;
+    for (int c = tid; c < BN; c += 64 * NW) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * BN + c];
+      cmean[c] = s / (float)nvalid;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const float mu = cmean[wn * TN + 16 * j + cl];
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + 16 * i + rq + r;
+          const float d = acc[i][j][r] - mu;
+          s += row < nvalid ? d * d : 0.f;
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      s1[j] = s;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + 16 * j + lane] = s1[j];
+    }
+    __syncthreads();
+    const long long tile = (long long)ph * p.mtiles + mt;
+    for (int c = tid; c < BN; c += 64 * NW) {
+      const int n = n0 + c;
+      if (n >= p.N) continue;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * BN + c];
+      float4 o = make_float4((float)nvalid, 0.f, s, cmean[c]);
+      *reinterpret_cast<float4*>(p.stats + (tile * p.N + n) * 4) = o;
+    }
+    __syncthreads();
+  }
+
+  if (p.vec_out) {
+    // bf16 tile through LDS: [BM][BN] with a 16-byte row pad, then 16-byte row stores
+    constexpr int PITCH = BN * 2 + 16;
+    char* tl = smem;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + 16 * i + rq + r, col = wn * TN + 16 * j + cl;
+          *reinterpret_cast<unsigned short*>(tl + row * PITCH + col * 2) = f2bf(acc[i][j][r]);
+        }
+    __syncthreads();
+    constexpr int CPR = BN / 8;  // 16-byte chunks per row
+    for (int q = tid; q < BM * CPR; q += 64 * NW) {
+      const int row = q / CPR, cc = q - row * CPR;
+      const int m = m0 + row, n = n0 + cc * 8;
+      if (m >= p.M || n >= p.N) continue;
+      const int b = m / GHW, rem = m - b * GHW;
+      const int y = rem / p.GW, x = rem - y * p.GW;
+      const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+      const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
+    }
+    return;
+  }
+  // general (strided / fp32) output: element stores
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * TM + 16 * i + rq + r;
+      if (m >= p.M) continue;
+      const int b = m / GHW, rem = m - b * GHW;
+      const int y = rem / p.GW, x = rem - y * p.GW;
+      const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+      const long long ro = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * TN + 16 * j + cl;
+        if (n >= p.N) continue;
+        const long long off = ro + (long long)(p.c_co + n) * p.c_cs;
+        if (p.out_f32) reinterpret_cast<float*>(p.c)[off] = acc[i][j][r];
+        else st1<bf16>(reinterpret_cast<bf16*>(p.c) + off, acc[i][j][r]);
+      }
+    }
+}
+
+// Split-K reduction: out[row] = sum_s slab[s][row] (+bias, tanh) -> bf16 16-byte stores, with the
+// BatchNorm partial statistics of the block's rows (shift = the block's first row, Chan-mergeable).
+// Thread = 8 consecutive channels of one GEMM row; the block walks a contiguous row range.
+__global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams p, int rows_per_block) {
+  const int CG = p.N / 8;  // channel groups (N % 8 == 0, N <= 2048)
+  const int RL = 256 / CG;  // rows in parallel
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  const long long R = (long long)p.nphase * p.M;  // rows = (phase, m)
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = min(R, r0 + rows_per_block);
+  const int n = cg * 8;
+  const int GHW = p.GH * p.GW;
+  float sh[8], s1[8], s2[8];
+  float cnt = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sh[e] = 0.f; s1[e] = 0.f; s2[e] = 0.f; }
+  float bz[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bz[e] = p.bias ? p.bias[n + e] : 0.f;
+  const long long MN = (long long)p.M * p.N;
+  auto rowval = [&](long long row, float* v) {
+    const int ph = (int)(row / p.M), m = (int)(row - (long long)ph * p.M);
+    const float* src = p.ws + ((long long)ph * p.ksplit * p.M + m) * p.N + n;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bz[e];
+    for (int s = 0; s < p.ksplit; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(src + s * MN);
+      const float4 b = *reinterpret_cast<const float4*>(src + s * MN + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    if (p.tanh_) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tanhf(v[e]);
+    }
+  };
+  if (rl < RL && r0 < r1 && p.stats) {
+    rowval(r0, sh);
+  }
+  if (rl < RL) {
+    for (long long row = r0 + rl; row < r1; row += RL) {
+      float v[8];
+      rowval(row, v);
+      const int ph = (int)(row / p.M), m = (int)(row - (long long)ph * p.M);
+      const int b = m / GHW, rem = m - b * GHW;
+      const int y = rem / p.GW, x = rem - y * p.GW;
+      const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+      const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
+      uint4 o;
+      o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+      o.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+      o.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
+      o.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[e] - sh[e];
+        s1[e] += d;
+        s2[e] += d * d;
+      }
+      cnt += 1.f;
+    }
+  }
+  if (!p.stats) return;
+  __shared__ float red[2][256][8];
+  __shared__ float rcnt[256];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][threadIdx.x][e] = s1[e]; red[1][threadIdx.x][e] = s2[e]; }
+  rcnt[threadIdx.x] = cnt;
+  __syncthreads();
+  if (rl == 0) {
+    float a1[8], a2[8], nn = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { a1[e] = 0.f; a2[e] = 0.f; }
+    for (int k = 0; k < RL; ++k) {
+      const int t = k * CG + cg;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { a1[e] += red[0][t][e]; a2[e] += red[1][t][e]; }
+      nn += rcnt[t];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      *reinterpret_cast<float4*>(p.stats + ((long long)blockIdx.x * p.N + n + e) * 4) = make_float4(nn, a1[e], a2[e], sh[e]);
+  }
+}
+
+// ------------------------------------------------------------------------- host
+struct BPlan {
+  int cfg;  // index into the tile table
+  int BM, BN, ksplit, kchunk, mtiles, ntiles;
+};
+
+struct TileCfg {
+  int BM, BN, WM, WN, NST;
+};
+static const TileCfg kTiles[] = {
+    {128, 128, 2, 2, 2},  // 0
+    {256, 128, 2, 2, 2},  // 1
+    {128, 64, 2, 2, 2},   // 2
+    {256, 64, 4, 1, 2},   // 3
+    {64, 128, 1, 4, 2},   // 4
+    {64, 64, 2, 2, 2},    // 5
+    {256, 256, 2, 4, 2},  // 6
+    {128, 256, 2, 4, 2},  // 7
+    {128, 128, 2, 2, 3},  // 8
+    {128, 256, 2, 4, 3},  // 9
+    {64, 128, 1, 4, 3},   // 10
+    {128, 64, 2, 2, 3},   // 11
+    {64, 64, 2, 2, 3},    // 12
+    {256, 128, 4, 2, 3},  // 13
+};
+constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+
+static size_t bf16_lds_bytes(int cfg) {
+  const TileCfg& t = kTiles[cfg];
+  size_t stage = (size_t)t.NST * (t.BM + t.BN) * 128;
+  size_t epi = (size_t)t.BM * (t.BN * 2 + 16);
+  size_t red = (size_t)(t.WM + 1) * t.BN * 4;
+  return std::max(stage, std::max(epi, red));
+}
+
+// Tile / split-K choice (fitted to the sweep of scripts/tune_bf16.py over one train step, see
+// profiles/): prefer the largest tile that still gives a full wave of workgroups (about one
+// 8-wave block or two 4-wave blocks per CU), splitting K only when no tile does.
+static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force_ks, bool allow_split) {
+  BPlan pl{};
+  auto tiles = [&](int c) { return (long long)cdiv(M, kTiles[c].BM) * cdiv(N, kTiles[c].BN) * nphase; };
+  const int ksteps = cdiv(K, 64);
+  int cfg = -1, ks = 1;
+  if (force_cfg >= 0 && force_cfg < kNumTiles) {
+    cfg = force_cfg;
+    ks = force_ks > 0 ? force_ks : 1;
+  } else {
+    int order[4], no = 0;
+    if (N >= 256) {
+      if ((long long)M * nphase >= 8192) { order[0] = 6; order[1] = 0; order[2] = 4; order[3] = 5; }
+      else { order[0] = 0; order[1] = 4; order[2] = 12; order[3] = 5; }
+      no = 4;
+    } else if (N >= 128) {
+      order[0] = 0; order[1] = 4; order[2] = 5; no = 3;
+    } else if (K <= 512) {
+      order[0] = 2; order[1] = 5; no = 2;
+    } else {
+      order[0] = 5; order[1] = 2; no = 2;
+    }
+    for (int k = 1; k <= 8 && cfg < 0; k *= 2) {
+      if (k > 1 && (ksteps / k < 8 || !allow_split)) break;
+      for (int i = 0; i < no; ++i) {
+        const int c = order[i];
+        const long long need = (c == 6 || c == 7 || c == 9) ? 240 : 400;
+        if (tiles(c) * k >= need) { cfg = c; ks = k; break; }
+      }
+    }
+    if (cfg < 0) {
+      cfg = order[no - 1];
+      ks = 1;
+      while (allow_split && tiles(cfg) * ks < 400 && ks < 8 && ksteps / (ks * 2) >= 8) ks *= 2;
+    }
+  }
+  if (!allow_split) ks = 1;
+  const TileCfg& t = kTiles[cfg];
+  pl.cfg = cfg;
+  pl.BM = t.BM;
+  pl.BN = t.BN;
+  pl.mtiles = cdiv(M, t.BM);
+  pl.ntiles = cdiv(N, t.BN);
+  pl.kchunk = cdiv(ksteps, ks) * 64;
+  pl.ksplit = cdiv(K, pl.kchunk);
+  return pl;
+}
+
+static int reduce_rows_per_block(long long rows, int N) {
+  const int RL = 256 / (N / 8);
+  long long blocks = std::min<long long>(1024, std::max<long long>(1, rows / std::max(RL, 4)));
+  return (int)((rows + blocks - 1) / blocks);
+}
+
+}  // namespace stc
+
+using namespace stc;
+
+namespace stc {
+
+struct Bf16Problem {
+  int M, N, K, nphase;
+  BPlan pl;
+  bool vec_out;
+  int64_t ws_bytes;
+  int stats_chunks;
+  int reduce_rows;
+};
+
+// Shared planning for query and launch.
+static Bf16Problem bf16_problem(int M, int N, int K, int nphase, const int32_t* force, bool vec_out) {
+  Bf16Problem pr{};
+  pr.M = M; pr.N = N; pr.K = K; pr.nphase = nphase;
+  pr.pl = bf16_plan(M, N, K, nphase, force ? force[0] : -1, force ? force[1] : 0, vec_out);
+  pr.vec_out = vec_out;
+  if (pr.pl.ksplit > 1) {
+    pr.ws_bytes = (int64_t)nphase * pr.pl.ksplit * (int64_t)M * N * 4;
+    const long long rows = (long long)nphase * M;
+    pr.reduce_rows = reduce_rows_per_block(rows, N);
+    pr.stats_chunks = (int)((rows + pr.reduce_rows - 1) / pr.reduce_rows);
+  } else {
+    pr.ws_bytes = 0;
+    pr.stats_chunks = nphase * pr.pl.mtiles;
+  }
+  return pr;
+}
+
+bool bf16_igemm_eligible(int N, int K) { return N >= 16 && N % 8 == 0 && N <= 2048 && K % 8 == 0; }
+
+int bf16_igemm_query(int M, int N, int K, int nphase, const int32_t* force, int64_t* ws_bytes, int32_t* stats_chunks,
+                     int32_t* plan_out) {
+  Bf16Problem pr = bf16_problem(M, N, K, nphase, force, true);
+  if (ws_bytes) *ws_bytes = pr.ws_bytes;
+  if (stats_chunks) *stats_chunks = pr.stats_chunks;
+  if (plan_out) {
+    plan_out[0] = pr.pl.BM; plan_out[1] = pr.pl.BN; plan_out[2] = pr.pl.ksplit; plan_out[3] = 0;
+    plan_out[4] = pr.pl.cfg;
+  }
+  return 0;
+}
+
+// p: filled by the caller (geometry, operands, output); returns 0 or error.
+int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_bytes, float* stats, int stats_chunks,
+                      hipStream_t st) {
+  Bf16Problem pr = bf16_problem(p.M, p.N, p.K, p.nphase, force, p.vec_out != 0);
+  const BPlan& pl = pr.pl;
+  p.ksplit = pl.ksplit; p.kchunk = pl.kchunk; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles;
+  p.stats = nullptr;
+  p.ws = nullptr;
+  if (pl.ksplit > 1) {
+    STC_REQUIRE(ws && ws_bytes >= pr.ws_bytes, "bf16 igemm: workspace %lld < %lld bytes", (long long)ws_bytes,
+                (long long)pr.ws_bytes);
+    p.ws = (float*)ws;
+  } else {
+    p.stats = stats;
+  }
+  if (stats) STC_REQUIRE(stats_chunks >= pr.stats_chunks, "bf16 igemm: stats chunks %d < %d", stats_chunks, pr.stats_chunks);
+  dim3 grid(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
+  const size_t lds = bf16_lds_bytes(pl.cfg);
+#define STC_B(I, BM_, BN_, WM_, WN_, NST_)                                                                  \
+  case I:                                                                                                   \
+    hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
+    break;
+  switch (pl.cfg) {
+    STC_B(0, 128, 128, 2, 2, 2)
+    STC_B(1, 256, 128, 2, 2, 2)
+    STC_B(2, 128, 64, 2, 2, 2)
+    STC_B(3, 256, 64, 4, 1, 2)
+    STC_B(4, 64, 128, 1, 4, 2)
+    STC_B(5, 64, 64, 2, 2, 2)
+    STC_B(6, 256, 256, 2, 4, 2)
+    STC_B(7, 128, 256, 2, 4, 2)
+    STC_B(8, 128, 128, 2, 2, 3)
+    STC_B(9, 128, 256, 2, 4, 3)
+    STC_B(10, 64, 128, 1, 4, 3)
+    STC_B(11, 128, 64, 2, 2, 3)
+    STC_B(12, 64, 64, 2, 2, 3)
+    STC_B(13, 256, 128, 4, 2, 3)
+    default:
+      return fail(-1, "bf16 igemm: bad tile config %d", pl.cfg);
+  }
+#undef STC_B
+  STC_CHECK_LAUNCH();
+  if (pl.ksplit > 1) {
+    STC_REQUIRE(p.vec_out, "bf16 igemm: split-K needs a 16-byte aligned NHWC bf16 output");
+    p.stats = stats;
+    const long long rows = (long long)p.nphase * p.M;
+    const int blocks = (int)((rows + pr.reduce_rows - 1) / pr.reduce_rows);
+    hipLaunchKernelGGL(splitk_reduce_stats_kernel, dim3(blocks), dim3(256), 0, st, p, pr.reduce_rows);
+    STC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// ---- conv-level wrappers (geometry -> GParams), used by stc_conv_fwd_query / stc_conv_fwd_ex
+static bool vec_out_ok(const stc_view& y, int out_f32) {
+  return !out_f32 && y.cs == 1 && y.co % 8 == 0 && y.ps % 8 == 0 && y.rs % 8 == 0 && y.bs % 8 == 0 &&
+         ((uintptr_t)y.p & 15) == 0;
+}
+
+bool bf16_conv_eligible(int kind, int B, const stc_view& x, int Cin, int Cout) {
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  const long long a_bytes = (long long)B * x.bs * 2;
+  const long long b_bytes = (long long)g.nphase * Cout * taps * Cin * 2;
+  return bf16_igemm_eligible(Cout, taps * Cin) && Cin % 8 == 0 && x.cs == 1 && x.co % 8 == 0 && x.ps % 8 == 0 &&
+         a_bytes < (1ll << 31) && b_bytes < (1ll << 31);
+}
+
+int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_f32, const int32_t* force,
+                    int64_t* ws_bytes, int32_t* stats_chunks, int32_t* plan_out) {
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  Bf16Problem pr = bf16_problem(B * Hg * Wg, Cout, taps * Cin, g.nphase, force, !out_f32);
+  if (ws_bytes) *ws_bytes = pr.ws_bytes;
+  if (stats_chunks) *stats_chunks = pr.stats_chunks;
+  if (plan_out) {
+    plan_out[0] = pr.pl.BM; plan_out[1] = pr.pl.BN; plan_out[2] = pr.pl.ksplit; plan_out[3] = 0;
+    plan_out[4] = pr.pl.cfg;
+  }
+  return 0;
+}
+
+int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
+                  const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
+                  const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st) {
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  GParams p{};
+  p.a = (const char*)x.p;
+  p.a_bytes = (unsigned)((long long)B * x.bs * 2);
+  p.a_bs = (int)x.bs; p.a_rs = (int)x.rs; p.a_ps = x.ps; p.a_co = x.co;
+  p.IH = x.H; p.IW = x.W;
+  p.cin = Cin; p.lg_tw = g.taps_lg_tw; p.in_stride = g.in_stride;
+  for (int i = 0; i < 4; ++i) { p.offy[i] = g.offy[i]; p.offx[i] = g.offx[i]; }
+  p.stepy = g.stepy; p.stepx = g.stepx;
+  if (kind == STC_CONVT_S2) { p.GH = x.H; p.GW = x.W; }
+  else { p.GH = y.H; p.GW = y.W; }
+  p.M = B * p.GH * p.GW; p.N = Cout; p.K = taps * Cin;
+  p.b = (const char*)w_packed;
+  p.b_phase_stride = Cout * p.K;
+  p.b_bytes = (unsigned)((long long)g.nphase * p.b_phase_stride * 2);
+  p.c = (char*)y.p; p.c_bs = y.bs; p.c_rs = y.rs; p.c_ps = y.ps; p.c_co = y.co; p.c_cs = y.cs;
+  p.os = g.os;
+  for (int i = 0; i < 4; ++i) { p.oy0[i] = g.nphase == 4 ? (i >> 1) : 0; p.ox0[i] = g.nphase == 4 ? (i & 1) : 0; }
+  p.bias = bias; p.tanh_ = epi_tanh; p.out_f32 = out_f32;
+  p.vec_out = vec_out_ok(y, out_f32) && Cout % 8 == 0 ? 1 : 0;
+  p.nphase = g.nphase;
+  if (p.M == 0 || Cout == 0) return 0;
+  if (!p.vec_out) STC_REQUIRE(!stats || out_f32 == 0, "bf16 conv: stats need a bf16 output");
+  return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st);
+}
+
+}  // namespace stc

@@ -1,0 +1,296 @@
+// Narrow-N bf16 convolutions on MFMA with an LDS halo tile (gfx950).
+//
+// The layers with N <= 8 output channels on the ST-CGAN path are HBM-bound on their input:
+//   * the generator output ConvTranspose2d (128 -> 1|3 channels, 128^2 -> 256^2, + bias, tanh;
+//     STCGAN/networks.py:112-116) and the input gradients of the first Conv2d layers (N = 8,
+//     padded 3/4/7 channels) -- ConvT geometry, 4 sub-pixel phases;
+//   * the PatchGAN logits Conv2d k4 s1 (512 -> 1, 31^2 -> 30^2, + bias; networks.py:183-184).
+// An im2col GEMM would re-read each input element 9-16x through L2.  Here a block stages a
+// (TY+halo) x (16+halo) pixel tile of one 64-channel chunk in LDS once (LDS-DMA, XOR-swizzled
+// 128-B pixel rows), and every output grid point's whole 3x3 (ConvT) / 4x4 (conv s1)
+// neighbourhood is read from that tile.  The reduction runs on v_mfma_f32_16x16x32_bf16 with
+// the MFMA M dimension = 16 consecutive grid points of a row and the N dimension = all
+// (phase, channel) outputs of a grid point (4N <= 32 for ConvT): per neighbour offset one
+// MFMA, whose B fragment holds the weights of the (phase, tap) pairs that read that
+// neighbour (zeros elsewhere).  Long reductions (the 8192-deep logits layer) split the
+// channel chunks over blocks and reduce fp32 partials in a second pass.
+#include "common.hpp"
+
+namespace stc {
+
+struct HParams {
+  const char* a;
+  unsigned a_bytes;
+  int a_bs, a_rs, a_ps, a_co;  // elements
+  int IH, IW, cin;
+  int GH, GW, N, NP;           // grid (output grid for conv s1, input grid for ConvT); N' = columns
+  const bf16* w;               // packed [phase][N][taps][cin]
+  int w_phase_stride;
+  char* c;
+  long long c_bs, c_rs;
+  int c_ps, c_co, c_cs;
+  const float* bias;
+  int tanh_, out_f32;
+  int tiles_x, tiles_per_img;
+  int chunks_per_split, nsplit;
+  float* ws;  // [split][Mtot][NP] when nsplit > 1
+  long long Mtot;  // B * GH * GW
+};
+
+typedef __bf16 bf16x8_h __attribute__((ext_vector_type(8)));
+using lds_vptr_h = __attribute__((address_space(3))) void*;
+
+__device__ __forceinline__ void hdma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr_h)lds_dst, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ void store_out(const HParams& p, long long off, float v) {
+  if (p.out_f32) reinterpret_cast<float*>(p.c)[off] = v;
+  else st1<bf16>(reinterpret_cast<bf16*>(p.c) + off, v);
+}
+
+// GEOM 0: ConvT k4 s2 (4 phases, 3x3 neighbourhood, NB column blocks of 16: N' = 4N <= 16*NB)
+// GEOM 1: Conv k4 s1 (16 taps, 4x4 neighbourhood, N' = N <= 16)
+template <int GEOM, int NB, int TY>
+__global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
+  constexpr int TX = 16;
+  constexpr int HALO = GEOM == 0 ? 2 : 3;
+  constexpr int RY = TY + HALO, RX = TX + HALO;
+  constexpr int NPIX = RY * RX;
+  constexpr int PIECES = (NPIX + 7) / 8;  // 1 KiB DMA pieces (8 pixels x 128 B)
+  constexpr int STAGE = PIECES * 1024;
+  constexpr int NBR = GEOM == 0 ? 9 : 16;  // neighbour offsets
+  constexpr int ROWS = TY / 4;             // grid rows per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.x / p.tiles_per_img, tix = blockIdx.x % p.tiles_per_img;
+  const int y0 = (tix / p.tiles_x) * TY, x0 = (tix % p.tiles_x) * TX;
+  const int split = blockIdx.y;
+  const int nchunks = p.cin / 64;
+  const int cbeg = split * p.chunks_per_split;
+  const int cend = min(nchunks, cbeg + p.chunks_per_split);
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, (short)0, (int)p.a_bytes, 0x00020000);
+  const unsigned OOBV = 0x80000000u;
+  const int abase = img * p.a_bs + p.a_co;
+  const int schunk = (lane & 7) ^ (lane >> 3);
+
+  auto issue = [&](int chunk, int stage) {
+    char* dst = smem + stage * STAGE;
+    const int ci = chunk * 64 + schunk * 8;
+    for (int pc = wave; pc < PIECES; pc += 4) {
+      const int pix = pc * 8 + (lane >> 3);
+      const int py = pix / RX, px = pix - py * RX;
+      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+      const bool ok = pix < NPIX && (unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW;
+      const unsigned off = (((unsigned)abase + (unsigned)iy * (unsigned)p.a_rs + (unsigned)ix * (unsigned)p.a_ps +
+                             (unsigned)ci) * 2u) | (ok ? 0u : OOBV);
+      hdma16(ra, dst + pc * 1024, off);
+    }
+  };
+
+  // B fragment of (neighbour nb, column block j, half kk) for this lane: column n' = 16j + (lane & 15),
+  // k = 8*(lane>>4) .. +8 within the 32-channel half.
+  auto load_b = [&](int chunk, int nb, int j, int kk) -> bf16x8_h {
+    const int np = 16 * j + (lane & 15);
+    const int c = chunk * 64 + kk * 32 + 8 * (lane >> 4);
+    int tap = -1, ph = 0, n = np;
+    if (GEOM == 0) {
+      const int dy = nb / 3 - 1, dx = nb % 3 - 1;
+      ph = np / p.N;
+      n = np - ph * p.N;
+      const int ty = (ph >> 1) - dy, tx = (ph & 1) - dx;
+      if (np < p.NP && ty >= 0 && ty <= 1 && tx >= 0 && tx <= 1) tap = ty * 2 + tx;
+    } else {
+      if (np < p.NP) tap = nb;  // tap index = (dy+1)*4 + (dx+1)
+    }
+    bf16x8_h v;
+    if (tap >= 0) {
+      v = *reinterpret_cast<const bf16x8_h*>(p.w + (long long)ph * p.w_phase_stride +
+                                             ((long long)n * (GEOM == 0 ? 4 : 16) + tap) * p.cin + c);
+    } else {
+      v = bf16x8_h{};
+    }
+    return v;
+  };
+
+  floatx4 acc[ROWS][NB];
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[r][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int gx = lane & 15;
+  if (cbeg < cend) issue(cbeg, 0);
+  int stage = 0;
+  for (int ch = cbeg; ch < cend; ++ch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ch + 1 < cend) issue(ch + 1, stage ^ 1);
+    const char* sT = smem + stage * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int cslot = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int nb = 0; nb < NBR; ++nb) {
+        const int dy = GEOM == 0 ? nb / 3 - 1 : nb / 4 - 1;
+        const int dx = GEOM == 0 ? nb % 3 - 1 : nb % 4 - 1;
+        bf16x8_h bfr[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) bfr[j] = load_b(ch, nb, j, kk);
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+          const int py = wave * ROWS + r + dy + 1, px = gx + dx + 1;
+          const int pix = py * RX + px;
+          const bf16x8_h af = *reinterpret_cast<const bf16x8_h*>(sT + pix * 128 + ((cslot ^ (pix & 7)) * 16));
+#pragma unroll
+          for (int j = 0; j < NB; ++j) acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[r][j], 0, 0, 0);
+        }
+      }
+    }
+    stage ^= 1;
+  }
+
+  // ---- epilogue: acc[r][j][e] = grid point (y0 + wave*ROWS + r, x0 + 4*(lane>>4) + e), column 16j + (lane&15)
+  const int np_l = lane & 15;
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    const int gy = y0 + wave * ROWS + r;
+    if (gy >= p.GH) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int gxx = x0 + 4 * (lane >> 4) + e;
+      if (gxx >= p.GW) continue;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int np = 16 * j + np_l;
+        if (np >= p.NP) continue;
+        float v = acc[r][j][e];
+        if (p.nsplit > 1) {
+          const long long m = ((long long)img * p.GH + gy) * p.GW + gxx;
+          p.ws[((long long)split * p.Mtot + m) * p.NP + np] = v;
+          continue;
+        }
+        int ph = 0, n = np;
+        if (GEOM == 0) { ph = np / p.N; n = np - ph * p.N; }
+        if (p.bias) v += p.bias[n];
+        if (p.tanh_) v = tanhf(v);
+        const int oy = GEOM == 0 ? 2 * gy + (ph >> 1) : gy;
+        const int ox = GEOM == 0 ? 2 * gxx + (ph & 1) : gxx;
+        store_out(p, (long long)img * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps +
+                         (long long)(p.c_co + n) * p.c_cs, v);
+      }
+    }
+  }
+}
+
+// split-K combine: out = epi(sum_s ws[s][m][n'])
+template <int GEOM>
+__global__ void narrow_reduce_kernel(const HParams p, int B) {
+  const long long total = p.Mtot * p.NP;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int np = (int)(idx % p.NP);
+    const long long m = idx / p.NP;
+    float v = 0.f;
+    for (int s = 0; s < p.nsplit; ++s) v += p.ws[(long long)s * total + idx];
+    int ph = 0, n = np;
+    if (GEOM == 0) { ph = np / p.N; n = np - ph * p.N; }
+    if (p.bias) v += p.bias[n];
+    if (p.tanh_) v = tanhf(v);
+    const int img = (int)(m / ((long long)p.GH * p.GW));
+    const int rem = (int)(m - (long long)img * p.GH * p.GW);
+    const int gy = rem / p.GW, gx = rem - gy * p.GW;
+    const int oy = GEOM == 0 ? 2 * gy + (ph >> 1) : gy;
+    const int ox = GEOM == 0 ? 2 * gx + (ph & 1) : gx;
+    store_out(p, (long long)img * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps +
+                     (long long)(p.c_co + n) * p.c_cs, v);
+  }
+}
+
+// ------------------------------------------------------------------------- host
+static size_t halo_lds(int geom, int ty) {
+  const int halo = geom == 0 ? 2 : 3;
+  const int npix = (ty + halo) * (16 + halo);
+  return 2 * (size_t)((npix + 7) / 8) * 1024;
+}
+
+// Narrow plan: {ty, nsplit}.  Enough blocks to cover the chip ~2x.
+static void narrow_plan(int geom, int B, int GH, int GW, int cin, int* ty, int* nsplit) {
+  *ty = 16;
+  const int nchunks = cin / 64;
+  const long long blocks = (long long)B * cdiv(GH, 16) * cdiv(GW, 16);
+  int ns = 1;
+  while (blocks * ns < 1024 && ns * 2 <= nchunks) ns *= 2;
+  *nsplit = ns;
+}
+
+bool bf16_narrow_eligible(int kind, int Cin, int Cout) {
+  if (kind != STC_CONVT_S2 && kind != STC_CONV_S1) return false;
+  if (Cin % 64 != 0) return false;
+  return kind == STC_CONVT_S2 ? Cout <= 8 : Cout <= 16;
+}
+
+int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout) {
+  const int geom = kind == STC_CONVT_S2 ? 0 : 1;
+  int ty, ns;
+  narrow_plan(geom, B, GH, GW, Cin, &ty, &ns);
+  if (ns <= 1) return 0;
+  const int np = geom == 0 ? 4 * Cout : Cout;
+  return (int64_t)ns * B * GH * GW * np * 4;
+}
+
+int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
+                    const float* bias, int epi_tanh, int out_f32, void* ws, int64_t ws_bytes, hipStream_t st) {
+  const int geom = kind == STC_CONVT_S2 ? 0 : 1;
+  HParams p{};
+  p.a = (const char*)x.p;
+  const long long a_bytes = (long long)B * x.bs * 2;
+  STC_REQUIRE(a_bytes < (1ll << 31) && x.cs == 1 && x.ps % 8 == 0 && x.co % 8 == 0,
+              "narrow bf16: input view must be NHWC, 16-byte aligned, < 2 GiB");
+  p.a_bytes = (unsigned)a_bytes;
+  p.a_bs = (int)x.bs; p.a_rs = (int)x.rs; p.a_ps = x.ps; p.a_co = x.co;
+  p.IH = x.H; p.IW = x.W; p.cin = Cin;
+  if (geom == 0) { p.GH = x.H; p.GW = x.W; }
+  else { p.GH = y.H; p.GW = y.W; }
+  p.N = Cout;
+  p.NP = geom == 0 ? 4 * Cout : Cout;
+  p.w = (const bf16*)w_packed;
+  p.w_phase_stride = Cout * (geom == 0 ? 4 : 16) * Cin;
+  p.c = (char*)y.p; p.c_bs = y.bs; p.c_rs = y.rs; p.c_ps = y.ps; p.c_co = y.co; p.c_cs = y.cs;
+  p.bias = bias; p.tanh_ = epi_tanh; p.out_f32 = out_f32;
+  p.Mtot = (long long)B * p.GH * p.GW;
+  int ty, ns;
+  narrow_plan(geom, B, p.GH, p.GW, Cin, &ty, &ns);
+  p.tiles_x = cdiv(p.GW, 16);
+  p.tiles_per_img = p.tiles_x * cdiv(p.GH, ty);
+  const int nchunks = Cin / 64;
+  p.chunks_per_split = cdiv(nchunks, ns);
+  p.nsplit = cdiv(nchunks, p.chunks_per_split);
+  if (p.nsplit > 1) {
+    const int64_t need = (int64_t)p.nsplit * B * p.GH * p.GW * p.NP * 4;
+    STC_REQUIRE(ws && ws_bytes >= need, "narrow bf16: workspace %lld < %lld", (long long)ws_bytes, (long long)need);
+    p.ws = (float*)ws;
+  }
+  if ((long long)B * p.GH * p.GW == 0) return 0;
+  dim3 grid((unsigned)(B * p.tiles_per_img), (unsigned)p.nsplit);
+  const size_t lds = halo_lds(geom, ty);
+  if (geom == 0) {
+    if (p.NP <= 16) hipLaunchKernelGGL((narrow_halo_kernel<0, 1, 16>), grid, dim3(256), lds, st, p);
+    else hipLaunchKernelGGL((narrow_halo_kernel<0, 2, 16>), grid, dim3(256), lds, st, p);
+  } else {
+    hipLaunchKernelGGL((narrow_halo_kernel<1, 1, 16>), grid, dim3(256), lds, st, p);
+  }
+  STC_CHECK_LAUNCH();
+  if (p.nsplit > 1) {
+    const long long total = (long long)B * p.GH * p.GW * p.NP;
+    const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+    if (geom == 0) hipLaunchKernelGGL(narrow_reduce_kernel<0>, dim3(blocks), dim3(256), 0, st, p, B);
+    else hipLaunchKernelGGL(narrow_reduce_kernel<1>, dim3(blocks), dim3(256), 0, st, p, B);
+    STC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // namespace stc

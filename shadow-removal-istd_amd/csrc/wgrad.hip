@@ -271,20 +271,27 @@ wgrad_kernel(const WgradParams p) {
     }
 }
 
-// dW[r][ci][kh][kw] = sum_s ws[s][r][(kh*4+kw)*Cg + ci]
+// dW[r][ci][kh][kw] = sum_s ws[s][r][(kh*4+kw)*Cg + ci]: one thread per (r, ci), the 16 taps in
+// registers; slab reads are coalesced over ci, each thread writes its 64 contiguous bytes of dW.
 __global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int R, int Cg, int Cg_out, float* dW) {
-  const long long total = (long long)R * Cg_out * 16;
+  const long long total = (long long)R * Cg_out;
   const long long Ncol = 16LL * Cg;
+  const long long slab = (long long)R * Ncol;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
-    const int tap = (int)(idx & 15);
-    const long long rc = idx >> 4;
-    const int ci = (int)(rc % Cg_out);
-    const int r = (int)(rc / Cg_out);
-    const float* src = ws + (long long)r * Ncol + (long long)tap * Cg + ci;
-    float v = 0.f;
-    for (int s = 0; s < nsplit; ++s) v += src[(long long)s * R * Ncol];
-    dW[idx] = v;
+    const int ci = (int)(idx % Cg_out);
+    const int r = (int)(idx / Cg_out);
+    const float* src = ws + (long long)r * Ncol + ci;
+    float v[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) v[t] = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) v[t] += src[(long long)s * slab + (long long)t * Cg];
+    }
+    float4* o = reinterpret_cast<float4*>(dW + idx * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
   }
 }
 
@@ -306,13 +313,21 @@ static WgPlan wg_plan(int P, int R, int Cg) {
 
 }  // namespace stc
 
+namespace stc {
+bool wgrad_bf16_eligible(int B, const stc_view& D, int R, const stc_view& G, int Cg);
+int64_t wgrad_bf16_workspace(int B, int Hd, int Wd, int R, int Cg);
+int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_out, float* dW, void* workspace,
+               int64_t workspace_bytes, hipStream_t st);
+}  // namespace stc
+
 using namespace stc;
 
 extern "C" int64_t stc_conv_wgrad_workspace(int dtype, int B, int Hd, int Wd, int R, int Cg) {
-  (void)dtype;
   const WgPlan pl = wg_plan(B * Hd * Wd, R, Cg);
-  if (pl.nsplit <= 1) return 0;  // written straight into dW
-  return (int64_t)pl.nsplit * R * 16LL * Cg * 4;
+  const int64_t ws_reg = pl.nsplit <= 1 ? 0 : (int64_t)pl.nsplit * R * 16LL * Cg * 4;  // 0: straight into dW
+  // bf16 without prologues runs the LDS-DMA kernel (wgrad_bf16.hip); the prologue form the register-staged one
+  const int64_t ws_dma = dtype == STC_BF16 ? wgrad_bf16_workspace(B, Hd, Wd, R, Cg) : 0;
+  return std::max(ws_reg, ws_dma);
 }
 
 extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
@@ -341,6 +356,8 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
     STC_CHECK_LAUNCH();
     return 0;
   }
+  if (dtype == STC_BF16 && !d_scale && !d_act && !g_scale && !g_act && wgrad_bf16_eligible(B, D, R, G, Cg))
+    return wgrad_bf16(B, stride, D, R, G, Cg, Cg_out, dW, workspace, workspace_bytes, st);
   const WgPlan pl = wg_plan(p.P, R, Cg);
   p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.nsplit = pl.nsplit; p.pchunk = pl.pchunk;
   p.Cg_out = Cg_out;
@@ -359,7 +376,7 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
   if (dtype == STC_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, p);
   STC_CHECK_LAUNCH();
-  const long long total = (long long)R * Cg_out * 16;
+  const long long total = (long long)R * Cg_out;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)p.ws, pl.nsplit, R, Cg,
                      Cg_out, dW);

@@ -35,6 +35,9 @@ _SIGS = {
                             _vp, _i64, _vp]),
     "stc_conv_fwd_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32, _i32]),
     "stc_conv_fwd_plan": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "stc_conv_fwd_query": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "stc_conv_fwd_ex": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _i32, _i32, _vp, _i32, _vp, _vp,
+                               _i64, _vp]),
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
                               _f32, _vp, _vp, _i64, _vp]),
     "stc_conv_wgrad_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32]),

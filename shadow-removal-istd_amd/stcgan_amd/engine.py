@@ -79,6 +79,20 @@ def _pad2(S, k):
     return (2 * S[k + 1][0], 2 * S[k + 1][1])
 
 
+def _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev):
+    """Conv whose output feeds a BatchNorm2d: returns ((2, cout) scale/shift table, (mean, rstd) or None).
+    Train mode: the batch statistics come out of the conv itself (stc_conv_fwd_ex)."""
+    t = torch.empty((2, cout), dtype=torch.float32, device=dev)
+    if train:
+        part, nch = ops.conv_stats(kind, B, xv, cin, w, cout, yv, dt)
+        st = ops.bn_finalize_part(part, nch, cout, bn, t[0], t[1])
+    else:
+        ops.conv(kind, B, xv, cin, w, cout, yv, dt)
+        ops.bn_eval_table(cout, bn, t[0], t[1])
+        st = None
+    return t, st
+
+
 # ----------------------------------------------------------------------------- generator
 
 
@@ -103,14 +117,9 @@ def gen_forward(plan, sources, train, dt, cache, save):
     rq = [None] + [_nhwc(B, *_pad2(S, k), co[k - 1], dt, dev) for k in range(1, Lv)]
     tab_d, tab_u, st_d, st_u = {}, {}, {}, {}
 
-    def bn_table(bn, xv, C):
-        t = torch.empty((2, C), dtype=torch.float32, device=dev)
-        st = None
-        if train:
-            st = ops.bn_train_table(B, xv, C, dt, bn, t[0], t[1])
-        else:
-            ops.bn_eval_table(C, bn, t[0], t[1])
-        return t, st
+    def conv_bn(kind, xv, cin_, w, cout, yv, bn):
+        """conv -> BatchNorm table (batch statistics fused into the conv in train mode)."""
+        return _conv_bn(kind, B, xv, cin_, w, cout, yv, dt, bn, train, dev)
 
     # ---- down path
     w0 = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_FWD, co[0], cin_pad, dt)
@@ -119,19 +128,20 @@ def gen_forward(plan, sources, train, dt, cache, save):
                  L.nhwc_view(cr[0], 0), 0.0)
     for k in range(1, Lv):
         wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
-        ops.conv(L.CONV_S2, B, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]), dt)
         if k <= Lv - 2:
-            tab_d[k], st_d[k] = bn_table(plan.bnd[k], L.nhwc_view(rd[k]), co[k])
+            tab_d[k], st_d[k] = conv_bn(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k],
+                                        L.nhwc_view(rd[k]), plan.bnd[k])
             ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]), LRELU,
                          L.nhwc_view(cr[k], 0), 0.0)
         else:  # innermost: no down-norm (STCGAN/networks.py:118-124)
+            ops.conv(L.CONV_S2, B, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]), dt)
             ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, None, L.nhwc_view(cr[k]), 0.0)
     # ---- up path
     for k in range(Lv - 1, 0, -1):
         wt = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_FWD, co[k - 1], cin_t(k), dt)
-        ops.conv(L.CONVT_S2, B, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]), dt)
         # statistics over the full ConvT extent (before the crop of an odd level)
-        tab_u[k], st_u[k] = bn_table(plan.bnu[k], L.nhwc_view(rq[k]), co[k - 1])
+        tab_u[k], st_u[k] = conv_bn(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
+                                    plan.bnu[k])
         ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
                      L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
     # ---- outermost: tanh(convT_0(cr[0]) + bias) -> NCHW fp32
@@ -290,16 +300,14 @@ def disc_forward(plan, sources, train, dt, cache, save):
                      out_f32=True)
             break
         o = _nhwc(B, h, w, cout, dt, dev)
-        ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(o), dt, bias=cv.bias)
         tab, st = None, None
-        if i >= 1:  # conv -> BatchNorm -> LeakyReLU (networks.py:167-180)
-            bn = plan.bns[i - 1]
-            t = torch.empty((2, cout), dtype=torch.float32, device=dev)
-            if train:
-                st = ops.bn_train_table(B, L.nhwc_view(o), cout, dt, bn, t[0], t[1])
-            else:
-                ops.bn_eval_table(cout, bn, t[0], t[1])
+        if i >= 1:  # conv -> BatchNorm -> LeakyReLU (networks.py:167-180); no conv bias there
+            assert cv.bias is None
+            t, st = _conv_bn(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(o), dt,
+                             plan.bns[i - 1], train, dev)
             tab = (t[0], t[1])
+        else:
+            ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(o), dt, bias=cv.bias)
         a = _nhwc(B, h, w, cout, dt, dev)
         ops.bn_apply(B, L.nhwc_view(o), cout, dt, tab, L.nhwc_view(a), LRELU)
         raw.append(o)

@@ -75,11 +75,63 @@ def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=No
     check(rc, "stc_conv_fwd")
     if timer is not None:
         e1.record()
-        bm, bn, ks, narrow = plan_of(kind, B, gh, gw, cin, cout, dt)
-        tname = "smalln" if narrow else f"igemm_{bm}x{bn}" + (f"_splitk{ks}" if ks > 1 else "")
-        outs = B * gh * gw * (4 if kind == L.CONVT_S2 else 1)
-        taps = 4 if kind == L.CONVT_S2 else 16
-        timer.append((tname, 2.0 * outs * cout * taps * cin, e0, e1))
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+
+
+def conv_query(kind, B, gh, gw, cin, cout, dt, out_f32=False, force=None):
+    """(workspace bytes, stats chunks, plan (BM, BN, ksplit, narrow, cfg)) of stc_conv_fwd_ex."""
+    ws = ctypes.c_int64()
+    nch = ctypes.c_int32()
+    po = (ctypes.c_int32 * 5)()
+    fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
+    check(lib().stc_conv_fwd_query(L.dtype_code(dt), kind, B, gh, gw, cin, cout, int(out_f32), fp, ctypes.byref(ws),
+                                   ctypes.byref(nch), po), "stc_conv_fwd_query")
+    return ws.value, nch.value, tuple(po)
+
+
+def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
+    """Conv forward + fused BatchNorm partial statistics of its output (stc_conv_fwd_ex).
+    Returns (part [chunks, cout, 4] fp32, chunks) for bn_finalize."""
+    dev = w_packed.device
+    gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
+    nbytes, nch, plan = conv_query(kind, B, gh, gw, cin, cout, dt, force=force)
+    ws, nb = _ws(nbytes, dev)
+    part = torch.empty((nch, cout, 4), dtype=torch.float32, device=dev)
+    fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
+    timer = _timer
+    if timer is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    check(lib().stc_conv_fwd_ex(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ptr(bias), 0, 0,
+                                ptr(part), nch, fp, ptr(ws), nb, stream()), "stc_conv_fwd_ex")
+    if timer is not None:
+        e1.record()
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+    return part, nch
+
+
+def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1):
+    bm, bn, ks, narrow = plan_of(kind, B, gh, gw, cin, cout, dt)
+    tname = "smalln" if narrow else f"igemm_{bm}x{bn}" + (f"_splitk{ks}" if ks > 1 else "")
+    outs = B * gh * gw * (4 if kind == L.CONVT_S2 else 1)
+    taps = 4 if kind == L.CONVT_S2 else 16
+    timer.append((tname, 2.0 * outs * cout * taps * cin, e0, e1))
+
+
+def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True):
+    """mean/rstd + (scale, shift) table from conv_stats partials; updates running stats."""
+    dev = scale_out.device
+    mean = torch.empty(C, dtype=torch.float32, device=dev)
+    rstd = torch.empty(C, dtype=torch.float32, device=dev)
+    rm = bn.running_mean if update_running else None
+    rv = bn.running_var if update_running else None
+    nbt = bn.num_batches_tracked if update_running else None
+    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+    check(lib().stc_bn_finalize(ptr(part), nch, C, ptr(bn.weight), ptr(bn.bias), ptr(rm), ptr(rv), ptr(nbt),
+                                float(mom), float(bn.eps), ptr(mean), ptr(rstd), ptr(scale_out), ptr(shift_out),
+                                stream()), "stc_bn_finalize")
+    return mean, rstd
 
 
 def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None):

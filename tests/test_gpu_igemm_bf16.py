@@ -1,0 +1,221 @@
+"""bf16 LDS-DMA implicit-GEMM kernel (csrc/igemm_bf16.hip) against torch fp32 references.
+
+Every conv kind on the ST-CGAN path (Conv2d k4 s2/s1, ConvTranspose2d k4 s2 as 4 phases, the
+conv-s1 input gradient), every tile configuration, split-K on/off, ragged M and N, channel-offset
+output views (the zero-copy skip concat), and the BatchNorm statistics fused into the epilogue /
+split-K reduction.  Operands are rounded to bf16 before the fp32 reference, so the only
+differences are fp32 summation order and the final bf16 rounding of the output:
+tolerance 1e-2 * max|ref| on outputs, 2e-3 relative on the per-channel mean/variance.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from stcgan_amd import _lib as L
+from stcgan_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g) * scale
+
+
+def q(t):
+    return t.to(BF).float()
+
+
+def run(kind, B, x_nchw, w, Cin, Cout, out_shape, force=None, co=0, extra_c=0, bias=None):
+    """Runs stc_conv_fwd_ex with stats; returns (y NCHW fp32, mean, var) on the CPU."""
+    pack_mode = {L.CONV_S2: L.PACK_CONV_FWD, L.CONV_S1: L.PACK_CONV_FWD, L.CONVT_S2: L.PACK_CONVT_FWD,
+                 L.CONV_S1_DGRAD: L.PACK_CONV_S1_DGRAD}[kind]
+    xg = nhwc(x_nchw).to(DEV, BF)
+    wp = ops.pack(pack_mode, w.to(DEV), Cout, Cin, BF)
+    Ho, Wo = out_shape
+    Ctot = Cout + extra_c
+    y = torch.full((B, Ho, Wo, Ctot), float("nan"), device=DEV, dtype=BF)
+    part, nch = ops.conv_stats(kind, B, L.nhwc_view(xg), Cin, wp, Cout, L.nhwc_view(y, co), BF,
+                               bias=None if bias is None else bias.to(DEV), force=force)
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV)
+    t = torch.empty((2, Cout), device=DEV)
+    mean, rstd = ops.bn_finalize_part(part, nch, Cout, bn, t[0], t[1])
+    var = 1.0 / rstd.double() ** 2 - bn.eps
+    torch.cuda.synchronize()
+    yo = nchw(y[..., co:co + Cout].float()).cpu()
+    return yo, mean.cpu().double(), var.cpu()
+
+
+def check(got, ref, mean, var, what, tol=1e-2):
+    scale = float(ref.abs().max()) + 1e-12
+    err = float((got - ref).abs().max())
+    assert err <= tol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+    rm = ref.double().mean(dim=(0, 2, 3))
+    rv = ref.double().var(dim=(0, 2, 3), unbiased=False)
+    sd = float(rv.max().sqrt()) + 1e-12
+    assert float((mean - rm).abs().max()) <= 2e-3 * sd, f"{what}: mean err {float((mean - rm).abs().max()):.3e}"
+    assert float(((var - rv).abs() / (rv + 1e-12)).max()) <= 2e-3 * 4, f"{what}: var err"
+
+
+CASES = [  # B, Cin, Cout, H(grid), W(grid)
+    (2, 64, 128, 32, 32),
+    (2, 128, 256, 16, 16),
+    (4, 512, 512, 4, 4),
+    (3, 64, 96, 10, 14),     # ragged M and N (N not a tile multiple)
+    (2, 8, 64, 64, 64),      # Cin = 8: a K-step spans 8 taps
+    (1, 256, 64, 7, 9),
+]
+CFGS = [None] + [(c, 1) for c in range(14)] + [(0, 2), (5, 4), (8, 2), (12, 4)]
+
+
+@pytest.mark.parametrize("force", CFGS, ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+def test_conv_s2(case, force):
+    B, Cin, Cout, Hg, Wg = case
+    x = q(rnd(B, Cin, 2 * Hg, 2 * Wg, seed=1))
+    w = q(rnd(Cout, Cin, 4, 4, seed=2, scale=0.05))
+    ref = F.conv2d(x, w, None, 2, 1)
+    y, mean, var = run(L.CONV_S2, B, x, w, Cin, Cout, (Hg, Wg), force=force)
+    check(y, ref, mean, var, f"conv s2 {case} {force}")
+
+
+@pytest.mark.parametrize("force", [None, (0, 1), (1, 1), (3, 1), (5, 2), (8, 1), (9, 1), (13, 1), (11, 2)],
+                         ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+def test_convT_s2(case, force):
+    B, Cin, Cout, Hg, Wg = case
+    x = q(rnd(B, Cin, Hg, Wg, seed=3))
+    w = q(rnd(Cin, Cout, 4, 4, seed=4, scale=0.05))
+    ref = F.conv_transpose2d(x, w, None, 2, 1)
+    y, mean, var = run(L.CONVT_S2, B, x, w, Cin, Cout, (2 * Hg, 2 * Wg), force=force)
+    check(y, ref, mean, var, f"convT {case} {force}")
+
+
+@pytest.mark.parametrize("force", [None, (0, 1), (6, 1), (0, 4)], ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
+def test_conv_s1_and_dgrad(force):
+    B, Cin, Cout, H = 2, 256, 512, 17   # PatchGAN layer 4 geometry (32x32 -> 31x31), smaller
+    x = q(rnd(B, Cin, H, H, seed=5))
+    w = q(rnd(Cout, Cin, 4, 4, seed=6, scale=0.05))
+    ref = F.conv2d(x, w, None, 1, 1)
+    y, mean, var = run(L.CONV_S1, B, x, w, Cin, Cout, (H - 1, H - 1), force=force)
+    check(y, ref, mean, var, f"conv s1 {force}")
+    # input gradient: dx = conv_transpose2d(dy, w, stride 1, pad 1), N = Cin, reduction over Cout
+    dy = q(rnd(B, Cout, H - 1, H - 1, seed=7))
+    ref = F.conv_transpose2d(dy, w, None, 1, 1)
+    y, mean, var = run(L.CONV_S1_DGRAD, B, dy, w, Cout, Cin, (H, H), force=force)
+    check(y, ref, mean, var, f"conv s1 dgrad {force}")
+
+
+@pytest.mark.parametrize("force", [None, (1, 1), (0, 2)], ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
+def test_channel_offset_view_and_bias(force):
+    """Output into the second half of a concat buffer (zero-copy skip) with a bias epilogue."""
+    B, Cin, Cout, Hg, Wg = 2, 128, 128, 16, 16
+    x = q(rnd(B, Cin, 2 * Hg, 2 * Wg, seed=8))
+    w = q(rnd(Cout, Cin, 4, 4, seed=9, scale=0.05))
+    b = rnd(Cout, seed=10)
+    ref = F.conv2d(x, w, b, 2, 1)
+    y, mean, var = run(L.CONV_S2, B, x, w, Cin, Cout, (Hg, Wg), force=force, co=64, extra_c=64, bias=b)
+    check(y, ref, mean, var, f"offset view {force}")
+
+
+def test_plan_query_consistent():
+    for kind, gh in ((L.CONV_S2, 64), (L.CONVT_S2, 8), (L.CONV_S1, 31)):
+        ws, nch, plan = ops.conv_query(kind, 32, gh, gh, 256, 512, BF)
+        assert plan[4] >= 0 and plan[2] >= 1 and nch >= 1
+        assert (ws > 0) == (plan[2] > 1)
+
+
+NARROW = [  # kind, B, Cin, N, grid H, grid W
+    ("convT", 2, 128, 3, 20, 24),    # generator output layer (bias + tanh, NCHW fp32)
+    ("convT", 2, 128, 1, 16, 16),
+    ("convT", 1, 64, 8, 9, 13),      # first-layer input gradient (N = 8 padded channels), ragged tiles
+    ("convT", 3, 64, 4, 33, 17),
+    ("conv_s1", 2, 512, 1, 30, 30),  # PatchGAN logits 31x31 -> 30x30 (split over channel chunks)
+    ("conv_s1", 1, 128, 2, 11, 9),
+]
+
+
+@pytest.mark.parametrize("out", ["nchw_f32", "nhwc_bf16"])
+@pytest.mark.parametrize("case", NARROW, ids=lambda c: "_".join(map(str, c)))
+def test_narrow_halo(case, out):
+    """bf16 narrow-N layers (N <= 8/16) on the LDS-halo MFMA kernel (csrc/narrow_bf16.hip)."""
+    kind, B, Cin, N, GH, GW = case
+    x_shape = (B, Cin, GH, GW) if kind == "convT" else (B, Cin, GH + 1, GW + 1)
+    x = q(rnd(*x_shape, seed=31))
+    b = rnd(N, seed=32)
+    if kind == "convT":
+        w = q(rnd(Cin, N, 4, 4, seed=33, scale=0.05))
+        ref = F.conv_transpose2d(x, w, b, 2, 1)
+        wp = ops.pack(L.PACK_CONVT_FWD, w.to(DEV), N, Cin, BF)
+        kd, Ho, Wo = L.CONVT_S2, 2 * GH, 2 * GW
+    else:
+        w = q(rnd(N, Cin, 4, 4, seed=34, scale=0.05))
+        ref = F.conv2d(x, w, b, 1, 1)
+        wp = ops.pack(L.PACK_CONV_FWD, w.to(DEV), N, Cin, BF)
+        kd, Ho, Wo = L.CONV_S1, GH, GW
+    assert ops.plan_of(kd, B, GH, GW, Cin, N, BF)[3] == 1
+    xg = nhwc(x).to(DEV, BF)
+    tanh = out == "nchw_f32"
+    if tanh:
+        ref = torch.tanh(ref)
+        y = torch.full((B, N, Ho, Wo), float("nan"), device=DEV)
+        ops.conv(kd, B, L.nhwc_view(xg), Cin, wp, N, L.nchw_view(y), BF, bias=b.to(DEV), tanh=True, out_f32=True)
+        got = y.cpu()
+    else:
+        y = torch.full((B, Ho, Wo, N), float("nan"), device=DEV, dtype=BF)
+        ops.conv(kd, B, L.nhwc_view(xg), Cin, wp, N, L.nhwc_view(y), BF, bias=b.to(DEV))
+        got = nchw(y.float()).cpu()
+    scale = float(ref.abs().max())
+    err = float((got - ref).abs().max())
+    tol = 2e-5 if tanh else 8e-3  # fp32 output: summation order only; bf16 output: final rounding
+    assert err <= tol * max(scale, 1.0) * (1 if tanh else 1) + (1e-5 if tanh else 0), f"narrow {case} {out}: {err:.3e}"
+
+
+WGRAD = [  # kind, stride, B, Cin, Cout, H, W (input grid of the forward layer)
+    ("conv", 2, 2, 64, 128, 32, 32),
+    ("conv", 2, 2, 8, 64, 64, 64),     # first layer: Cg = 8, 16 taps per 128-column tile
+    ("conv", 2, 4, 512, 512, 4, 4),    # small pixel count, many column tiles
+    ("conv", 1, 2, 256, 512, 17, 17),  # PatchGAN layer 4 geometry
+    ("conv", 2, 3, 32, 96, 10, 14),    # ragged R / columns
+    ("convT", 2, 2, 128, 64, 16, 16),
+    ("convT", 2, 2, 1024, 512, 2, 2),
+    ("convT", 2, 1, 64, 8, 9, 13),     # R = 64 rows of a 128-row tile, odd grid
+]
+
+
+@pytest.mark.parametrize("case", WGRAD, ids=lambda c: "_".join(map(str, c)))
+def test_wgrad_bf16_dma(case):
+    """bf16 weight gradient on the LDS-DMA / transposed-read kernel (csrc/wgrad_bf16.hip)."""
+    kind, s, B, Cin, Cout, H, W = case
+    x = q(rnd(B, Cin, H, W, seed=41))
+    if kind == "conv":
+        w = torch.zeros(Cout, Cin, 4, 4, requires_grad=True)
+        y = F.conv2d(x, w, None, s, 1)
+        dy = q(rnd(*y.shape, seed=42))
+        (gw,) = torch.autograd.grad(y, w, dy)
+        # D = dy (R = Cout), G = x (Cg = Cin)
+        dW = ops.wgrad(B, s, L.nhwc_view(nhwc(dy).to(DEV, BF)), Cout, L.nhwc_view(nhwc(x).to(DEV, BF)), Cin, Cin, BF,
+                       device=DEV)
+    else:
+        w = torch.zeros(Cin, Cout, 4, 4, requires_grad=True)
+        y = F.conv_transpose2d(x, w, None, 2, 1)
+        dy = q(rnd(*y.shape, seed=43))
+        (gw,) = torch.autograd.grad(y, w, dy)
+        # D = x (R = Cin), G = dy (Cg = Cout)
+        dW = ops.wgrad(B, 2, L.nhwc_view(nhwc(x).to(DEV, BF)), Cin, L.nhwc_view(nhwc(dy).to(DEV, BF)), Cout, Cout, BF,
+                       device=DEV)
+    torch.cuda.synchronize()
+    got = dW.cpu()
+    err = float((got - gw).abs().max())
+    scale = float(gw.abs().max())
+    assert err <= 2e-5 * scale + 1e-6, f"wgrad {case}: {err:.3e} vs {scale:.3e}"  # exact products, fp32 sums
