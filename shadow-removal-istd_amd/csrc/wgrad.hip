@@ -271,27 +271,29 @@ wgrad_kernel(const WgradParams p) {
     }
 }
 
-// dW[r][ci][kh][kw] = sum_s ws[s][r][(kh*4+kw)*Cg + ci]: one thread per (r, ci), the 16 taps in
-// registers; slab reads are coalesced over ci, each thread writes its 64 contiguous bytes of dW.
+// dW[r][ci][kh][kw] = sum_s ws[s][r][(kh*4+kw)*Cg + ci]: one thread per (r, tap, ci) with ci fastest
+// (coalesced slab reads), the splits summed in a fixed order with 4 independent partial sums.
 __global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int R, int Cg, int Cg_out, float* dW) {
-  const long long total = (long long)R * Cg_out;
+  const long long total = (long long)R * 16 * Cg_out;
   const long long Ncol = 16LL * Cg;
   const long long slab = (long long)R * Ncol;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
     const int ci = (int)(idx % Cg_out);
-    const int r = (int)(idx / Cg_out);
-    const float* src = ws + (long long)r * Ncol + ci;
-    float v[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) v[t] = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
-#pragma unroll
-      for (int t = 0; t < 16; ++t) v[t] += src[(long long)s * slab + (long long)t * Cg];
+    const long long rt = idx / Cg_out;
+    const int tap = (int)(rt & 15);
+    const int r = (int)(rt >> 4);
+    const float* src = ws + (long long)r * Ncol + (long long)tap * Cg + ci;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    int sp = 0;
+    for (; sp + 4 <= nsplit; sp += 4) {
+      v0 += src[(long long)sp * slab];
+      v1 += src[(long long)(sp + 1) * slab];
+      v2 += src[(long long)(sp + 2) * slab];
+      v3 += src[(long long)(sp + 3) * slab];
     }
-    float4* o = reinterpret_cast<float4*>(dW + idx * 16);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    for (; sp < nsplit; ++sp) v0 += src[(long long)sp * slab];
+    dW[((long long)r * Cg_out + ci) * 16 + tap] = (v0 + v1) + (v2 + v3);
   }
 }
 
@@ -376,8 +378,8 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
   if (dtype == STC_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, p);
   STC_CHECK_LAUNCH();
-  const long long total = (long long)R * Cg_out;
-  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  const long long total = (long long)R * 16 * Cg_out;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)p.ws, pl.nsplit, R, Cg,
                      Cg_out, dW);
   STC_CHECK_LAUNCH();

@@ -268,8 +268,8 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
   p.ws = (float*)workspace;
   hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(256), lds, st, p);
   STC_CHECK_LAUNCH();
-  const long long total = (long long)R * Cg_out;
-  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  const long long total = (long long)R * 16 * Cg_out;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)p.ws, pl.nsplit, R, Cg, Cg_out,
                      dW);
   STC_CHECK_LAUNCH();

@@ -41,7 +41,7 @@ def _pro(pro):
     return ptr(sc), ptr(sh)
 
 
-_timer = None  # when a list: conv() appends (tile name, flops, start event, end event) per launch
+_timer = None  # when a list: conv()/conv_stats()/wgrad() append (kernel, single-kernel launch, flops, start, end)
 _DEBUG_NO_PROLOGUE = False
 
 
@@ -111,12 +111,35 @@ def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
     return part, nch
 
 
+# bf16 LDS-DMA tile configurations (csrc/igemm_bf16.hip kTiles): cfg -> (BM, BN, WM, WN, stages)
+_BF16_TILES = [(128, 128, 2, 2, 2), (256, 128, 2, 2, 2), (128, 64, 2, 2, 2), (256, 64, 4, 1, 2), (64, 128, 1, 4, 2),
+               (64, 64, 2, 2, 2), (256, 256, 2, 4, 2), (128, 256, 2, 4, 2), (128, 128, 2, 2, 3), (128, 256, 2, 4, 3),
+               (64, 128, 1, 4, 3), (128, 64, 2, 2, 3), (64, 64, 2, 2, 3), (256, 128, 4, 2, 3)]
+
+
+def kernel_name(kind, B, gh, gw, cin, cout, dt):
+    """(kernel symbol as rocprof shows it, launches-a-single-kernel) of one conv call."""
+    ws, _, plan = conv_query(kind, B, gh, gw, cin, cout, dt)
+    bm, bn, ks, narrow, cfg = plan
+    if narrow:
+        if dt == torch.bfloat16 and cin % 64 == 0:
+            geom = 0 if kind == L.CONVT_S2 else 1
+            nb = 2 if (kind == L.CONVT_S2 and 4 * cout > 16) else 1
+            return f"narrow_halo_kernel<{geom}, {nb}, 16>", ws == 0
+        return "narrow_tiled_kernel", True
+    if cfg >= 0:
+        t = _BF16_TILES[cfg]
+        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}>", ks == 1
+    tname = {torch.float32: "float", torch.bfloat16: "__hip_bfloat16"}[dt]
+    return f"igemm_kernel<{tname}, {bm}, {bn}>", ks == 1
+
+
 def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1):
-    bm, bn, ks, narrow = plan_of(kind, B, gh, gw, cin, cout, dt)
-    tname = "smalln" if narrow else f"igemm_{bm}x{bn}" + (f"_splitk{ks}" if ks > 1 else "")
+    name, single = kernel_name(kind, B, gh, gw, cin, cout, dt)
     outs = B * gh * gw * (4 if kind == L.CONVT_S2 else 1)
     taps = 4 if kind == L.CONVT_S2 else 16
-    timer.append((tname, 2.0 * outs * cout * taps * cin, e0, e1))
+    timer.append((name, single, 2.0 * outs * cout * taps * cin, e0, e1,
+                  f"{['conv_s2', 'conv_s1', 'convT', 's1_dgrad'][kind]} B{B} grid{gh}x{gw} cin{cin} cout{cout}"))
 
 
 def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True):
@@ -142,11 +165,22 @@ def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=Non
     dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)
     dsc, dsh = _pro(dpro)
     gsc, gsh = _pro(gpro)
+    timer = _timer
+    if timer is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     rc = l.stc_conv_wgrad(L.dtype_code(dt), B, stride, Dv, R, dsc, dsh, 0 if dslope is None else 1,
                           0.0 if dslope is None else float(dslope), Gv, Cg, Cg_out, gsc, gsh,
                           0 if gslope is None else 1, 0.0 if gslope is None else float(gslope), ptr(dW), ptr(ws), nb,
                           stream())
     check(rc, "stc_conv_wgrad")
+    if timer is not None:
+        e1.record()
+        dma = dt == torch.bfloat16 and dpro is None and gpro is None and dslope is None and gslope is None
+        name = "wgrad_bf16_kernel" if dma else "wgrad_kernel"
+        timer.append((name, nbytes == 0, 2.0 * B * Dv.H * Dv.W * R * 16 * Cg, e0, e1,
+                      f"wgrad s{stride} P={B * Dv.H * Dv.W} R{R} Cg{Cg}"))
     return dW
 
 
