@@ -22,53 +22,123 @@ __host__ __device__ inline int stat_chunks(long long P) {
   return (int)c;
 }
 
-template <typename T>
-__device__ __forceinline__ float4 vload(const View& v, int b, int y, int x, int c) {
-  return Vec4<T>::load(reinterpret_cast<const T*>(v.p) + vidx(v, b, y, x, c));
+// ---- 16-byte vectors of T (8 bf16 / 4 fp32 channels per thread)
+template <typename T> struct VW;
+template <> struct VW<float> {
+  static constexpr int N = 4;
+  __device__ __forceinline__ static void load(const float* p, float* f) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float* f) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  }
+};
+template <> struct VW<bf16> {
+  static constexpr int N = 8;
+  __device__ __forceinline__ static void load(const bf16* p, float* f) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { f[2 * q] = __uint_as_float(w[q] << 16); f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+  }
+  __device__ __forceinline__ static void store(bf16* p, const float* f) {
+    uint4 v;
+    v.x = (unsigned)f2bf(f[0]) | ((unsigned)f2bf(f[1]) << 16);
+    v.y = (unsigned)f2bf(f[2]) | ((unsigned)f2bf(f[3]) << 16);
+    v.z = (unsigned)f2bf(f[4]) | ((unsigned)f2bf(f[5]) << 16);
+    v.w = (unsigned)f2bf(f[6]) | ((unsigned)f2bf(f[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+};
+
+// pixel index -> (b, y, x); exact float-reciprocal division below 2^24 pixels, integer division above
+struct PixDiv {
+  int HW, W;
+  float inv_hw, inv_w;
+  bool big;
+};
+static inline PixDiv mkpix(int B, int H, int W) {
+  PixDiv d;
+  d.HW = H * W; d.W = W;
+  d.inv_hw = 1.f / (float)(H * W); d.inv_w = 1.f / (float)W;
+  d.big = (long long)B * H * W >= (1ll << 24);
+  return d;
+}
+__device__ __forceinline__ int qdiv(int n, int d, float inv) {
+  int q = (int)((float)n * inv);
+  const int r = n - q * d;
+  return q + (r >= d) - (r < 0);
+}
+__device__ __forceinline__ void pix_bxy(const PixDiv& d, long long pix, int& b, int& y, int& x) {
+  int rem;
+  if (d.big) {
+    b = (int)(pix / d.HW);
+    rem = (int)(pix - (long long)b * d.HW);
+    y = rem / d.W;
+  } else {
+    const int pi = (int)pix;
+    b = qdiv(pi, d.HW, d.inv_hw);
+    rem = pi - b * d.HW;
+    y = qdiv(rem, d.W, d.inv_w);
+  }
+  x = rem - y * d.W;
 }
 
+template <typename T>
+__device__ __forceinline__ const T* vptr(const View& v, int b, int y, int x, int c) {
+  return reinterpret_cast<const T*>(v.p) + vidx(v, b, y, x, c);
+}
+
+// Reduction layout shared by the per-channel reductions: thread = (channel group cg of N channels,
+// pixel lane pl); the block owns a contiguous pixel range and the lanes stride through it.
 // part[chunk][c] = {n, S1, S2, shift}
 template <typename T>
-__global__ void __launch_bounds__(256) chan_stats_kernel(View x, int B, int C, float* part, int nchunks) {
-  const int cq = C >> 2;
-  const int ppb = 256 / cq;  // pixels processed in parallel
-  const int q = threadIdx.x % cq, pl = threadIdx.x / cq;
-  const long long HW = (long long)x.H * x.W, P = HW * B;
+__global__ void __launch_bounds__(256) chan_stats_kernel(View x, PixDiv pd, long long P, int C, float* part, int nchunks) {
+  constexpr int N = VW<T>::N;
+  const int CG = C / N;
+  const int RL = 256 / CG;
+  const int cg = threadIdx.x % CG, pl = threadIdx.x / CG;
   const long long per = (P + nchunks - 1) / nchunks;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  __shared__ float red[3][256][4];
-  float4 s1 = make_float4(0, 0, 0, 0), s2 = make_float4(0, 0, 0, 0), sh = make_float4(0, 0, 0, 0);
-  float cnt = 0.f;
-  if (pl < ppb && p0 < p1) {
-    {
-      const int b = (int)(p0 / HW), rem = (int)(p0 % HW);
-      sh = vload<T>(x, b, rem / x.W, rem % x.W, 4 * q);
-    }
-    for (long long pix = p0 + pl; pix < p1; pix += ppb) {
-      const int b = (int)(pix / HW), rem = (int)(pix % HW);
-      float4 v = vload<T>(x, b, rem / x.W, rem % x.W, 4 * q);
-      v.x -= sh.x; v.y -= sh.y; v.z -= sh.z; v.w -= sh.w;
-      s1.x += v.x; s1.y += v.y; s1.z += v.z; s1.w += v.w;
-      s2.x += v.x * v.x; s2.y += v.y * v.y; s2.z += v.z * v.z; s2.w += v.w * v.w;
+  __shared__ float red[256][2 * N + 1];
+  float s1[N], s2[N], sh[N], cnt = 0.f;
+#pragma unroll
+  for (int e = 0; e < N; ++e) { s1[e] = 0.f; s2[e] = 0.f; sh[e] = 0.f; }
+  if (pl < RL && p0 < p1) {
+    int b, yy, xx;
+    pix_bxy(pd, p0, b, yy, xx);
+    VW<T>::load(vptr<T>(x, b, yy, xx, N * cg), sh);
+    for (long long pix = p0 + pl; pix < p1; pix += RL) {
+      pix_bxy(pd, pix, b, yy, xx);
+      float v[N];
+      VW<T>::load(vptr<T>(x, b, yy, xx, N * cg), v);
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const float d = v[e] - sh[e];
+        s1[e] += d;
+        s2[e] += d * d;
+      }
       cnt += 1.f;
     }
   }
-  red[0][threadIdx.x][0] = s1.x; red[0][threadIdx.x][1] = s1.y; red[0][threadIdx.x][2] = s1.z; red[0][threadIdx.x][3] = s1.w;
-  red[1][threadIdx.x][0] = s2.x; red[1][threadIdx.x][1] = s2.y; red[1][threadIdx.x][2] = s2.z; red[1][threadIdx.x][3] = s2.w;
-  red[2][threadIdx.x][0] = cnt;
+#pragma unroll
+  for (int e = 0; e < N; ++e) { red[threadIdx.x][e] = s1[e]; red[threadIdx.x][N + e] = s2[e]; }
+  red[threadIdx.x][2 * N] = cnt;
   __syncthreads();
-  if (pl == 0 && threadIdx.x < cq) {
-    float a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0}, n = 0.f;
-    for (int k = 0; k < ppb; ++k) {  // fixed order
-      const int t = k * cq + q;
-      for (int e = 0; e < 4; ++e) { a1[e] += red[0][t][e]; a2[e] += red[1][t][e]; }
-      n += red[2][t][0];
+  if (pl == 0) {
+    float a1[N], a2[N], n = 0.f;
+#pragma unroll
+    for (int e = 0; e < N; ++e) { a1[e] = 0.f; a2[e] = 0.f; }
+    for (int k = 0; k < RL; ++k) {  // fixed order
+      const int t = k * CG + cg;
+#pragma unroll
+      for (int e = 0; e < N; ++e) { a1[e] += red[t][e]; a2[e] += red[t][N + e]; }
+      n += red[t][2 * N];
     }
-    const float shv[4] = {sh.x, sh.y, sh.z, sh.w};
-    for (int e = 0; e < 4; ++e) {
-      float* o = part + ((long long)blockIdx.x * C + 4 * q + e) * 4;
-      o[0] = n; o[1] = a1[e]; o[2] = a2[e]; o[3] = shv[e];
-    }
+#pragma unroll
+    for (int e = 0; e < N; ++e)
+      *reinterpret_cast<float4*>(part + ((long long)blockIdx.x * C + N * cg + e) * 4) = make_float4(n, a1[e], a2[e], sh[e]);
   }
 }
 
@@ -141,64 +211,82 @@ struct GradIn {
 };
 
 template <typename T>
-__device__ __forceinline__ float4 dn_of(const GradIn& gi, int b, int y, int x, int c, float4 n) {
-  float4 d = make_float4(0, 0, 0, 0);
+__device__ __forceinline__ void dn_of(const GradIn& gi, int b, int y, int x, int c, const float* n, float* d) {
+  constexpr int N = VW<T>::N;
+#pragma unroll
+  for (int e = 0; e < N; ++e) d[e] = 0.f;
   if (gi.has1) {
-    const float4 g = vload<T>(gi.g1, b, y, x, c);
-    d.x += g.x * dact(n.x, gi.s1); d.y += g.y * dact(n.y, gi.s1);
-    d.z += g.z * dact(n.z, gi.s1); d.w += g.w * dact(n.w, gi.s1);
+    float g[N];
+    VW<T>::load(vptr<T>(gi.g1, b, y, x, c), g);
+#pragma unroll
+    for (int e = 0; e < N; ++e) d[e] += g[e] * dact(n[e], gi.s1);
   }
   if (gi.has2) {
-    const float4 g = vload<T>(gi.g2, b, y, x, c);
-    d.x += g.x * dact(n.x, gi.s2); d.y += g.y * dact(n.y, gi.s2);
-    d.z += g.z * dact(n.z, gi.s2); d.w += g.w * dact(n.w, gi.s2);
+    float g[N];
+    VW<T>::load(vptr<T>(gi.g2, b, y, x, c), g);
+#pragma unroll
+    for (int e = 0; e < N; ++e) d[e] += g[e] * dact(n[e], gi.s2);
   }
-  return d;
+}
+
+template <int N>
+__device__ __forceinline__ void ldc(const float* p, float* f) {
+#pragma unroll
+  for (int e = 0; e < N; e += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p + e);
+    f[e] = v.x; f[e + 1] = v.y; f[e + 2] = v.z; f[e + 3] = v.w;
+  }
 }
 
 // part2[chunk][c] = {sum dn, sum dn*xhat}
 template <typename T>
-__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(View x, int B, int C, const float* scale, const float* shift,
-                                                            const float* mean, const float* rstd, GradIn gi,
-                                                            float* part, int nchunks) {
-  const int cq = C >> 2;
-  const int ppb = 256 / cq;
-  const int q = threadIdx.x % cq, pl = threadIdx.x / cq;
-  const long long HW = (long long)x.H * x.W, P = HW * B;
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(View x, PixDiv pd, long long P, int C, const float* scale,
+                                                            const float* shift, const float* mean, const float* rstd,
+                                                            GradIn gi, float* part, int nchunks) {
+  constexpr int N = VW<T>::N;
+  const int CG = C / N;
+  const int RL = 256 / CG;
+  const int cg = threadIdx.x % CG, pl = threadIdx.x / CG;
   const long long per = (P + nchunks - 1) / nchunks;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  __shared__ float red[2][256][4];
-  float a[4] = {0, 0, 0, 0}, bsum[4] = {0, 0, 0, 0};
-  if (pl < ppb) {
-    const int c = 4 * q;
-    const float4 sc = *reinterpret_cast<const float4*>(scale + c);
-    const float4 shf = *reinterpret_cast<const float4*>(shift + c);
-    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
-    const float4 rs = *reinterpret_cast<const float4*>(rstd + c);
-    for (long long pix = p0 + pl; pix < p1; pix += ppb) {
-      const int b = (int)(pix / HW), rem = (int)(pix % HW);
-      const int y = rem / x.W, xx = rem % x.W;
-      const float4 v = vload<T>(x, b, y, xx, c);
-      const float4 n = make_float4(fmaf(v.x, sc.x, shf.x), fmaf(v.y, sc.y, shf.y), fmaf(v.z, sc.z, shf.z),
-                                   fmaf(v.w, sc.w, shf.w));
-      const float4 d = dn_of<T>(gi, b, y, xx, c, n);
-      a[0] += d.x; a[1] += d.y; a[2] += d.z; a[3] += d.w;
-      bsum[0] += d.x * (v.x - mu.x) * rs.x; bsum[1] += d.y * (v.y - mu.y) * rs.y;
-      bsum[2] += d.z * (v.z - mu.z) * rs.z; bsum[3] += d.w * (v.w - mu.w) * rs.w;
+  __shared__ float red[256][2 * N];
+  float a[N], bs[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) { a[e] = 0.f; bs[e] = 0.f; }
+  if (pl < RL) {
+    const int c = N * cg;
+    float sc[N], shf[N], mu[N], rs[N];
+    ldc<N>(scale + c, sc); ldc<N>(shift + c, shf); ldc<N>(mean + c, mu); ldc<N>(rstd + c, rs);
+    for (long long pix = p0 + pl; pix < p1; pix += RL) {
+      int b, yy, xx;
+      pix_bxy(pd, pix, b, yy, xx);
+      float v[N], n[N], d[N];
+      VW<T>::load(vptr<T>(x, b, yy, xx, c), v);
+#pragma unroll
+      for (int e = 0; e < N; ++e) n[e] = fmaf(v[e], sc[e], shf[e]);
+      dn_of<T>(gi, b, yy, xx, c, n, d);
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        a[e] += d[e];
+        bs[e] += d[e] * (v[e] - mu[e]) * rs[e];
+      }
     }
   }
-  for (int e = 0; e < 4; ++e) { red[0][threadIdx.x][e] = a[e]; red[1][threadIdx.x][e] = bsum[e]; }
+#pragma unroll
+  for (int e = 0; e < N; ++e) { red[threadIdx.x][e] = a[e]; red[threadIdx.x][N + e] = bs[e]; }
   __syncthreads();
-  if (pl == 0 && threadIdx.x < cq) {
-    float r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
-    for (int k = 0; k < ppb; ++k) {
-      const int t = k * cq + q;
-      for (int e = 0; e < 4; ++e) { r0[e] += red[0][t][e]; r1[e] += red[1][t][e]; }
+  if (pl == 0) {
+    float r0[N], r1[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) { r0[e] = 0.f; r1[e] = 0.f; }
+    for (int k = 0; k < RL; ++k) {
+      const int t = k * CG + cg;
+#pragma unroll
+      for (int e = 0; e < N; ++e) { r0[e] += red[t][e]; r1[e] += red[t][N + e]; }
     }
-    for (int e = 0; e < 4; ++e) {
-      float* o = part + ((long long)blockIdx.x * C + 4 * q + e) * 2;
-      o[0] = r0[e]; o[1] = r1[e];
-    }
+#pragma unroll
+    for (int e = 0; e < N; ++e)
+      *reinterpret_cast<float2*>(part + ((long long)blockIdx.x * C + N * cg + e) * 2) = make_float2(r0[e], r1[e]);
   }
 }
 
@@ -221,43 +309,43 @@ __global__ void bn_bwd_finalize_kernel(const float* part, int nchunks, int C, fl
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, int B, int C, const float* scale, const float* shift,
-                                                           const float* mean, const float* rstd, const float* gamma,
-                                                           GradIn gi, const float* dgamma, const float* dbeta,
-                                                           View dx) {
-  const int cq = C >> 2;
-  const long long HW = (long long)x.H * x.W, P = HW * B;
-  const long long total = P * cq;
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, PixDiv pd, long long P, int C, const float* scale,
+                                                           const float* shift, const float* mean, const float* rstd,
+                                                           const float* gamma, GradIn gi, const float* dgamma,
+                                                           const float* dbeta, View dx) {
+  constexpr int N = VW<T>::N;
+  const int CG = C / N;
+  const long long total = P * CG;
   const float invP = 1.f / (float)P;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(idx % cq);
-    const long long pix = idx / cq;
-    const int b = (int)(pix / HW), rem = (int)(pix % HW);
-    const int y = rem / x.W, xx = rem % x.W;
-    const int c = 4 * q;
-    const float4 v = vload<T>(x, b, y, xx, c);
-    float4 n;
+    const int cg = (int)(idx % CG);
+    const long long pix = idx / CG;
+    int b, yy, xx;
+    pix_bxy(pd, pix, b, yy, xx);
+    const int c = N * cg;
+    float v[N], n[N], d[N];
+    VW<T>::load(vptr<T>(x, b, yy, xx, c), v);
     if (scale) {
-      const float4 sc = *reinterpret_cast<const float4*>(scale + c);
-      const float4 shf = *reinterpret_cast<const float4*>(shift + c);
-      n = make_float4(fmaf(v.x, sc.x, shf.x), fmaf(v.y, sc.y, shf.y), fmaf(v.z, sc.z, shf.z), fmaf(v.w, sc.w, shf.w));
+      float sc[N], shf[N];
+      ldc<N>(scale + c, sc); ldc<N>(shift + c, shf);
+#pragma unroll
+      for (int e = 0; e < N; ++e) n[e] = fmaf(v[e], sc[e], shf[e]);
     } else {
-      n = v;
+#pragma unroll
+      for (int e = 0; e < N; ++e) n[e] = v[e];
     }
-    float4 d = dn_of<T>(gi, b, y, xx, c, n);
+    dn_of<T>(gi, b, yy, xx, c, n, d);
     if (mean) {
-      const float vv[4] = {v.x, v.y, v.z, v.w};
-      float dd[4] = {d.x, d.y, d.z, d.w};
-      for (int e = 0; e < 4; ++e) {
-        const int ch = c + e;
-        const float rs = rstd[ch];
-        const float xh = (vv[e] - mean[ch]) * rs;
-        dd[e] = gamma[ch] * rs * (dd[e] - dbeta[ch] * invP - xh * dgamma[ch] * invP);
+      float mu[N], rs[N], gm[N], dg[N], db[N];
+      ldc<N>(mean + c, mu); ldc<N>(rstd + c, rs); ldc<N>(gamma + c, gm); ldc<N>(dgamma + c, dg); ldc<N>(dbeta + c, db);
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const float xh = (v[e] - mu[e]) * rs[e];
+        d[e] = gm[e] * rs[e] * (d[e] - db[e] * invP - xh * dg[e] * invP);
       }
-      d = make_float4(dd[0], dd[1], dd[2], dd[3]);
     }
-    Vec4<T>::store(reinterpret_cast<T*>(dx.p) + vidx(dx, b, y, xx, c), d);
+    VW<T>::store(reinterpret_cast<T*>(dx.p) + vidx(dx, b, yy, xx, c), d);
   }
 }
 
@@ -267,56 +355,73 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, int B, int C,
 // that consume y1/y2 (each input element is re-read 4-16x by the im2col) stage plain
 // operands with no per-load transform.
 template <typename T>
-__global__ void __launch_bounds__(256) bn_apply_kernel(View x, int B, int C, const float* scale, const float* shift,
-                                                       View y1, float s1, View y2, float s2, int has2) {
-  const int cq = C >> 2;
-  const long long HW = (long long)x.H * x.W, total = HW * B * cq;
+__global__ void __launch_bounds__(256) bn_apply_kernel(View x, PixDiv pd, long long P, int C, const float* scale,
+                                                       const float* shift, View y1, float s1, View y2, float s2,
+                                                       int has2) {
+  constexpr int N = VW<T>::N;
+  const int CG = C / N;
+  const long long total = P * CG;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(idx % cq);
-    const long long pix = idx / cq;
-    const int b = (int)(pix / HW), rem = (int)(pix % HW);
-    const int yy = rem / x.W, xx = rem % x.W;
-    const int c = 4 * q;
-    float4 v = vload<T>(x, b, yy, xx, c);
+    const int cg = (int)(idx % CG);
+    const long long pix = idx / CG;
+    int b, yy, xx;
+    pix_bxy(pd, pix, b, yy, xx);
+    const int c = N * cg;
+    float v[N], o[N];
+    VW<T>::load(vptr<T>(x, b, yy, xx, c), v);
     if (scale) {
-      const float4 sc = *reinterpret_cast<const float4*>(scale + c);
-      const float4 sh = *reinterpret_cast<const float4*>(shift + c);
-      v = make_float4(fmaf(v.x, sc.x, sh.x), fmaf(v.y, sc.y, sh.y), fmaf(v.z, sc.z, sh.z), fmaf(v.w, sc.w, sh.w));
+      float sc[N], sh[N];
+      ldc<N>(scale + c, sc); ldc<N>(shift + c, sh);
+#pragma unroll
+      for (int e = 0; e < N; ++e) v[e] = fmaf(v[e], sc[e], sh[e]);
     }
-    Vec4<T>::store(reinterpret_cast<T*>(y1.p) + vidx(y1, b, yy, xx, c),
-                   make_float4(act(v.x, s1), act(v.y, s1), act(v.z, s1), act(v.w, s1)));
-    if (has2)
-      Vec4<T>::store(reinterpret_cast<T*>(y2.p) + vidx(y2, b, yy, xx, c),
-                     make_float4(act(v.x, s2), act(v.y, s2), act(v.z, s2), act(v.w, s2)));
+#pragma unroll
+    for (int e = 0; e < N; ++e) o[e] = act(v[e], s1);
+    VW<T>::store(reinterpret_cast<T*>(y1.p) + vidx(y1, b, yy, xx, c), o);
+    if (has2) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) o[e] = act(v[e], s2);
+      VW<T>::store(reinterpret_cast<T*>(y2.p) + vidx(y2, b, yy, xx, c), o);
+    }
   }
 }
 
 // part[chunk][c] = sum over the chunk's pixels of x (conv bias gradients)
 template <typename T>
-__global__ void __launch_bounds__(256) chan_sum_kernel(View x, int B, int C, float* part, int nchunks) {
-  const int cq = C >> 2;
-  const int ppb = 256 / cq;
-  const int q = threadIdx.x % cq, pl = threadIdx.x / cq;
-  const long long HW = (long long)x.H * x.W, P = HW * B;
+__global__ void __launch_bounds__(256) chan_sum_kernel(View x, PixDiv pd, long long P, int C, float* part, int nchunks) {
+  constexpr int N = VW<T>::N;
+  const int CG = C / N;
+  const int RL = 256 / CG;
+  const int cg = threadIdx.x % CG, pl = threadIdx.x / CG;
   const long long per = (P + nchunks - 1) / nchunks;
   const long long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  __shared__ float red[256][4];
-  float a[4] = {0, 0, 0, 0};
-  if (pl < ppb) {
-    for (long long pix = p0 + pl; pix < p1; pix += ppb) {
-      const int b = (int)(pix / HW), rem = (int)(pix % HW);
-      const float4 v = vload<T>(x, b, rem / x.W, rem % x.W, 4 * q);
-      a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
+  __shared__ float red[256][N];
+  float a[N];
+#pragma unroll
+  for (int e = 0; e < N; ++e) a[e] = 0.f;
+  if (pl < RL) {
+    for (long long pix = p0 + pl; pix < p1; pix += RL) {
+      int b, yy, xx;
+      pix_bxy(pd, pix, b, yy, xx);
+      float v[N];
+      VW<T>::load(vptr<T>(x, b, yy, xx, N * cg), v);
+#pragma unroll
+      for (int e = 0; e < N; ++e) a[e] += v[e];
     }
   }
-  for (int e = 0; e < 4; ++e) red[threadIdx.x][e] = a[e];
+#pragma unroll
+  for (int e = 0; e < N; ++e) red[threadIdx.x][e] = a[e];
   __syncthreads();
-  if (threadIdx.x < cq) {
-    float r[4] = {0, 0, 0, 0};
-    for (int k = 0; k < ppb; ++k)
-      for (int e = 0; e < 4; ++e) r[e] += red[k * cq + q][e];
-    for (int e = 0; e < 4; ++e) part[(long long)blockIdx.x * C + 4 * q + e] = r[e];
+  if (pl == 0) {
+    float r[N];
+#pragma unroll
+    for (int e = 0; e < N; ++e) r[e] = 0.f;
+    for (int k = 0; k < RL; ++k)
+#pragma unroll
+      for (int e = 0; e < N; ++e) r[e] += red[k * CG + cg][e];
+#pragma unroll
+    for (int e = 0; e < N; ++e) part[(long long)blockIdx.x * C + N * cg + e] = r[e];
   }
 }
 
@@ -351,41 +456,51 @@ using namespace stc;
 
 extern "C" int stc_chan_stats_chunks(int B, int H, int W) { return stat_chunks((long long)B * H * W); }
 
+static bool vec_ok(int dtype, int C, const stc_view& v) {
+  const int N = dtype == STC_F32 ? 4 : 8;
+  return C % N == 0 && C / N <= 256 && v.cs == 1 && v.co % N == 0 && v.ps % N == 0 && v.rs % N == 0 && v.bs % N == 0;
+}
+
 extern "C" int stc_chan_stats(int dtype, int B, stc_view x, int C, float* part, int nchunks, void* stream) {
-  STC_REQUIRE(C % 4 == 0 && C <= 1024, "stc_chan_stats: C=%d must be a multiple of 4 and <= 1024", C);
-  STC_REQUIRE(x.cs == 1 && x.co % 4 == 0 && x.ps % 4 == 0, "stc_chan_stats: NHWC view, 4-aligned");
+  STC_REQUIRE(vec_ok(dtype, C, x), "stc_chan_stats: C=%d / view not 16-byte vectorisable (NHWC, <= 256 vectors)", C);
   hipStream_t st = (hipStream_t)stream;
   View v = mkview(x);
-  if (dtype == STC_F32) hipLaunchKernelGGL(chan_stats_kernel<float>, dim3(nchunks), dim3(256), 0, st, v, B, C, part, nchunks);
-  else hipLaunchKernelGGL(chan_stats_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, v, B, C, part, nchunks);
+  const PixDiv pd = mkpix(B, x.H, x.W);
+  const long long P = (long long)B * x.H * x.W;
+  if (dtype == STC_F32) hipLaunchKernelGGL(chan_stats_kernel<float>, dim3(nchunks), dim3(256), 0, st, v, pd, P, C, part, nchunks);
+  else hipLaunchKernelGGL(chan_stats_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, v, pd, P, C, part, nchunks);
   STC_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int stc_bn_apply(int dtype, int B, stc_view x, int C, const float* scale, const float* shift, stc_view y1,
                             float slope1, stc_view y2, float slope2, void* stream) {
-  STC_REQUIRE(C % 4 == 0, "stc_bn_apply: C=%d must be a multiple of 4", C);
   STC_REQUIRE((scale == nullptr) == (shift == nullptr), "stc_bn_apply: scale/shift must come together");
-  STC_REQUIRE(x.cs == 1 && y1.cs == 1 && y1.p, "stc_bn_apply: NHWC views required");
+  STC_REQUIRE(y1.p && vec_ok(dtype, C, x) && vec_ok(dtype, C, y1) && (!y2.p || vec_ok(dtype, C, y2)),
+              "stc_bn_apply: C=%d / views not 16-byte vectorisable NHWC", C);
   hipStream_t st = (hipStream_t)stream;
   View v = mkview(x), o1 = mkview(y1), o2 = y2.p ? mkview(y2) : mkview(y1);
-  const long long work = (long long)B * x.H * x.W * (C / 4);
-  const int blocks = grid_for(work);
+  const PixDiv pd = mkpix(B, x.H, x.W);
+  const long long P = (long long)B * x.H * x.W;
+  const int N = dtype == STC_F32 ? 4 : 8;
+  const int blocks = grid_for(P * (C / N));
   if (dtype == STC_F32)
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(blocks), dim3(256), 0, st, v, B, C, scale, shift, o1, slope1, o2, slope2, y2.p != nullptr ? 1 : 0);
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(blocks), dim3(256), 0, st, v, pd, P, C, scale, shift, o1, slope1, o2, slope2, y2.p != nullptr ? 1 : 0);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(blocks), dim3(256), 0, st, v, B, C, scale, shift, o1, slope1, o2, slope2, y2.p != nullptr ? 1 : 0);
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(blocks), dim3(256), 0, st, v, pd, P, C, scale, shift, o1, slope1, o2, slope2, y2.p != nullptr ? 1 : 0);
   STC_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int stc_chan_sum(int dtype, int B, stc_view x, int C, int Cout, float* part, int nchunks, float* out,
                             void* stream) {
-  STC_REQUIRE(C % 4 == 0 && C <= 1024 && Cout <= C, "stc_chan_sum: bad C=%d", C);
+  STC_REQUIRE(vec_ok(dtype, C, x) && Cout <= C, "stc_chan_sum: bad C=%d / view", C);
   hipStream_t st = (hipStream_t)stream;
   View v = mkview(x);
-  if (dtype == STC_F32) hipLaunchKernelGGL(chan_sum_kernel<float>, dim3(nchunks), dim3(256), 0, st, v, B, C, part, nchunks);
-  else hipLaunchKernelGGL(chan_sum_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, v, B, C, part, nchunks);
+  const PixDiv pd = mkpix(B, x.H, x.W);
+  const long long P = (long long)B * x.H * x.W;
+  if (dtype == STC_F32) hipLaunchKernelGGL(chan_sum_kernel<float>, dim3(nchunks), dim3(256), 0, st, v, pd, P, C, part, nchunks);
+  else hipLaunchKernelGGL(chan_sum_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, v, pd, P, C, part, nchunks);
   STC_CHECK_LAUNCH();
   hipLaunchKernelGGL(chan_sum_final_kernel, dim3(C), dim3(256), 0, st, (const float*)part, nchunks, C, Cout, out);
   STC_CHECK_LAUNCH();
@@ -412,15 +527,18 @@ extern "C" int stc_bn_finalize(const float* part, int nchunks, int C, const floa
 extern "C" int stc_bn_bwd_reduce(int dtype, int B, stc_view x, int C, const float* scale, const float* shift,
                                  const float* mean, const float* rstd, stc_view g1, float slope1, stc_view g2,
                                  float slope2, float* part2, int nchunks, void* stream) {
-  STC_REQUIRE(C % 4 == 0 && C <= 1024, "stc_bn_bwd_reduce: bad C=%d", C);
+  STC_REQUIRE(vec_ok(dtype, C, x) && (!g1.p || vec_ok(dtype, C, g1)) && (!g2.p || vec_ok(dtype, C, g2)),
+              "stc_bn_bwd_reduce: bad C=%d / views", C);
   STC_REQUIRE(scale && shift && mean && rstd, "stc_bn_bwd_reduce: BN tables required");
   hipStream_t st = (hipStream_t)stream;
   GradIn gi = mkgrad(g1, slope1, g2, slope2);
   View v = mkview(x);
+  const PixDiv pd = mkpix(B, x.H, x.W);
+  const long long P = (long long)B * x.H * x.W;
   if (dtype == STC_F32)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(nchunks), dim3(256), 0, st, v, B, C, scale, shift, mean, rstd, gi, part2, nchunks);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(nchunks), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gi, part2, nchunks);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, v, B, C, scale, shift, mean, rstd, gi, part2, nchunks);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gi, part2, nchunks);
   STC_CHECK_LAUNCH();
   return 0;
 }
@@ -429,7 +547,9 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
                                 const float* mean, const float* rstd, const float* gamma, stc_view g1, float slope1,
                                 stc_view g2, float slope2, const float* part2, int nchunks, stc_view dx,
                                 float* dgamma, float* dbeta, void* stream) {
-  STC_REQUIRE(C % 4 == 0, "stc_bn_bwd_apply: bad C=%d", C);
+  STC_REQUIRE(vec_ok(dtype, C, x) && vec_ok(dtype, C, dx) && (!g1.p || vec_ok(dtype, C, g1)) &&
+                  (!g2.p || vec_ok(dtype, C, g2)),
+              "stc_bn_bwd_apply: bad C=%d / views", C);
   hipStream_t st = (hipStream_t)stream;
   GradIn gi = mkgrad(g1, slope1, g2, slope2);
   if (mean) {
@@ -438,11 +558,13 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
     STC_CHECK_LAUNCH();
   }
   View v = mkview(x), o = mkview(dx);
-  const long long work = (long long)B * x.H * x.W * (C / 4);
+  const PixDiv pd = mkpix(B, x.H, x.W);
+  const long long P = (long long)B * x.H * x.W;
+  const long long work = P * (C / (dtype == STC_F32 ? 4 : 8));
   if (dtype == STC_F32)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_for(work)), dim3(256), 0, st, v, B, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_for(work)), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(grid_for(work)), dim3(256), 0, st, v, B, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(grid_for(work)), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o);
   STC_CHECK_LAUNCH();
   return 0;
 }
