@@ -123,6 +123,17 @@ enum { STC_PACK_CONV_FWD = 0, STC_PACK_CONV_DGRAD = 1, STC_PACK_CONV_S1_DGRAD = 
        STC_PACK_CONVT_FWD = 3, STC_PACK_CONVT_DGRAD = 4 };
 int stc_pack_weight(int dtype, int mode, const float* W, int P, int Q,
                     void* out, int N_pad, int C_pad, void* stream);
+/* Multi-tensor packing: all stale packed operands of a network after an optimiser step in one
+ * launch (n <= STC_PACK_MAX descriptors, each as stc_pack_weight's arguments).               */
+#define STC_PACK_MAX 40
+typedef struct {
+  int32_t mode;
+  int32_t P, Q, N_pad, C_pad;
+  int32_t pad_;
+  const float* W;
+  void* out;
+} stc_pack_desc;
+int stc_pack_weights(int dtype, int n, const stc_pack_desc* descs, void* stream);
 
 /* ---- batch norm -------------------------------------------------------------
  * stc_chan_stats: per-channel partial statistics of x over pixel chunks:

@@ -280,6 +280,80 @@ extern "C" int stc_loss_bwd(int kind, const float* p, const float* t, float c, i
   return 0;
 }
 
+// Multi-tensor form: one launch packs up to STC_PACK_MAX weights; block ranges per descriptor.
+struct PackSet {
+  stc_pack_desc d[STC_PACK_MAX];
+  int bstart[STC_PACK_MAX + 1];
+  int n;
+};
+
+template <typename T>
+__global__ void pack_multi_kernel(const PackSet ps) {
+  int i = 0;
+  while (i + 1 < ps.n && (int)blockIdx.x >= ps.bstart[i + 1]) ++i;
+  const stc_pack_desc& d = ps.d[i];
+  const int mode = d.mode;
+  const bool phased = mode == STC_PACK_CONV_DGRAD || mode == STC_PACK_CONVT_FWD;
+  const int taps = phased ? 4 : 16;
+  const long long total = (long long)d.N_pad * d.C_pad;
+  const bool n_is_p = (mode == STC_PACK_CONV_FWD || mode == STC_PACK_CONVT_DGRAD);
+  const int nblk = ps.bstart[i + 1] - ps.bstart[i];
+  T* out = reinterpret_cast<T*>(d.out);
+  for (long long idx = (long long)(blockIdx.x - ps.bstart[i]) * blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)nblk * blockDim.x) {
+    const int c = (int)(idx % d.C_pad);
+    const int n = (int)(idx / d.C_pad);
+    const int pi = n_is_p ? n : c, qi = n_is_p ? c : n;
+    float w[16];
+    if (pi < d.P && qi < d.Q) {
+      const float4* src = reinterpret_cast<const float4*>(d.W + ((long long)pi * d.Q + qi) * 16);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float4 f = src[v];
+        w[4 * v] = f.x; w[4 * v + 1] = f.y; w[4 * v + 2] = f.z; w[4 * v + 3] = f.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) w[t] = 0.f;
+    }
+    if (taps == 16) {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) st1<T>(out + ((long long)n * 16 + t) * d.C_pad + c, w[t]);
+    } else {
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int ph = z >> 1, pw = z & 1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int kh = (1 - ph) + 2 * (t >> 1), kw = (1 - pw) + 2 * (t & 1);
+          st1<T>(out + (((long long)z * d.N_pad + n) * 4 + t) * d.C_pad + c, w[kh * 4 + kw]);
+        }
+      }
+    }
+  }
+}
+
+extern "C" int stc_pack_weights(int dtype, int n, const stc_pack_desc* descs, void* stream) {
+  STC_REQUIRE(n >= 0 && n <= STC_PACK_MAX && (n == 0 || descs), "stc_pack_weights: bad count %d", n);
+  if (n == 0) return 0;
+  PackSet ps{};
+  ps.n = n;
+  int b = 0;
+  for (int i = 0; i < n; ++i) {
+    STC_REQUIRE(descs[i].mode >= 0 && descs[i].mode <= 4 && descs[i].W && descs[i].out, "stc_pack_weights: bad desc %d", i);
+    ps.d[i] = descs[i];
+    ps.bstart[i] = b;
+    const long long total = (long long)descs[i].N_pad * descs[i].C_pad;
+    b += (int)std::max<long long>(1, std::min<long long>((total + 255) / 256, 1024));
+  }
+  ps.bstart[n] = b;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == STC_F32) hipLaunchKernelGGL(pack_multi_kernel<float>, dim3(b), dim3(256), 0, st, ps);
+  else hipLaunchKernelGGL(pack_multi_kernel<bf16>, dim3(b), dim3(256), 0, st, ps);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int stc_pack_weight(int dtype, int mode, const float* W, int P, int Q, void* out, int N_pad, int C_pad,
                                void* stream) {
   STC_REQUIRE(mode >= 0 && mode <= 4, "stc_pack_weight: bad mode");

@@ -27,6 +27,14 @@ class View(ctypes.Structure):
 
 NULL_VIEW = View(None, 0, 0, 0, 0, 0, 0, 1, 0)
 
+PACK_MAX = 40
+
+
+class PackDesc(ctypes.Structure):
+    """stc_pack_desc: one stc_pack_weight job of a multi-tensor stc_pack_weights launch."""
+    _fields_ = [("mode", ctypes.c_int32), ("P", ctypes.c_int32), ("Q", ctypes.c_int32), ("N_pad", ctypes.c_int32),
+                ("C_pad", ctypes.c_int32), ("pad_", ctypes.c_int32), ("W", ctypes.c_void_p), ("out", ctypes.c_void_p)]
+
 _vp, _i32, _i64, _f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 
 # name: (restype, argtypes)
@@ -42,6 +50,7 @@ _SIGS = {
                               _f32, _vp, _vp, _i64, _vp]),
     "stc_conv_wgrad_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32]),
     "stc_pack_weight": (_i32, [_i32, _i32, _vp, _i32, _i32, _vp, _i32, _i32, _vp]),
+    "stc_pack_weights": (_i32, [_i32, _i32, _vp, _vp]),
     "stc_chan_stats": (_i32, [_i32, _i32, View, _i32, _vp, _i32, _vp]),
     "stc_chan_stats_chunks": (_i32, [_i32, _i32, _i32]),
     "stc_chan_sum": (_i32, [_i32, _i32, View, _i32, _i32, _vp, _i32, _vp, _vp]),

@@ -395,6 +395,7 @@ class NetFn(torch.autograd.Function):
         plan, kind, train, dt, cache, nsrc = ctrl
         sources = [t.contiguous().float() for t in tensors[:nsrc]]
         save = train and any(ctx.needs_input_grad[1:])
+        ops.refresh_packs(cache)  # all operands packed since the last optimiser step, one launch
         fwd = gen_forward if kind == "G" else disc_forward
         out, saved = fwd(plan, sources, train, dt, cache, save)
         ctx.ctrl = ctrl

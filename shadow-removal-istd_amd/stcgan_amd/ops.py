@@ -210,15 +210,47 @@ def bump(params):
 
 
 def packed(cache, W, mode, n_pad, c_pad, dt):
-    """Cached packed weight; repacked when the parameter changed (version or optimizer step)."""
+    """Cached packed weight; repacked when the parameter changed (version or optimizer step).
+    Every key is remembered so that refresh_packs() can repack all stale ones in one launch."""
     key = (id(W), mode, n_pad, c_pad, dt)
     ver = (W._version, _GEN.get(id(W), 0), W.data_ptr())
     hit = cache.get(key)
     if hit is not None and hit[0] == ver:
         return hit[1]
+    cache.setdefault("__keys__", {})[key] = (W, mode, n_pad, c_pad, dt)
     t = pack(mode, W, n_pad, c_pad, dt)
     cache[key] = (ver, t)
     return t
+
+
+def refresh_packs(cache):
+    """Repack every stale cached operand of a network (after an optimiser step) with one
+    multi-tensor launch per dtype (stc_pack_weights), reusing the packed buffers in place."""
+    keys = cache.get("__keys__")
+    if not keys:
+        return
+    jobs = {}
+    for key, (W, mode, n_pad, c_pad, dt) in keys.items():
+        ver = (W._version, _GEN.get(id(W), 0), W.data_ptr())
+        hit = cache.get(key)
+        if hit is not None and hit[0] == ver:
+            continue
+        if hit is None:
+            nph, taps = (4, 4) if mode in _PHASED else (1, 16)
+            out = torch.empty((nph, n_pad, taps, c_pad), dtype=dt, device=W.device)
+        else:
+            out = hit[1]
+        Wc = W.detach()
+        assert Wc.is_contiguous()
+        jobs.setdefault(dt, []).append((L.PackDesc(mode, W.shape[0], W.shape[1], n_pad, c_pad, 0, Wc.data_ptr(),
+                                                   out.data_ptr()), key, ver, out))
+    for dt, lst in jobs.items():
+        for i in range(0, len(lst), L.PACK_MAX):
+            chunk = lst[i:i + L.PACK_MAX]
+            arr = (L.PackDesc * len(chunk))(*[c[0] for c in chunk])
+            check(lib().stc_pack_weights(L.dtype_code(dt), len(chunk), arr, stream()), "stc_pack_weights")
+            for _, key, ver, out in chunk:
+                cache[key] = (ver, out)
 
 
 def stats_chunks(B, H, W):
