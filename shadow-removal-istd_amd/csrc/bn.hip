@@ -109,6 +109,7 @@ __global__ void __launch_bounds__(256) chan_stats_kernel(View x, PixDiv pd, long
     int b, yy, xx;
     pix_bxy(pd, p0, b, yy, xx);
     VW<T>::load(vptr<T>(x, b, yy, xx, N * cg), sh);
+#pragma unroll 4
     for (long long pix = p0 + pl; pix < p1; pix += RL) {
       pix_bxy(pd, pix, b, yy, xx);
       float v[N];
@@ -257,6 +258,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(View x, PixDiv pd, l
     const int c = N * cg;
     float sc[N], shf[N], mu[N], rs[N];
     ldc<N>(scale + c, sc); ldc<N>(shift + c, shf); ldc<N>(mean + c, mu); ldc<N>(rstd + c, rs);
+#pragma unroll 4
     for (long long pix = p0 + pl; pix < p1; pix += RL) {
       int b, yy, xx;
       pix_bxy(pd, pix, b, yy, xx);

@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
   constexpr int ROWS = TY / 4;             // grid rows per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int img = blockIdx.x / p.tiles_per_img, tix = blockIdx.x % p.tiles_per_img;
   const int y0 = (tix / p.tiles_x) * TY, x0 = (tix % p.tiles_x) * TX;
   const int split = blockIdx.y;
@@ -218,9 +218,9 @@ static size_t halo_lds(int geom, int ty) {
 
 // Narrow plan: {ty, nsplit}.  Enough blocks to cover the chip ~2x.
 static void narrow_plan(int geom, int B, int GH, int GW, int cin, int* ty, int* nsplit) {
-  *ty = 16;
+  *ty = 8;
   const int nchunks = cin / 64;
-  const long long blocks = (long long)B * cdiv(GH, 16) * cdiv(GW, 16);
+  const long long blocks = (long long)B * cdiv(GH, *ty) * cdiv(GW, 16);
   int ns = 1;
   while (blocks * ns < 1024 && ns * 2 <= nchunks) ns *= 2;
   *nsplit = ns;
@@ -277,10 +277,10 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
   dim3 grid((unsigned)(B * p.tiles_per_img), (unsigned)p.nsplit);
   const size_t lds = halo_lds(geom, ty);
   if (geom == 0) {
-    if (p.NP <= 16) hipLaunchKernelGGL((narrow_halo_kernel<0, 1, 16>), grid, dim3(256), lds, st, p);
-    else hipLaunchKernelGGL((narrow_halo_kernel<0, 2, 16>), grid, dim3(256), lds, st, p);
+    if (p.NP <= 16) hipLaunchKernelGGL((narrow_halo_kernel<0, 1, 8>), grid, dim3(256), lds, st, p);
+    else hipLaunchKernelGGL((narrow_halo_kernel<0, 2, 8>), grid, dim3(256), lds, st, p);
   } else {
-    hipLaunchKernelGGL((narrow_halo_kernel<1, 1, 16>), grid, dim3(256), lds, st, p);
+    hipLaunchKernelGGL((narrow_halo_kernel<1, 1, 8>), grid, dim3(256), lds, st, p);
   }
   STC_CHECK_LAUNCH();
   if (p.nsplit > 1) {

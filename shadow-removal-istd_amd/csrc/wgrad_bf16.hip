@@ -50,15 +50,40 @@ __device__ __forceinline__ int fdiv(int n, int d, float inv) {
   return q;
 }
 
-__device__ __forceinline__ int wswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// LDS image swizzle of a [pixel][W channels] operand row (W*2 bytes, CH = W/8 chunks):
+//   CH = 16 (256-B rows): chunk ^ ((row&3)<<2 | (row>>2)&3)   (T10 image (b))
+//   CH = 8  (128-B rows): chunk ^ (2*((row>>1)&1) + 4*((row>>3)&1))
+//   CH = 2  (32-B rows) : none (2-way conflicts on a small operand)
+// chosen so that the transposed 16x16x32 operand reads (rows 8g+q, g = 0/1 per 32-lane half) hit
+// distinct bank slots.
+template <int CH>
+__device__ __forceinline__ int wswz(int row) {
+  if constexpr (CH == 16) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else if constexpr (CH == 8) return 2 * ((row >> 1) & 1) + 4 * ((row >> 3) & 1);
+  else return 0;
+}
 
-constexpr int WB_BM = 128, WB_BN = 128, WB_BK = 64;
-constexpr int WB_TILE = WB_BK * 256;  // bytes per operand per stage
+constexpr int WB_BK = 64;
 
-__global__ void __launch_bounds__(256) wgrad_bf16_kernel(const WbParams p) {
+// Operand roles: the "row" operand (MFMA M) and the "column" operand (MFMA N) each come from either
+// D (plain pixel-major channels r) or Gcol (im2col columns tap*Cg + ci).  SWAP = false: rows = D
+// (r), columns = Gcol; SWAP = true (R <= 16): rows = Gcol, columns = D, so the tiny R dimension
+// becomes a 16-wide MFMA N tile instead of wasting 7/8 of a 128-row tile.
+template <int BM, int BN, int WM, int WN, bool SWAP>
+__global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams p) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int CHA = BM / 8, CHB = BN / 8;            // 16-byte chunks per pixel row
+  constexpr int ROWA = BM * 2, ROWB = BN * 2;          // bytes per pixel row
+  constexpr int PA = WB_BK * ROWA / 1024, PB = WB_BK * ROWB / 1024;  // 1 KiB DMA pieces per step
+  constexpr int TILEA = WB_BK * ROWA, TILEB = WB_BK * ROWB;
+  constexpr int STAGE = TILEA + TILEB;
+  constexpr int IA = (PA + NW - 1) / NW, IB = (PB + NW - 1) / NW;
+  static_assert(FM >= 1 && FN >= 1 && PA >= 1 && PB >= 1, "tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
   const int nwg = p.mtiles * p.ntiles;
   int bid = blockIdx.x;
   {
@@ -66,7 +91,7 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(const WbParams p) {
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
   const int mt = bid / p.ntiles, nt = bid % p.ntiles;
-  const int r0 = mt * WB_BM, c0 = nt * WB_BN;
+  const int a0 = mt * BM, b0 = nt * BN;  // first row / column of the tile
   const int split = blockIdx.z;
   const int pbeg = split * p.pchunk;
   const int pend = min(p.P, pbeg + p.pchunk);
@@ -77,91 +102,139 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(const WbParams p) {
   const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, (int)p.g_bytes, 0x00020000);
   const unsigned OOBV = 0x80000000u;
 
-  // DMA roles: a piece = 4 pixel rows x 256 B; lane -> row (lane>>4) of the piece, LDS slot lane&15.
-  // Each wave issues pieces wave, wave+4, ... (4 per operand per step).
-  const int prow = lane >> 4;
-  // per-lane column roles (fixed over the K loop): the chunk this lane loads depends on its row's swizzle,
-  // and rows 4*pc + prow have (row & 3) = prow and ((row >> 2) & 3) = pc & 3 -> per piece constant.
-  int d_chunk_off[4], g_tap_dy[4], g_tap_dx[4], g_ci[4];
-  unsigned d_pen[4], g_pen[4];
+  // A piece of an operand with CH chunks per row covers 64/CH rows; lane -> (row lane/CH, slot lane%CH).
+  struct Role {
+    int chan_off;     // D: channel offset (co + r); G: co + ci
+    int dy, dx;       // G tap offsets
+    unsigned pen;     // column out of range
+  };
+  auto role = [&](bool is_g, int ch_per_row, int piece, int first) -> Role {
+    const int rows_pp = 64 / ch_per_row;
+    const int row = piece * rows_pp + lane / ch_per_row;
+    int swz = 0;
+    if (ch_per_row == 16) swz = wswz<16>(row);
+    else if (ch_per_row == 8) swz = wswz<8>(row);
+    const int chunk = (lane % ch_per_row) ^ swz;
+    Role ro{};
+    if (!is_g) {
+      const int r = first + chunk * 8;
+      ro.chan_off = p.d_co + r;
+      ro.pen = r < p.R ? 0u : OOBV;
+    } else {
+      const int col = first + chunk * 8;
+      const int tap = col / p.Cg;
+      ro.chan_off = p.g_co + col - tap * p.Cg;
+      ro.dy = (tap >> 2) - 1;
+      ro.dx = (tap & 3) - 1;
+      ro.pen = col < p.Ncol ? 0u : OOBV;
+    }
+    return ro;
+  };
+  Role ra_[IA], rb_[IB];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int pc = wave + 4 * i;  // piece index 0..15
-    const int row = 4 * pc + prow;
-    const int chunk = (lane & 15) ^ wswz(row);
-    const int rr = r0 + chunk * 8;
-    d_chunk_off[i] = p.d_co + rr;
-    d_pen[i] = rr < p.R ? 0u : OOBV;
-    const int col = c0 + chunk * 8;
-    const int tap = col / p.Cg;
-    g_ci[i] = p.g_co + col - tap * p.Cg;
-    g_tap_dy[i] = (tap >> 2) - 1;
-    g_tap_dx[i] = (tap & 3) - 1;
-    g_pen[i] = col < p.Ncol ? 0u : OOBV;
-  }
+  for (int i = 0; i < IA; ++i) ra_[i] = role(SWAP, CHA, wave + NW * i, a0);
+#pragma unroll
+  for (int i = 0; i < IB; ++i) rb_[i] = role(!SWAP, CHB, wave + NW * i, b0);
 
-  auto issue = [&](int s, int stage) {
-    char* sD = smem + stage * 2 * WB_TILE;
-    char* sG = sD + WB_TILE;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int pc = wave + 4 * i;
-      const int pix = pbeg + s * WB_BK + 4 * pc + prow;
-      const unsigned ppen = pix < pend ? 0u : OOBV;
-      const int pp = pix < pend ? pix : pbeg;
-      const int b = fdiv(pp, GHW, p.inv_ghw), rem = pp - b * GHW;
-      const int oy = fdiv(rem, p.GW, p.inv_gw), ox = rem - oy * p.GW;
-      const unsigned doff = (((unsigned)b * (unsigned)p.d_bs + (unsigned)oy * (unsigned)p.d_rs +
-                              (unsigned)ox * (unsigned)p.d_ps + (unsigned)d_chunk_off[i]) * 2u) | ppen | d_pen[i];
-      wdma16(rd, sD + pc * 1024, doff);
-      const int iy = oy * p.stride + g_tap_dy[i], ix = ox * p.stride + g_tap_dx[i];
+  struct Pix {
+    int b, oy, ox;
+    unsigned pen;
+  };
+  auto pixel = [&](int rows_pp, int piece, int s) -> Pix {
+    const int pix = pbeg + s * WB_BK + piece * rows_pp + lane / (64 / rows_pp);
+    Pix px;
+    px.pen = pix < pend ? 0u : OOBV;
+    const int pp = pix < pend ? pix : pbeg;
+    px.b = fdiv(pp, GHW, p.inv_ghw);
+    const int rem = pp - px.b * GHW;
+    px.oy = fdiv(rem, p.GW, p.inv_gw);
+    px.ox = rem - px.oy * p.GW;
+    return px;
+  };
+  auto dma_piece = [&](bool is_g, const Role& ro, const Pix& px, int piece, char* dst) {
+    if (!is_g) {
+      const unsigned off = (((unsigned)px.b * (unsigned)p.d_bs + (unsigned)px.oy * (unsigned)p.d_rs +
+                             (unsigned)px.ox * (unsigned)p.d_ps + (unsigned)ro.chan_off) * 2u) | px.pen | ro.pen;
+      wdma16(rd, dst + piece * 1024, off);
+    } else {
+      const int iy = px.oy * p.stride + ro.dy, ix = px.ox * p.stride + ro.dx;
       const unsigned ipen = ((unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) ? 0u : OOBV;
-      const unsigned goff = (((unsigned)b * (unsigned)p.g_bs + (unsigned)iy * (unsigned)p.g_rs +
-                              (unsigned)ix * (unsigned)p.g_ps + (unsigned)g_ci[i]) * 2u) | ppen | g_pen[i] | ipen;
-      wdma16(rg, sG + pc * 1024, goff);
+      const unsigned off = (((unsigned)px.b * (unsigned)p.g_bs + (unsigned)iy * (unsigned)p.g_rs +
+                             (unsigned)ix * (unsigned)p.g_ps + (unsigned)ro.chan_off) * 2u) | px.pen | ro.pen | ipen;
+      wdma16(rg, dst + piece * 1024, off);
     }
   };
 
-  floatx4 acc[4][4];
+  auto issue = [&](int s, int stage) {
+    char* sA = smem + stage * STAGE;
+    char* sB = sA + TILEA;
+    if constexpr (CHA == CHB && IA == IB) {  // A and B pieces cover the same pixel rows
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < IA; ++i) {
+        const int pc = wave + NW * i;
+        if (pc < PA) {
+          const Pix px = pixel(64 / CHA, pc, s);
+          dma_piece(SWAP, ra_[i], px, pc, sA);
+          dma_piece(!SWAP, rb_[i], px, pc, sB);
+        }
+      }
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < IA; ++i) {
+        const int pc = wave + NW * i;
+        if (pc < PA) dma_piece(SWAP, ra_[i], pixel(64 / CHA, pc, s), pc, sA);
+      }
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int pc = wave + NW * i;
+        if (pc < PB) dma_piece(!SWAP, rb_[i], pixel(64 / CHB, pc, s), pc, sB);
+      }
+    }
+  };
 
-  // transposed-read addressing: lane 4q+p of 16-lane group g reads row (8g + q [+4]), columns 4p..4p+3
-  // of the fragment's 16 columns.  Byte offset of (row, col) = 256*row + 16*((col>>3) ^ wswz(row)) + 2*(col&7).
-  const int kq = lane >> 4;       // k-chunk: pixels 8*kq .. 8*kq+7 of the 32-pixel sub-step
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed reads: lane 4q+p of 16-lane group kq reads row 8*kq + q (+4), columns 4p..4p+3 of the
+  // fragment's 16 columns; byte offset of (row, col) = row*ROW + 16*((col>>3) ^ swz(row)) + 2*(col&7).
+  const int kq = lane >> 4;
   const int q = (lane & 15) >> 2, pcol = lane & 3;
-  auto tr_off = [&](int row, int colbase) {
+  auto tr_off = [&](int row, int colbase, int rowbytes, int ch) {
     const int col = colbase + 4 * pcol;
-    return 256 * row + 16 * ((col >> 3) ^ wswz(row)) + 2 * (col & 7);
+    int swz = 0;
+    if (ch == 16) swz = wswz<16>(row);
+    else if (ch == 8) swz = wswz<8>(row);
+    return row * rowbytes + 16 * ((col >> 3) ^ swz) + 2 * (col & 7);
   };
 
   auto compute = [&](int stage) {
-    const char* sD = smem + stage * 2 * WB_TILE;
-    const char* sG = sD + WB_TILE;
+    const char* sA = smem + stage * STAGE;
+    const char* sB = sA + TILEA;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int rowa = kk * 32 + 8 * kq + q;  // rows rowa and rowa + 4
-      wbf16x8 fa[4], fb[4];
+      wbf16x8 fa[FM], fb[FN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int cb = wm * 64 + 16 * i;
-        const w4i16 lo = wtr16(sD + tr_off(rowa, cb)), hi = wtr16(sD + tr_off(rowa + 4, cb));
+      for (int i = 0; i < FM; ++i) {
+        const int cb = wm * TM + 16 * i;
+        const w4i16 lo = wtr16(sA + tr_off(rowa, cb, ROWA, CHA)), hi = wtr16(sA + tr_off(rowa + 4, cb, ROWA, CHA));
         const w4i16 v8[2] = {lo, hi};
         fa[i] = __builtin_bit_cast(wbf16x8, v8);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int cb = wn * 64 + 16 * j;
-        const w4i16 lo = wtr16(sG + tr_off(rowa, cb)), hi = wtr16(sG + tr_off(rowa + 4, cb));
+      for (int j = 0; j < FN; ++j) {
+        const int cb = wn * TN + 16 * j;
+        const w4i16 lo = wtr16(sB + tr_off(rowa, cb, ROWB, CHB)), hi = wtr16(sB + tr_off(rowa + 4, cb, ROWB, CHB));
         const w4i16 v8[2] = {lo, hi};
         fb[j] = __builtin_bit_cast(wbf16x8, v8);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
   };
 
@@ -173,48 +246,65 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(const WbParams p) {
     compute(s & 1);
   }
 
-  // epilogue: acc[i][j][e] = C[r0 + wm*64 + 16i + 4*(lane>>4) + e][c0 + wn*64 + 16j + (lane&15)]
+  // epilogue: acc[i][j][e] = C[a0 + wm*TM + 16i + 4*(lane>>4) + e][b0 + wn*TN + 16j + (lane&15)]
+  // (row, column) = (r, n) or, swapped, (n, r); n = tap*Cg + ci goes to dW[r][ci][tap].
   const int rq = 4 * (lane >> 4), cl = lane & 15;
-  if (p.dW) {
+  float* slab = p.dW ? nullptr : p.ws + (long long)split * p.R * p.Ncol;
+  auto put = [&](int r, int n, int tt, int cc, float v) {
+    if (r >= p.R || n >= p.Ncol) return;
+    if (slab) slab[(long long)r * p.Ncol + n] = v;
+    else if (cc < p.Cg_out) p.dW[((long long)r * p.Cg_out + cc) * 16 + tt] = v;
+  };
+  if (!SWAP && slab) {  // the common split case: plain row-major slab, no tap decomposition
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = c0 + wn * 64 + 16 * j + cl;
-      const int tt = n / p.Cg, cc = n - tt * p.Cg;
-      if (n >= p.Ncol || cc >= p.Cg_out) continue;
+    for (int j = 0; j < FN; ++j) {
+      const int n = b0 + wn * TN + 16 * j + cl;
+      if (n >= p.Ncol) continue;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int m = r0 + wm * 64 + 16 * i + rq + e;
-          if (m < p.R) p.dW[((long long)m * p.Cg_out + cc) * 16 + tt] = acc[i][j][e];
+          const int r = a0 + wm * TM + 16 * i + rq + e;
+          if (r < p.R) slab[(long long)r * p.Ncol + n] = acc[i][j][e];
         }
     }
     return;
   }
-  float* slab = p.ws + (long long)split * p.R * p.Ncol;
+  if constexpr (!SWAP) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < FN; ++j) {
+      const int n = b0 + wn * TN + 16 * j + cl;
+      const int tt = n / p.Cg, cc = n - tt * p.Cg;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = c0 + wn * 64 + 16 * j + cl;
-      if (n >= p.Ncol) continue;
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) put(a0 + wm * TM + 16 * i + rq + e, n, tt, cc, acc[i][j][e]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int m = r0 + wm * 64 + 16 * i + rq + e;
-        if (m < p.R) slab[(long long)m * p.Ncol + n] = acc[i][j][e];
+        const int n = a0 + wm * TM + 16 * i + rq + e;
+        const int tt = n / p.Cg, cc = n - tt * p.Cg;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) put(b0 + wn * TN + 16 * j + cl, n, tt, cc, acc[i][j][e]);
       }
-    }
+  }
 }
 
 // ------------------------------------------------------------------------- host
 struct WbPlan {
-  int mtiles, ntiles, nsplit, pchunk;
+  int cfg;  // 0: 128x128 (rows = D channels), 1: 64x128 (R <= 64), 2: swapped 128x16 (R <= 16)
+  int BM, BN, mtiles, ntiles, nsplit, pchunk;
 };
 
 static WbPlan wb_plan(int P, int R, int Cg) {
   WbPlan pl{};
-  pl.mtiles = cdiv(R, WB_BM);
-  pl.ntiles = cdiv(16LL * Cg, WB_BN);
+  const long long ncol = 16LL * Cg;
+  if (R <= 16) { pl.cfg = 2; pl.BM = 128; pl.BN = 16; pl.mtiles = cdiv(ncol, 128); pl.ntiles = 1; }
+  else if (R <= 64) { pl.cfg = 1; pl.BM = 64; pl.BN = 128; pl.mtiles = cdiv(R, 64); pl.ntiles = cdiv(ncol, 128); }
+  else { pl.cfg = 0; pl.BM = 128; pl.BN = 128; pl.mtiles = cdiv(R, 128); pl.ntiles = cdiv(ncol, 128); }
   const long long tiles = (long long)pl.mtiles * pl.ntiles;
   const int steps = cdiv(P, WB_BK);
   int ns = 1;
@@ -255,19 +345,22 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
   const WbPlan pl = wb_plan(p.P, R, Cg);
   p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.nsplit = pl.nsplit; p.pchunk = pl.pchunk;
   dim3 grid(pl.mtiles * pl.ntiles, 1, pl.nsplit);
-  const size_t lds = 2 * 2 * WB_TILE;
+  const size_t lds = 2 * (size_t)WB_BK * (pl.BM + pl.BN) * 2;
   if (pl.nsplit <= 1) {
     p.dW = dW;
-    hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(256), lds, st, p);
-    STC_CHECK_LAUNCH();
-    return 0;
+  } else {
+    const int64_t need = (int64_t)pl.nsplit * R * 16LL * Cg * 4;
+    STC_REQUIRE(workspace && workspace_bytes >= need, "wgrad bf16: workspace %lld < %lld", (long long)workspace_bytes,
+                (long long)need);
+    p.ws = (float*)workspace;
   }
-  const int64_t need = (int64_t)pl.nsplit * R * 16LL * Cg * 4;
-  STC_REQUIRE(workspace && workspace_bytes >= need, "wgrad bf16: workspace %lld < %lld", (long long)workspace_bytes,
-              (long long)need);
-  p.ws = (float*)workspace;
-  hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(256), lds, st, p);
+  switch (pl.cfg) {
+    case 0: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false>), grid, dim3(256), lds, st, p); break;
+    case 1: hipLaunchKernelGGL((wgrad_bf16_kernel<64, 128, 1, 4, false>), grid, dim3(256), lds, st, p); break;
+    default: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 16, 4, 1, true>), grid, dim3(256), lds, st, p); break;
+  }
   STC_CHECK_LAUNCH();
+  if (pl.nsplit <= 1) return 0;
   const long long total = (long long)R * 16 * Cg_out;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)p.ws, pl.nsplit, R, Cg, Cg_out,

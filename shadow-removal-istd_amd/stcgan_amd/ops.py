@@ -125,7 +125,7 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt):
         if dt == torch.bfloat16 and cin % 64 == 0:
             geom = 0 if kind == L.CONVT_S2 else 1
             nb = 2 if (kind == L.CONVT_S2 and 4 * cout > 16) else 1
-            return f"narrow_halo_kernel<{geom}, {nb}, 16>", ws == 0
+            return f"narrow_halo_kernel<{geom}, {nb}, 8>", ws == 0
         return "narrow_tiled_kernel", True
     if cfg >= 0:
         t = _BF16_TILES[cfg]

@@ -189,7 +189,10 @@ WGRAD = [  # kind, stride, B, Cin, Cout, H, W (input grid of the forward layer)
     ("conv", 2, 3, 32, 96, 10, 14),    # ragged R / columns
     ("convT", 2, 2, 128, 64, 16, 16),
     ("convT", 2, 2, 1024, 512, 2, 2),
-    ("convT", 2, 1, 64, 8, 9, 13),     # R = 64 rows of a 128-row tile, odd grid
+    ("convT", 2, 1, 64, 8, 9, 13),     # R = 64 (64-row tile), odd grid
+    ("conv", 1, 2, 512, 8, 17, 17),    # PatchGAN logits (N = 8 padded): R <= 16 -> swapped 128x16 tile
+    ("conv", 1, 1, 64, 8, 9, 11),      # R = 8, ragged
+    ("conv", 2, 2, 16, 64, 40, 24),    # R = 64 with Cg = 16
 ]
 
 
