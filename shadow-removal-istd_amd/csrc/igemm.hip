@@ -747,7 +747,7 @@ extern "C" int stc_conv_fwd_ex(int dtype, int kind, int B, stc_view x, int Cin, 
                                void* stream) {
   STC_REQUIRE(kind >= 0 && kind <= 3, "stc_conv_fwd_ex: bad kind %d", kind);
   hipStream_t st = (hipStream_t)stream;
-  if (bf16_path(dtype, kind, Cin, Cout) && bf16_conv_eligible(kind, B, x, Cin, Cout))
+  if (bf16_path(dtype, kind, Cin, Cout) && !epi_tanh && bf16_conv_eligible(kind, B, x, Cin, Cout))
     return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, epi_tanh, out_f32, stats_part, stats_chunks,
                          force_plan, workspace, workspace_bytes, st);
   const int rc = stc_conv_fwd(dtype, kind, B, x, Cin, nullptr, nullptr, 0, 0.f, w_packed, Cout, y, bias, epi_tanh,
@@ -814,7 +814,7 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
     STC_CHECK_LAUNCH();
     return 0;
   }
-  if (dtype == STC_BF16 && p.sc == nullptr && pro_act == 0 && bf16_conv_eligible(kind, B, x, Cin, Cout))
+  if (dtype == STC_BF16 && p.sc == nullptr && pro_act == 0 && !epi_tanh && bf16_conv_eligible(kind, B, x, Cin, Cout))
     return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, epi_tanh, out_f32, nullptr, 0, nullptr,
                          workspace, workspace_bytes, st0);
   const Plan pl = plan_for(dtype, p.M, Cout, K, g.nphase);

@@ -94,44 +94,65 @@ igemm_bf16_kernel(const GParams p) {
   // around the DMA instructions.
   const int prow = lane >> 3;
   const int schunk = (lane & 7) ^ prow;
-  int a_base[AG], a_y[AG], a_x[AG];
+  // Per DMA row: element offset of the tap-(0,0) source pixel, and a validity mask over the taps
+  // (bit ty: row in range for tap row ty; bit 4+tx: column in range for tap column tx) -- the
+  // K loop then needs one add and a bit test per row instead of re-deriving and bounds-checking
+  // the im2col address (this VALU work, not the MFMA, bounded the first version of the loop).
+  const int ntap1 = 1 << p.lg_tw;
+  unsigned a_off0[AG], a_vm[AG];
 #pragma unroll
   for (int g = 0; g < AG; ++g) {
     const int m = m0 + (wave * AG + g) * 8 + prow;
     const int mm = m < p.M ? m : 0;
     const int b = mm / GHW, rem = mm - b * GHW;
     const int y = rem / p.GW, x = rem - y * p.GW;
-    a_base[g] = b * p.a_bs + p.a_co;
-    a_y[g] = m < p.M ? y * p.in_stride + p.offy[ph] : -(1 << 20);
-    a_x[g] = x * p.in_stride + p.offx[ph];
+    const int ay = y * p.in_stride + p.offy[ph], ax = x * p.in_stride + p.offx[ph];
+    a_off0[g] = (unsigned)(b * p.a_bs + p.a_co) + (unsigned)ay * (unsigned)p.a_rs + (unsigned)ax * (unsigned)p.a_ps;
+    unsigned vm = 0;
+    for (int tt = 0; tt < ntap1; ++tt) {
+      if ((unsigned)(ay + p.stepy * tt) < (unsigned)p.IH) vm |= 1u << tt;
+      if ((unsigned)(ax + p.stepx * tt) < (unsigned)p.IW) vm |= 1u << (4 + tt);
+    }
+    a_vm[g] = m < p.M ? vm : 0u;
   }
-  int b_row[BG];
+  unsigned b_off[BG];
 #pragma unroll
   for (int g = 0; g < BG; ++g) {
     const int n = n0 + (wave * BG + g) * 8 + prow;
-    b_row[g] = n < p.N ? ph * p.b_phase_stride + n * p.K : (1 << 30);
+    b_off[g] = n < p.N ? (unsigned)(ph * p.b_phase_stride + n * p.K) : OOB;
   }
-  const int tw_mask = (1 << p.lg_tw) - 1;
+  const int tw_mask = ntap1 - 1;
+  // this lane's K position: k = kbeg + 64*s + 8*schunk = t*cin + ci, advanced incrementally
+  int kcur = kbeg + schunk * 8;
+  int tcur = kcur / p.cin, ccur = kcur - tcur * p.cin;
+  const bool cdiv64 = (64 % p.cin) == 0;
+  const int tadv = cdiv64 ? 64 / p.cin : 0;
 
-  auto issue = [&](int s, int stage) {
+  auto issue = [&](int stage) {
     char* sA = smem + stage * STAGE;
     char* sB = sA + BM * 128;
-    const int k = kbeg + s * 64 + schunk * 8;
-    const unsigned kpen = k < kend ? 0u : OOB;
-    const int t = k / p.cin, ci = k - t * p.cin;
-    const int dy = p.stepy * (t >> p.lg_tw), dx = p.stepx * (t & tw_mask);
+    const unsigned kpen = kcur < kend ? 0u : OOB;
+    const int ty = tcur >> p.lg_tw, tx = tcur & tw_mask;
+    const unsigned delta = (unsigned)(p.stepy * ty) * (unsigned)p.a_rs + (unsigned)(p.stepx * tx) * (unsigned)p.a_ps +
+                           (unsigned)ccur;
 #pragma unroll
     for (int g = 0; g < AG; ++g) {
-      const int iy = a_y[g] + dy, ix = a_x[g] + dx;
-      const unsigned pen = ((unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) ? kpen : OOB;
-      const unsigned off = (((unsigned)a_base[g] + (unsigned)iy * (unsigned)p.a_rs + (unsigned)ix * (unsigned)p.a_ps +
-                             (unsigned)ci) * 2u) | pen;
+      const unsigned ok = (a_vm[g] >> ty) & (a_vm[g] >> (4 + tx)) & 1u;
+      const unsigned off = ((a_off0[g] + delta) * 2u) | (ok ? kpen : OOB);
       dma16(ra, sA + (wave * AG + g) * 1024, off);
     }
 #pragma unroll
     for (int g = 0; g < BG; ++g) {
-      const unsigned off = (((unsigned)b_row[g] + (unsigned)k) * 2u) | kpen;
+      const unsigned off = ((b_off[g] + (unsigned)kcur) * 2u) | kpen | (b_off[g] & OOB);
       dma16(rb, sB + (wave * BG + g) * 1024, off);
+    }
+    // advance to the next K-step
+    kcur += 64;
+    if (cdiv64) {
+      tcur += tadv;
+    } else {
+      ccur += 64;
+      while (ccur >= p.cin) { ccur -= p.cin; ++tcur; }
     }
   };
 
@@ -166,11 +187,11 @@ igemm_bf16_kernel(const GParams p) {
 
   if constexpr (NST == 2) {
     // DMA of step s+1 lands under the MFMAs of step s; vmcnt(0) + barrier per step.
-    if (nsteps > 0) issue(0, 0);
+    if (nsteps > 0) issue(0);
     for (int s = 0; s < nsteps; ++s) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+      if (s + 1 < nsteps) issue((s + 1) & 1);
       compute(s & 1);
     }
   } else {
@@ -178,14 +199,14 @@ igemm_bf16_kernel(const GParams p) {
     // AG+BG youngest, step s+1's, stay in flight across the raw barrier), then refill the
     // stage that step s-1 read (every wave has passed the barrier, so those reads are done).
     constexpr int P = AG + BG;
-    if (nsteps > 0) issue(0, 0);
-    if (nsteps > 1) issue(1, 1);
+    if (nsteps > 0) issue(0);
+    if (nsteps > 1) issue(1);
     int cur = 0, nxt = 2;
     for (int s = 0; s < nsteps; ++s) {
       if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(P) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (s + 2 < nsteps) issue(s + 2, nxt);
+      if (s + 2 < nsteps) issue(nxt);
       compute(cur);
       cur = cur == 2 ? 0 : cur + 1;
       nxt = nxt == 2 ? 0 : nxt + 1;
@@ -212,22 +233,17 @@ igemm_bf16_kernel(const GParams p) {
     return;
   }
 
-  float bz[FN];
+  if (p.bias) {  // (tanh epilogues only occur on narrow-N layers: narrow_bf16.hip)
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * TN + 16 * j + cl;
-    bz[j] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * TN + 16 * j + cl;
+      const float bz = n < p.N ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += bz;
+    }
   }
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = acc[i][j][r] + bz[j];
-        if (p.tanh_) v = tanhf(v);
-        acc[i][j][r] = v;
-      }
 
   __syncthreads();  // every wave is done with the stage buffers
   float* red = reinterpret_cast<float*>(smem);  // [WM][BN] partials, then [BN] column means
@@ -677,6 +693,7 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
   p.vec_out = vec_out_ok(y, out_f32) && Cout % 8 == 0 ? 1 : 0;
   p.nphase = g.nphase;
   if (p.M == 0 || Cout == 0) return 0;
+  STC_REQUIRE(!epi_tanh, "bf16 conv: the MFMA tile kernel has no tanh epilogue");
   if (!p.vec_out) STC_REQUIRE(!stats || out_f32 == 0, "bf16 conv: stats need a bf16 output");
   return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st);
 }
