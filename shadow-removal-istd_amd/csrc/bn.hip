@@ -143,44 +143,51 @@ __global__ void __launch_bounds__(256) chan_stats_kernel(View x, PixDiv pd, long
   }
 }
 
+// Merge of the per-chunk statistics {n, S1 = sum(x - shift), S2 = sum((x - shift)^2), shift}:
+// chunk mean m_b = shift + S1/n, chunk M2_b = S2 - S1^2/n; then (exactly, in fp64)
+//   mean = sum n_b m_b / N,   M2 = sum [M2_b + n_b (m_b - mean)^2]
+// in two passes over the chunks (one block per channel, fixed-order tree -> deterministic).
+__device__ __forceinline__ double block_sum256(double v, double* sh) {
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+    __syncthreads();
+  }
+  const double r = sh[0];
+  __syncthreads();
+  return r;
+}
+
 __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int nchunks, int C,
                                                           const float* gamma, const float* beta,
                                                           float* rmean, float* rvar, long long* nbt,
                                                           float momentum, float eps,
                                                           float* mean_o, float* rstd_o, float* scale, float* shift) {
   const int c = blockIdx.x;
-  __shared__ double sn[256], sm[256], sq[256];
-  double n = 0, mean = 0, m2 = 0;
+  __shared__ double sh[256];
+  double n = 0, sm = 0;
   for (int k = threadIdx.x; k < nchunks; k += 256) {
-    const float* pp = part + ((long long)k * C + c) * 4;
-    const double nb = pp[0];
-    if (nb <= 0) continue;
-    const double s1 = pp[1], s2 = pp[2], shv = pp[3];
-    const double mb = shv + s1 / nb;
-    double qb = s2 - s1 * s1 / nb;
-    if (qb < 0) qb = 0;
-    const double nn = n + nb, d = mb - mean;
-    mean += d * nb / nn;
-    m2 += qb + d * d * n * nb / nn;
-    n = nn;
+    const float4 pp = *reinterpret_cast<const float4*>(part + ((long long)k * C + c) * 4);
+    if (pp.x <= 0.f) continue;
+    n += pp.x;
+    sm += (double)pp.x * pp.w + (double)pp.y;  // n_b * m_b = n_b*shift + S1
   }
-  sn[threadIdx.x] = n; sm[threadIdx.x] = mean; sq[threadIdx.x] = m2;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      const double na = sn[threadIdx.x], nb = sn[threadIdx.x + s];
-      if (nb > 0) {
-        const double nn = na + nb, d = sm[threadIdx.x + s] - sm[threadIdx.x];
-        sm[threadIdx.x] += d * nb / nn;
-        sq[threadIdx.x] += sq[threadIdx.x + s] + d * d * na * nb / nn;
-        sn[threadIdx.x] = nn;
-      }
-    }
-    __syncthreads();
+  const double N = block_sum256(n, sh);
+  const double mu = N > 0 ? block_sum256(sm, sh) / N : (block_sum256(sm, sh), 0.0);
+  double m2 = 0;
+  for (int k = threadIdx.x; k < nchunks; k += 256) {
+    const float4 pp = *reinterpret_cast<const float4*>(part + ((long long)k * C + c) * 4);
+    if (pp.x <= 0.f) continue;
+    const double nb = pp.x, s1 = pp.y, r = s1 / nb;
+    double q = (double)pp.z - s1 * r;
+    if (q < 0) q = 0;
+    const double d = (double)pp.w + r - mu;
+    m2 += q + nb * d * d;
   }
+  const double M2 = block_sum256(m2, sh);
   if (threadIdx.x == 0) {
-    const double N = sn[0], mu = sm[0];
-    const double var = N > 0 ? sq[0] / N : 0.0;
+    const double var = N > 0 ? M2 / N : 0.0;
     const float rs = (float)(1.0 / sqrt(var + (double)eps));
     const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
     if (mean_o) mean_o[c] = (float)mu;
@@ -189,7 +196,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int
     scale[c] = sc;
     shift[c] = bt - (float)mu * sc;
     if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
-    if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(N > 1 ? sq[0] / (N - 1) : var);
+    if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(N > 1 ? M2 / (N - 1) : var);
     if (nbt && c == 0) nbt[0] += 1;
   }
 }
@@ -292,22 +299,23 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(View x, PixDiv pd, l
   }
 }
 
-// dbeta[c] = sum dn, dgamma[c] = sum dn*xhat  (fixed order over chunks)
-__global__ void bn_bwd_finalize_kernel(const float* part, int nchunks, int C, float* dgamma, float* dbeta) {
+// dbeta[c] = sum dn, dgamma[c] = sum dn*xhat  (fixed order over chunks, one block per channel)
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* part, int nchunks, int C, float* dgamma,
+                                                              float* dbeta) {
   const int c = blockIdx.x;
-  __shared__ double s0[256], s1[256];
+  __shared__ double sh[256];
   double a = 0, b = 0;
   for (int k = threadIdx.x; k < nchunks; k += 256) {
-    a += part[((long long)k * C + c) * 2];
-    b += part[((long long)k * C + c) * 2 + 1];
+    const float2 pp = *reinterpret_cast<const float2*>(part + ((long long)k * C + c) * 2);
+    a += pp.x;
+    b += pp.y;
   }
-  s0[threadIdx.x] = a; s1[threadIdx.x] = b;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) { s0[threadIdx.x] += s0[threadIdx.x + s]; s1[threadIdx.x] += s1[threadIdx.x + s]; }
-    __syncthreads();
+  const double ta = block_sum256(a, sh);
+  const double tb = block_sum256(b, sh);
+  if (threadIdx.x == 0) {
+    dbeta[c] = (float)ta;
+    dgamma[c] = (float)tb;
   }
-  if (threadIdx.x == 0) { dbeta[c] = (float)s0[0]; dgamma[c] = (float)s1[0]; }
 }
 
 template <typename T>
