@@ -187,8 +187,24 @@ def main():
         fwd_ms = ev0.elapsed_time(ev1) / reps
     set_tf = flops / (fwd_ms * 1e-3) / 1e12
     top = sorted(per.items(), key=lambda kv: -kv[1][2])[:8]
+    # HBM traffic per launch of the dominant kernel: rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE;
+    # gfx950 FETCH_SIZE x2 correction) over the same bench command, committed under profiles/
+    # (scripts/profile_round.sh -> profiles/<round>/pmc_traffic.json); mean over all its launches.
+    traffic, traffic_src = None, None
+    import glob
+    for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        try:
+            tab = json.load(open(fpath))
+        except (OSError, ValueError):
+            continue
+        hit = [v for k, v in tab.items() if dom in k]
+        if hit and args.dtype == "bf16":
+            traffic = int(hit[0]["hbm_bytes_per_launch"])
+            traffic_src = os.path.relpath(fpath, ROOT) + f" (mean over {hit[0]['launches']} launches, all shapes)"
+            break
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_src": traffic_src,
                 "kernel": f"{dom}: {n_dom} single-kernel launches in one train step, {fl_dom / 1e9:.2f} GFLOP, "
                           f"{ms_dom:.3f} ms, avg {ms_dom / n_dom * 1e3:.1f} us/launch (HIP events)",
                 "per_kernel": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 2), "ms": round(v[2], 3),
