@@ -98,6 +98,31 @@ int stc_conv_fwd_ex(int dtype, int kind, int B, stc_view x, int Cin, const void*
                     float* stats_part, int stats_chunks, const int32_t* force_plan,
                     void* workspace, int64_t workspace_bytes, void* stream);
 
+/* Input-gradient conv with the BatchNorm-backward reduction of its consumer fused in.
+ * The conv output v is the gradient reaching the output of a BatchNorm (through an activation)
+ * at BN channel ch = n - ch_off; with the BN input x (raw conv output of the forward), the same
+ * pixel's optional second gradient g_other and the BN tables:
+ *   nn = x*scale + shift,  dn = v*act'(nn, slope_self) + g_other*act'(nn, slope_other),
+ *   part2[chunk][ch] = {sum dn, sum dn*(x - mean)*rstd}     (stc_bn_bwd_reduce format)
+ * over the pixels inside x's extent; stc_bn_bwd_apply then finishes the BN backward
+ * (STCGAN/networks.py:107-109,170-171,179-180 backward).  bf16 NHWC outputs compute the sums in
+ * the GEMM epilogue / split-K reduction; other cases run the conv and stc_bn_bwd_reduce.
+ * stc_conv_bwd_bn_chunks: the part2 chunk count for the same arguments.                    */
+typedef struct {
+  stc_view x;        /* BN input (raw pre-BN values), C channels, extent = the BN domain  */
+  stc_view g_other;  /* optional second gradient into the BN output (p == NULL: none)     */
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* rstd;
+  float slope_self, slope_other;
+  int32_t C, ch_off;
+} stc_bnb_fuse;
+int stc_conv_bwd_bn_chunks(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int xH, int xW);
+int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout, stc_view out,
+                    const stc_bnb_fuse* bnb, float* part2, int nchunks,
+                    void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---- weight gradient ---------------------------------------------------------
  * dW[r][ci][kh][kw] = sum_{b,oy,ox} D[b,oy,ox,r] * G[b, oy*s+kh-1, ox*s+kw-1, ci]
  *   Conv2d s2/s1 : D = dy (grid = output), G = x (input), s = stride

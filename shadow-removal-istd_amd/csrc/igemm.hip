@@ -667,7 +667,8 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
                     int64_t* ws_bytes, int32_t* stats_chunks, int32_t* plan_out);
 int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
-                  const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st);
+                  const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
+                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr);
 bool bf16_narrow_eligible(int kind, int Cin, int Cout);
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout);
 int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
@@ -828,4 +829,53 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
   hipStream_t st = (hipStream_t)stream;
   if (dtype == STC_F32) return launch_igemm<float>(pl, p, st);
   return launch_igemm<bf16>(pl, p, st);
+}
+
+// ---- input-gradient conv + fused BN-backward reduction
+static bool bnb_fused_path(int dtype, int kind, int B, const stc_view& dy, int Cin, int Cout, const stc_view& out) {
+  const bool vec = out.cs == 1 && out.co % 8 == 0 && out.ps % 8 == 0 && out.rs % 8 == 0 && out.bs % 8 == 0 &&
+                   ((uintptr_t)out.p & 15) == 0;
+  return bf16_path(dtype, kind, Cin, Cout) && vec && bf16_conv_eligible(kind, B, dy, Cin, Cout);
+}
+
+extern "C" int stc_conv_bwd_bn_chunks(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int xH, int xW) {
+  if (bf16_path(dtype, kind, Cin, Cout)) {
+    int32_t nch = 0;
+    bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &nch, nullptr);
+    return nch;  // (NHWC 16-byte aligned views assumed: the fused path)
+  }
+  return stc_chan_stats_chunks(B, xH, xW);
+}
+
+extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout,
+                               stc_view out, const stc_bnb_fuse* bnb, float* part2, int nchunks, void* workspace,
+                               int64_t workspace_bytes, void* stream) {
+  STC_REQUIRE(bnb && part2, "stc_conv_bwd_bn: bnb and part2 required");
+  hipStream_t st = (hipStream_t)stream;
+  if (bnb_fused_path(dtype, kind, B, dy, Cin, Cout, out)) {
+    const Geometry g = geometry(kind);
+    const int Hg = kind == STC_CONVT_S2 ? dy.H : out.H, Wg = kind == STC_CONVT_S2 ? dy.W : out.W;
+    int32_t need = 0;
+    bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &need, nullptr);
+    (void)g;
+    STC_REQUIRE(nchunks >= need, "stc_conv_bwd_bn: %d chunks < %d", nchunks, need);
+    // unused chunk rows (if the caller sized for the fallback) must read as zeros in the finalize
+    if (nchunks > need) {
+      (void)hipMemsetAsync(part2 + (size_t)need * bnb->C * 2, 0, (size_t)(nchunks - need) * bnb->C * 2 * 4, st);
+    }
+    return bf16_conv_fwd(kind, B, dy, Cin, w_packed, Cout, out, nullptr, 0, 0, nullptr, need, nullptr, workspace,
+                         workspace_bytes, st, bnb, part2);
+  }
+  int rc = stc_conv_fwd(dtype, kind, B, dy, Cin, nullptr, nullptr, 0, 0.f, w_packed, Cout, out, nullptr, 0, 0,
+                        workspace, workspace_bytes, stream);
+  if (rc) return rc;
+  stc_view g1 = out;  // this conv's output, at the BN channels, over the BN extent
+  g1.co += bnb->ch_off;
+  g1.H = bnb->x.H;
+  g1.W = bnb->x.W;
+  const int need = stc_chan_stats_chunks(B, bnb->x.H, bnb->x.W);
+  STC_REQUIRE(nchunks >= need, "stc_conv_bwd_bn: %d chunks < %d", nchunks, need);
+  if (nchunks > need) (void)hipMemsetAsync(part2 + (size_t)need * bnb->C * 2, 0, (size_t)(nchunks - need) * bnb->C * 2 * 4, st);
+  return stc_bn_bwd_reduce(dtype, B, bnb->x, bnb->C, bnb->scale, bnb->shift, bnb->mean, bnb->rstd, g1, bnb->slope_self,
+                           bnb->g_other, bnb->slope_other, part2, need, stream);
 }

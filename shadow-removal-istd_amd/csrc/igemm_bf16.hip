@@ -42,7 +42,52 @@ struct GParams {
   float* ws;
   float* stats;
   int nphase, mtiles, ntiles;
+  // Fused BatchNorm-backward reduction (optional, NHWC bf16 output only): with this conv's output
+  // v (the gradient reaching a BN's output through an activation) and the BN input x at the same
+  // pixel, BN channel ch = n - bch_off:  nn = x*scale + shift,
+  //   dn = v * act'(nn, bs_self) + g_other * act'(nn, bs_other),  xhat = (x - mean) * rstd,
+  // part2[tile][ch] += {dn, dn * xhat} over the pixels inside the BN input extent.
+  float* part2;
+  const char* bx;
+  long long bx_bs, bx_rs;
+  int bx_ps, bx_co, bxH, bxW;
+  const char* bg;
+  long long bg_bs, bg_rs;
+  int bg_ps, bg_co;
+  const float *bsc, *bsh, *bmu, *brs;
+  float bs_self, bs_other;
+  int bC, bch_off;
 };
+
+// {dn, dn*xhat} of 8 consecutive BN channels at one pixel (v: this conv's 8 output values)
+__device__ __forceinline__ void bnb_accum(const GParams& p, int b, int oy, int ox, int ch, const float* v, float* sa,
+                                          float* sb) {
+  const bf16* xp = reinterpret_cast<const bf16*>(p.bx) + (long long)b * p.bx_bs + (long long)oy * p.bx_rs +
+                   (long long)ox * p.bx_ps + p.bx_co + ch;
+  const uint4 xr = *reinterpret_cast<const uint4*>(xp);
+  float xv[8], gv[8];
+  {
+    const unsigned w[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { xv[2 * q] = __uint_as_float(w[q] << 16); xv[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+  }
+  if (p.bg) {
+    const bf16* gp = reinterpret_cast<const bf16*>(p.bg) + (long long)b * p.bg_bs + (long long)oy * p.bg_rs +
+                     (long long)ox * p.bg_ps + p.bg_co + ch;
+    const uint4 gr = *reinterpret_cast<const uint4*>(gp);
+    const unsigned w[4] = {gr.x, gr.y, gr.z, gr.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { gv[2 * q] = __uint_as_float(w[q] << 16); gv[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float nn = fmaf(xv[e], p.bsc[ch + e], p.bsh[ch + e]);
+    float dn = v[e] * (nn > 0.f ? 1.f : p.bs_self);
+    if (p.bg) dn += gv[e] * (nn > 0.f ? 1.f : p.bs_other);
+    sa[e] += dn;
+    sb[e] += dn * (xv[e] - p.bmu[ch + e]) * p.brs[ch + e];
+  }
+}
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 using lds_vptr = __attribute__((address_space(3))) void*;
@@ -53,17 +98,31 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, u
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)lds_dst, 16, voff, 0, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN, int NST>
+// LDS swizzle of a K-row image: BK = 64 -> 128-B rows, chunk ^ (row & 7); BK = 32 -> 64-B rows,
+// chunk ^ ((row >> 1) & 3).  Both make every ds_read_b128 lane group of the 16x16x32 operand
+// read conflict-free for any 16-row-aligned fragment.
+template <int BK>
+__device__ __forceinline__ int kswz(int row) {
+  if constexpr (BK == 64) return row & 7;
+  else return (row >> 1) & 3;
+}
+
+template <int BM, int BN, int WM, int WN, int NST, int BK>
 __global__ void __launch_bounds__(64 * WM * WN)
 igemm_bf16_kernel(const GParams p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int AG = BM / (8 * NW), BG = BN / (8 * NW);  // 1 KiB DMA pieces per wave per K-step
-  constexpr int STAGE = (BM + BN) * 128;
-  static_assert(AG * 8 * NW == BM && BG * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
+  constexpr int RB = BK * 2;             // bytes per LDS row (one GEMM row's K-step)
+  constexpr int CH = BK / 8;             // 16-byte chunks per row
+  constexpr int RPP = 1024 / RB;         // rows per 1 KiB DMA piece
+  constexpr int AG = BM / (RPP * NW), BG = BN / (RPP * NW);  // pieces per wave per K-step
+  constexpr int STAGE = (BM + BN) * RB;
+  constexpr int KK = BK / 32;            // 16x16x32 MFMA sub-steps per K-step
+  static_assert(AG * RPP * NW == BM && BG * RPP * NW == BN, "tile rows must split into whole pieces per wave");
   static_assert(FM >= 1 && FN >= 1, "wave tile >= 16x16");
-  static_assert(NST == 2 || NST == 3, "2- or 3-stage ring");
+  static_assert(NST >= 2 && NST <= 4, "2..4-stage ring");
+  static_assert(BK == 64 || BK == 32, "BK");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -82,7 +141,7 @@ igemm_bf16_kernel(const GParams p) {
   const int ph = z / p.ksplit, split = z % p.ksplit;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
-  const int nsteps = (kend - kbeg + 63) / 64;
+  const int nsteps = (kend - kbeg + BK - 1) / BK;
   const int GHW = p.GH * p.GW;
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, (short)0, (int)p.a_bytes, 0x00020000);
@@ -92,8 +151,8 @@ igemm_bf16_kernel(const GParams p) {
   // Every offset is computed unconditionally and pushed out of range by OR-ing bit 31 where the
   // element is padding (any offset >= 2^31 > num_records reads zeros): no divergent branches
   // around the DMA instructions.
-  const int prow = lane >> 3;
-  const int schunk = (lane & 7) ^ prow;
+  const int prow = lane / CH;                   // row within the piece
+  const int schunk = (lane % CH) ^ kswz<BK>(prow);  // source chunk of this lane's LDS slot
   // Per DMA row: element offset of the tap-(0,0) source pixel, and a validity mask over the taps
   // (bit ty: row in range for tap row ty; bit 4+tx: column in range for tap column tx) -- the
   // K loop then needs one add and a bit test per row instead of re-deriving and bounds-checking
@@ -102,7 +161,7 @@ igemm_bf16_kernel(const GParams p) {
   unsigned a_off0[AG], a_vm[AG];
 #pragma unroll
   for (int g = 0; g < AG; ++g) {
-    const int m = m0 + (wave * AG + g) * 8 + prow;
+    const int m = m0 + (wave * AG + g) * RPP + prow;
     const int mm = m < p.M ? m : 0;
     const int b = mm / GHW, rem = mm - b * GHW;
     const int y = rem / p.GW, x = rem - y * p.GW;
@@ -118,19 +177,19 @@ igemm_bf16_kernel(const GParams p) {
   unsigned b_off[BG];
 #pragma unroll
   for (int g = 0; g < BG; ++g) {
-    const int n = n0 + (wave * BG + g) * 8 + prow;
+    const int n = n0 + (wave * BG + g) * RPP + prow;
     b_off[g] = n < p.N ? (unsigned)(ph * p.b_phase_stride + n * p.K) : OOB;
   }
   const int tw_mask = ntap1 - 1;
-  // this lane's K position: k = kbeg + 64*s + 8*schunk = t*cin + ci, advanced incrementally
+  // this lane's K position: k = kbeg + BK*s + 8*schunk = t*cin + ci, advanced incrementally
   int kcur = kbeg + schunk * 8;
   int tcur = kcur / p.cin, ccur = kcur - tcur * p.cin;
-  const bool cdiv64 = (64 % p.cin) == 0;
-  const int tadv = cdiv64 ? 64 / p.cin : 0;
+  const bool cdivk = (BK % p.cin) == 0;
+  const int tadv = cdivk ? BK / p.cin : 0;
 
   auto issue = [&](int stage) {
     char* sA = smem + stage * STAGE;
-    char* sB = sA + BM * 128;
+    char* sB = sA + BM * RB;
     const unsigned kpen = kcur < kend ? 0u : OOB;
     const int ty = tcur >> p.lg_tw, tx = tcur & tw_mask;
     const unsigned delta = (unsigned)(p.stepy * ty) * (unsigned)p.a_rs + (unsigned)(p.stepx * tx) * (unsigned)p.a_ps +
@@ -147,11 +206,11 @@ igemm_bf16_kernel(const GParams p) {
       dma16(rb, sB + (wave * BG + g) * 1024, off);
     }
     // advance to the next K-step
-    kcur += 64;
-    if (cdiv64) {
+    kcur += BK;
+    if (cdivk) {
       tcur += tadv;
     } else {
-      ccur += 64;
+      ccur += BK;
       while (ccur >= p.cin) { ccur -= p.cin; ++tcur; }
     }
   };
@@ -162,22 +221,22 @@ igemm_bf16_kernel(const GParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment read offsets: row (l & 15), chunk 4*kk + (l >> 4), slot = chunk ^ (row & 7)
+  // fragment read offsets: row (l & 15), chunk 4*kk + (l >> 4), slot = chunk ^ swizzle(row)
   const int frow = lane & 15;
-  int rd_off[2];
+  int rd_off[KK];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) rd_off[kk] = frow * 128 + (((4 * kk + (lane >> 4)) ^ (frow & 7)) * 16);
+  for (int kk = 0; kk < KK; ++kk) rd_off[kk] = frow * RB + (((4 * kk + (lane >> 4)) ^ kswz<BK>(frow)) * 16);
 
   auto compute = [&](int stage) {
-    const char* sA = smem + stage * STAGE + (wm * TM) * 128;
-    const char* sB = smem + stage * STAGE + BM * 128 + (wn * TN) * 128;
+    const char* sA = smem + stage * STAGE + (wm * TM) * RB;
+    const char* sB = smem + stage * STAGE + BM * RB + (wn * TN) * RB;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
       bf16x8_t fa[FM], fb[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + i * 16 * 128 + rd_off[kk]);
+      for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + i * 16 * RB + rd_off[kk]);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sB + j * 16 * 128 + rd_off[kk]);
+      for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sB + j * 16 * RB + rd_off[kk]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -195,21 +254,23 @@ igemm_bf16_kernel(const GParams p) {
       compute(s & 1);
     }
   } else {
-    // 3-stage ring: two K-steps in flight; at step s wait only for step s's pieces (the
-    // AG+BG youngest, step s+1's, stay in flight across the raw barrier), then refill the
+    // NST-stage ring: NST-1 K-steps in flight.  At step s wait only for step s's pieces (the
+    // P*(steps issued after s) youngest stay in flight across the raw barrier), then refill the
     // stage that step s-1 read (every wave has passed the barrier, so those reads are done).
     constexpr int P = AG + BG;
-    if (nsteps > 0) issue(0);
-    if (nsteps > 1) issue(1);
-    int cur = 0, nxt = 2;
+#pragma unroll
+    for (int i = 0; i < NST - 1; ++i)
+      if (i < nsteps) issue(i);
+    int cur = 0;
     for (int s = 0; s < nsteps; ++s) {
-      if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(P) : "memory");
+      const int ahead = min(NST - 2, nsteps - 1 - s);  // steps already issued beyond s
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * P) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(P) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (s + 2 < nsteps) issue(nxt);
+      if (s + NST - 1 < nsteps) issue(cur == 0 ? NST - 1 : cur - 1);
       compute(cur);
-      cur = cur == 2 ? 0 : cur + 1;
-      nxt = nxt == 2 ? 0 : nxt + 1;
+      cur = cur == NST - 1 ? 0 : cur + 1;
     }
   }
 
@@ -326,16 +387,52 @@ igemm_bf16_kernel(const GParams p) {
           *reinterpret_cast<unsigned short*>(tl + row * PITCH + col * 2) = f2bf(acc[i][j][r]);
         }
     __syncthreads();
-    constexpr int CPR = BN / 8;  // 16-byte chunks per row
+    constexpr int CPR = BN / 8;  // 16-byte chunks per row (64*NW is a multiple of CPR: fixed cc per thread)
+    float sa[8], sb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sa[e] = 0.f; sb[e] = 0.f; }
+    const int cc = tid % CPR;
+    const int nch = n0 + cc * 8 - p.bch_off;  // BN channel of this thread's chunk
+    const bool bnb_on = p.part2 != nullptr && nch >= 0 && nch < p.bC;
     for (int q = tid; q < BM * CPR; q += 64 * NW) {
-      const int row = q / CPR, cc = q - row * CPR;
+      const int row = q / CPR;
       const int m = m0 + row, n = n0 + cc * 8;
       if (m >= p.M || n >= p.N) continue;
       const int b = m / GHW, rem = m - b * GHW;
       const int y = rem / p.GW, x = rem - y * p.GW;
       const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
       const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
+      const uint4 t = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = t;
+      if (bnb_on && oy < p.bxH && ox < p.bxW) {
+        float v[8];
+        const unsigned w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[2 * e] = __uint_as_float(w[e] << 16); v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u); }
+        bnb_accum(p, b, oy, ox, nch, v, sa, sb);
+      }
+    }
+    if (p.part2 == nullptr) return;
+    // per-tile reduction over the threads sharing a channel chunk (fixed order)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [threads][16]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sa[e]; red[tid * 16 + 8 + e] = sb[e]; }
+    __syncthreads();
+    if (tid < CPR) {
+      const int ch0 = n0 + tid * 8 - p.bch_off;
+      if (ch0 >= 0 && ch0 < p.bC) {
+        float ta[8], tb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { ta[e] = 0.f; tb[e] = 0.f; }
+        for (int t = tid; t < 64 * NW; t += CPR)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { ta[e] += red[t * 16 + e]; tb[e] += red[t * 16 + 8 + e]; }
+        const long long tile = (long long)ph * p.mtiles + mt;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          *reinterpret_cast<float2*>(p.part2 + (tile * p.bC + ch0 + e) * 2) = make_float2(ta[e], tb[e]);
+      }
     }
     return;
   }
@@ -400,6 +497,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
   if (rl < RL && r0 < r1 && p.stats) {
     rowval(r0, sh);
   }
+  float ba[8], bb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { ba[e] = 0.f; bb[e] = 0.f; }
+  const int bnch = n - p.bch_off;
+  const bool bnb_on = p.part2 != nullptr && bnch >= 0 && bnch < p.bC;
   if (rl < RL) {
     for (long long row = r0 + rl; row < r1; row += RL) {
       float v[8];
@@ -415,6 +517,13 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
       o.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
       o.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = o;
+      if (bnb_on && oy < p.bxH && ox < p.bxW) {
+        float vr[8];  // the bf16-rounded values, as a separate reduction pass would read them
+        const unsigned w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { vr[2 * e] = __uint_as_float(w[e] << 16); vr[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u); }
+        bnb_accum(p, b, oy, ox, bnch, vr, ba, bb);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float d = v[e] - sh[e];
@@ -422,6 +531,25 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
         s2[e] += d * d;
       }
       cnt += 1.f;
+    }
+  }
+  if (p.part2) {
+    __shared__ float bred[256][16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { bred[threadIdx.x][e] = ba[e]; bred[threadIdx.x][8 + e] = bb[e]; }
+    __syncthreads();
+    if (rl == 0 && bnb_on) {
+      float ta[8], tb[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { ta[e] = 0.f; tb[e] = 0.f; }
+      for (int k = 0; k < RL; ++k) {
+        const int t = k * CG + cg;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { ta[e] += bred[t][e]; tb[e] += bred[t][8 + e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        *reinterpret_cast<float2*>(p.part2 + ((long long)blockIdx.x * p.bC + bnch + e) * 2) = make_float2(ta[e], tb[e]);
     }
   }
   if (!p.stats) return;
@@ -454,29 +582,35 @@ struct BPlan {
 };
 
 struct TileCfg {
-  int BM, BN, WM, WN, NST;
+  int BM, BN, WM, WN, NST, BK;
 };
 static const TileCfg kTiles[] = {
-    {128, 128, 2, 2, 2},  // 0
-    {256, 128, 2, 2, 2},  // 1
-    {128, 64, 2, 2, 2},   // 2
-    {256, 64, 4, 1, 2},   // 3
-    {64, 128, 1, 4, 2},   // 4
-    {64, 64, 2, 2, 2},    // 5
-    {256, 256, 2, 4, 2},  // 6
-    {128, 256, 2, 4, 2},  // 7
-    {128, 128, 2, 2, 3},  // 8
-    {128, 256, 2, 4, 3},  // 9
-    {64, 128, 1, 4, 3},   // 10
-    {128, 64, 2, 2, 3},   // 11
-    {64, 64, 2, 2, 3},    // 12
-    {256, 128, 4, 2, 3},  // 13
+    {128, 128, 2, 2, 2, 64},  // 0
+    {256, 128, 2, 2, 2, 64},  // 1
+    {128, 64, 2, 2, 2, 64},   // 2
+    {256, 64, 4, 1, 2, 64},   // 3
+    {64, 128, 1, 4, 2, 64},   // 4
+    {64, 64, 2, 2, 2, 64},    // 5
+    {256, 256, 2, 4, 2, 64},  // 6
+    {128, 256, 2, 4, 2, 64},  // 7
+    {128, 128, 2, 2, 3, 64},  // 8
+    {128, 256, 2, 4, 3, 64},  // 9
+    {64, 128, 1, 4, 3, 64},   // 10
+    {128, 64, 2, 2, 3, 64},   // 11
+    {64, 64, 2, 2, 3, 64},    // 12
+    {256, 128, 4, 2, 3, 64},  // 13
+    {256, 256, 2, 4, 4, 32},  // 14
+    {256, 128, 4, 2, 4, 32},  // 15
+    {128, 256, 2, 4, 4, 32},  // 16
+    {128, 128, 2, 2, 4, 32},  // 17
+    {128, 64, 2, 2, 4, 32},   // 18
+    {64, 64, 2, 2, 4, 32},    // 19
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
 static size_t bf16_lds_bytes(int cfg) {
   const TileCfg& t = kTiles[cfg];
-  size_t stage = (size_t)t.NST * (t.BM + t.BN) * 128;
+  size_t stage = (size_t)t.NST * (t.BM + t.BN) * t.BK * 2;
   size_t epi = (size_t)t.BM * (t.BN * 2 + 16);
   size_t red = (size_t)(t.WM + 1) * t.BN * 4;
   return std::max(stage, std::max(epi, red));
@@ -593,35 +727,44 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
   p.ksplit = pl.ksplit; p.kchunk = pl.kchunk; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles;
   p.stats = nullptr;
   p.ws = nullptr;
+  float* part2 = p.part2;
   if (pl.ksplit > 1) {
     STC_REQUIRE(ws && ws_bytes >= pr.ws_bytes, "bf16 igemm: workspace %lld < %lld bytes", (long long)ws_bytes,
                 (long long)pr.ws_bytes);
     p.ws = (float*)ws;
+    p.part2 = nullptr;  // computed by the split-K reduction
   } else {
     p.stats = stats;
   }
-  if (stats) STC_REQUIRE(stats_chunks >= pr.stats_chunks, "bf16 igemm: stats chunks %d < %d", stats_chunks, pr.stats_chunks);
+  if (stats || part2)
+    STC_REQUIRE(stats_chunks >= pr.stats_chunks, "bf16 igemm: stats chunks %d < %d", stats_chunks, pr.stats_chunks);
   dim3 grid(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
   const size_t lds = bf16_lds_bytes(pl.cfg);
-#define STC_B(I, BM_, BN_, WM_, WN_, NST_)                                                                  \
+#define STC_B(I, BM_, BN_, WM_, WN_, NST_, BK_)                                                             \
   case I:                                                                                                   \
-    hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
+    hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
     break;
   switch (pl.cfg) {
-    STC_B(0, 128, 128, 2, 2, 2)
-    STC_B(1, 256, 128, 2, 2, 2)
-    STC_B(2, 128, 64, 2, 2, 2)
-    STC_B(3, 256, 64, 4, 1, 2)
-    STC_B(4, 64, 128, 1, 4, 2)
-    STC_B(5, 64, 64, 2, 2, 2)
-    STC_B(6, 256, 256, 2, 4, 2)
-    STC_B(7, 128, 256, 2, 4, 2)
-    STC_B(8, 128, 128, 2, 2, 3)
-    STC_B(9, 128, 256, 2, 4, 3)
-    STC_B(10, 64, 128, 1, 4, 3)
-    STC_B(11, 128, 64, 2, 2, 3)
-    STC_B(12, 64, 64, 2, 2, 3)
-    STC_B(13, 256, 128, 4, 2, 3)
+    STC_B(0, 128, 128, 2, 2, 2, 64)
+    STC_B(1, 256, 128, 2, 2, 2, 64)
+    STC_B(2, 128, 64, 2, 2, 2, 64)
+    STC_B(3, 256, 64, 4, 1, 2, 64)
+    STC_B(4, 64, 128, 1, 4, 2, 64)
+    STC_B(5, 64, 64, 2, 2, 2, 64)
+    STC_B(6, 256, 256, 2, 4, 2, 64)
+    STC_B(7, 128, 256, 2, 4, 2, 64)
+    STC_B(8, 128, 128, 2, 2, 3, 64)
+    STC_B(9, 128, 256, 2, 4, 3, 64)
+    STC_B(10, 64, 128, 1, 4, 3, 64)
+    STC_B(11, 128, 64, 2, 2, 3, 64)
+    STC_B(12, 64, 64, 2, 2, 3, 64)
+    STC_B(13, 256, 128, 4, 2, 3, 64)
+    STC_B(14, 256, 256, 2, 4, 4, 32)
+    STC_B(15, 256, 128, 4, 2, 4, 32)
+    STC_B(16, 128, 256, 2, 4, 4, 32)
+    STC_B(17, 128, 128, 2, 2, 4, 32)
+    STC_B(18, 128, 64, 2, 2, 4, 32)
+    STC_B(19, 64, 64, 2, 2, 4, 32)
     default:
       return fail(-1, "bf16 igemm: bad tile config %d", pl.cfg);
   }
@@ -630,6 +773,7 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
   if (pl.ksplit > 1) {
     STC_REQUIRE(p.vec_out, "bf16 igemm: split-K needs a 16-byte aligned NHWC bf16 output");
     p.stats = stats;
+    p.part2 = part2;
     const long long rows = (long long)p.nphase * p.M;
     const int blocks = (int)((rows + pr.reduce_rows - 1) / pr.reduce_rows);
     hipLaunchKernelGGL(splitk_reduce_stats_kernel, dim3(blocks), dim3(256), 0, st, p, pr.reduce_rows);
@@ -669,7 +813,8 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
 
 int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
-                  const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st) {
+                  const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
+                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr) {
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   GParams p{};
@@ -695,6 +840,21 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
   if (p.M == 0 || Cout == 0) return 0;
   STC_REQUIRE(!epi_tanh, "bf16 conv: the MFMA tile kernel has no tanh epilogue");
   if (!p.vec_out) STC_REQUIRE(!stats || out_f32 == 0, "bf16 conv: stats need a bf16 output");
+  if (bnb) {
+    STC_REQUIRE(p.vec_out && part2 && !stats, "bf16 conv: fused BN backward needs a 16-byte NHWC bf16 output");
+    STC_REQUIRE(bnb->C % 8 == 0 && bnb->ch_off % 8 == 0 && bnb->x.cs == 1 && bnb->x.co % 8 == 0 && bnb->x.ps % 8 == 0 &&
+                    (!bnb->g_other.p || (bnb->g_other.cs == 1 && bnb->g_other.co % 8 == 0 && bnb->g_other.ps % 8 == 0)) &&
+                    bnb->scale && bnb->shift && bnb->mean && bnb->rstd,
+                "bf16 conv: bad fused BN-backward arguments");
+    p.part2 = part2;
+    p.bx = (const char*)bnb->x.p; p.bx_bs = bnb->x.bs; p.bx_rs = bnb->x.rs; p.bx_ps = bnb->x.ps; p.bx_co = bnb->x.co;
+    p.bxH = bnb->x.H; p.bxW = bnb->x.W;
+    p.bg = (const char*)bnb->g_other.p; p.bg_bs = bnb->g_other.bs; p.bg_rs = bnb->g_other.rs; p.bg_ps = bnb->g_other.ps;
+    p.bg_co = bnb->g_other.co;
+    p.bsc = bnb->scale; p.bsh = bnb->shift; p.bmu = bnb->mean; p.brs = bnb->rstd;
+    p.bs_self = bnb->slope_self; p.bs_other = bnb->slope_other;
+    p.bC = bnb->C; p.bch_off = bnb->ch_off;
+  }
   return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st);
 }
 

@@ -30,6 +30,13 @@ NULL_VIEW = View(None, 0, 0, 0, 0, 0, 0, 1, 0)
 PACK_MAX = 40
 
 
+class BnbFuse(ctypes.Structure):
+    """stc_bnb_fuse: the BatchNorm-backward reduction fused into an input-gradient conv."""
+    _fields_ = [("x", View), ("g_other", View), ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p),
+                ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p), ("slope_self", ctypes.c_float),
+                ("slope_other", ctypes.c_float), ("C", ctypes.c_int32), ("ch_off", ctypes.c_int32)]
+
+
 class PackDesc(ctypes.Structure):
     """stc_pack_desc: one stc_pack_weight job of a multi-tensor stc_pack_weights launch."""
     _fields_ = [("mode", ctypes.c_int32), ("P", ctypes.c_int32), ("Q", ctypes.c_int32), ("N_pad", ctypes.c_int32),
@@ -44,6 +51,8 @@ _SIGS = {
     "stc_conv_fwd_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32, _i32]),
     "stc_conv_fwd_plan": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "stc_conv_fwd_query": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "stc_conv_bwd_bn_chunks": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32]),
+    "stc_conv_bwd_bn": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _i32, _vp, _i64, _vp]),
     "stc_conv_fwd_ex": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _i32, _i32, _vp, _i32, _vp, _vp,
                                _i64, _vp]),
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,

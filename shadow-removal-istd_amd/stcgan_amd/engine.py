@@ -192,18 +192,20 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
             gcat[k] = _nhwc(B, ah, aw, cin_t, dt, dev, zero=(ah, aw) != S[k + 1])
         else:
             gcat[k] = _nhwc(B, *S[Lv], cin_t, dt, dev)
-        ops.conv(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt)
         if k == Lv - 1:
+            ops.conv(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt)
             break
-        # BN_up[k+1] over q_{k+1}: full (padded) extent; the cropped rows carry zero gradient
+        # BN_up[k+1] over q_{k+1}: full (padded) extent; the cropped rows carry zero gradient.
+        # Its gradient is the second half of gcat[k] (ReLU of the concat), so the BN reduction
+        # is fused into the conv that writes gcat[k] (channels C..2C -> BN channels 0..C).
         ah, aw = _pad2(S, k + 1)
         C = co[k]
         mean, rstd = st_u[k + 1]
         t = tab_u[k + 1]
         dq = _nhwc(B, ah, aw, C, dt, dev)
-        dg, db = ops.bn_backward(B, L.nhwc_view(rq[k + 1]), C, dt, L.nhwc_view(dq),
-                                 g1=L.nhwc_view(gcat[k], C, ah, aw), s1=0.0,
-                                 bn_state=(t[0], t[1], mean, rstd, plan.bnu[k + 1].weight))
+        dg, db = ops.conv_bn_backward(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt,
+                                      bn_x=L.nhwc_view(rq[k + 1]), C=C, bn_state=(t[0], t[1], mean, rstd),
+                                      gamma=plan.bnu[k + 1].weight, s_self=0.0, ch_off=C, dxv=L.nhwc_view(dq))
         put(plan.bnu[k + 1].weight, dg)
         put(plan.bnu[k + 1].bias, db)
     # ---- innermost r_{L-1}: ReLU backward (no BN)
@@ -232,20 +234,20 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
                                                device=dev))
         wd = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_DGRAD, cprev, co[k], dt)
         ga = _nhwc(B, 2 * S[k + 1][0], 2 * S[k + 1][1], cprev, dt, dev)
-        ops.conv(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt)
         # r_{k-1} feeds the skip (ReLU) and conv_k (LeakyReLU); then BN_down[k-1] (absent for k-1 == 0)
         dr = _nhwc(B, *S[k], cprev, dt, dev)
         xv = L.nhwc_view(rd[k - 1])
         g1 = L.nhwc_view(gcat[k - 1], 0, *S[k])
-        g2 = L.nhwc_view(ga, 0, *S[k])
         if k - 1 == 0:
-            ops.bn_backward(B, xv, cprev, dt, L.nhwc_view(dr), g1=g1, s1=0.0, g2=g2, s2=LRELU)
-        else:
+            ops.conv(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt)
+            ops.bn_backward(B, xv, cprev, dt, L.nhwc_view(dr), g1=g1, s1=0.0, g2=L.nhwc_view(ga, 0, *S[k]), s2=LRELU)
+        else:  # BN reduction fused into the input-gradient conv that produces ga
             mean, rstd = st_d[k - 1]
             t = tab_d[k - 1]
             bn = plan.bnd[k - 1]
-            dg, db = ops.bn_backward(B, xv, cprev, dt, L.nhwc_view(dr), g1=g1, s1=0.0, g2=g2, s2=LRELU,
-                                     bn_state=(t[0], t[1], mean, rstd, bn.weight))
+            dg, db = ops.conv_bn_backward(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt, bn_x=xv, C=cprev,
+                                          bn_state=(t[0], t[1], mean, rstd), gamma=bn.weight, s_self=LRELU,
+                                          g_other=g1, s_other=0.0, dxv=L.nhwc_view(dr))
             put(bn.weight, dg)
             put(bn.bias, db)
     return src_grads, grads
@@ -363,20 +365,23 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
         ga = _nhwc(B, ph, pw, cin, dt, dev)
         if s == 2:
             wd = ops.packed(cache, cv.weight, L.PACK_CONV_DGRAD, cin, gch, dt)
-            ops.conv(L.CONVT_S2, B, gv, gch, wd, cin, L.nhwc_view(ga), dt)
+            dkind = L.CONVT_S2
         else:
             wd = ops.packed(cache, cv.weight, L.PACK_CONV_S1_DGRAD, cin, gch, dt)
-            ops.conv(L.CONV_S1_DGRAD, B, gv, gch, wd, cin, L.nhwc_view(ga), dt)
-        # through LeakyReLU (and the BN of layer i-1's output, when present)
+            dkind = L.CONV_S1_DGRAD
+        # through LeakyReLU (and the BN of layer i-1's output, when present: its reduction fused
+        # into the input-gradient conv)
         gn = _nhwc(B, ph, pw, cin, dt, dev)
         xv = L.nhwc_view(raw[i])
         if tabs[i] is None:
+            ops.conv(dkind, B, gv, gch, wd, cin, L.nhwc_view(ga), dt)
             ops.bn_backward(B, xv, cin, dt, L.nhwc_view(gn), g1=L.nhwc_view(ga), s1=LRELU)
         else:
             mean, rstd = stats[i]
             bn = plan.bns[i - 2]
-            dg, db = ops.bn_backward(B, xv, cin, dt, L.nhwc_view(gn), g1=L.nhwc_view(ga), s1=LRELU,
-                                     bn_state=(tabs[i][0], tabs[i][1], mean, rstd, bn.weight))
+            dg, db = ops.conv_bn_backward(dkind, B, gv, gch, wd, cin, L.nhwc_view(ga), dt, bn_x=xv, C=cin,
+                                          bn_state=(tabs[i][0], tabs[i][1], mean, rstd), gamma=bn.weight,
+                                          s_self=LRELU, dxv=L.nhwc_view(gn))
             if need_w:
                 grads[id(bn.weight)] = dg
                 grads[id(bn.bias)] = db

@@ -111,10 +111,12 @@ def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
     return part, nch
 
 
-# bf16 LDS-DMA tile configurations (csrc/igemm_bf16.hip kTiles): cfg -> (BM, BN, WM, WN, stages)
-_BF16_TILES = [(128, 128, 2, 2, 2), (256, 128, 2, 2, 2), (128, 64, 2, 2, 2), (256, 64, 4, 1, 2), (64, 128, 1, 4, 2),
-               (64, 64, 2, 2, 2), (256, 256, 2, 4, 2), (128, 256, 2, 4, 2), (128, 128, 2, 2, 3), (128, 256, 2, 4, 3),
-               (64, 128, 1, 4, 3), (128, 64, 2, 2, 3), (64, 64, 2, 2, 3), (256, 128, 4, 2, 3)]
+# bf16 LDS-DMA tile configurations (csrc/igemm_bf16.hip kTiles): cfg -> (BM, BN, WM, WN, stages, BK)
+_BF16_TILES = [(128, 128, 2, 2, 2, 64), (256, 128, 2, 2, 2, 64), (128, 64, 2, 2, 2, 64), (256, 64, 4, 1, 2, 64),
+               (64, 128, 1, 4, 2, 64), (64, 64, 2, 2, 2, 64), (256, 256, 2, 4, 2, 64), (128, 256, 2, 4, 2, 64),
+               (128, 128, 2, 2, 3, 64), (128, 256, 2, 4, 3, 64), (64, 128, 1, 4, 3, 64), (128, 64, 2, 2, 3, 64),
+               (64, 64, 2, 2, 3, 64), (256, 128, 4, 2, 3, 64), (256, 256, 2, 4, 4, 32), (256, 128, 4, 2, 4, 32),
+               (128, 256, 2, 4, 4, 32), (128, 128, 2, 2, 4, 32), (128, 64, 2, 2, 4, 32), (64, 64, 2, 2, 4, 32)]
 
 
 def kernel_name(kind, B, gh, gw, cin, cout, dt):
@@ -129,7 +131,7 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt):
         return "narrow_tiled_kernel", True
     if cfg >= 0:
         t = _BF16_TILES[cfg]
-        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}>", ks == 1
+        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}>", ks == 1
     tname = {torch.float32: "float", torch.bfloat16: "__hip_bfloat16"}[dt]
     return f"igemm_kernel<{tname}, {bm}, {bn}>", ks == 1
 
@@ -140,6 +142,43 @@ def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1):
     taps = 4 if kind == L.CONVT_S2 else 16
     timer.append((name, single, 2.0 * outs * cout * taps * cin, e0, e1,
                   f"{['conv_s2', 'conv_s1', 'convT', 's1_dgrad'][kind]} B{B} grid{gh}x{gw} cin{cin} cout{cout}"))
+
+
+def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state, gamma, s_self, ch_off=0,
+                     g_other=None, s_other=0.0, dxv=None):
+    """Input-gradient conv (output yv) whose output feeds a BatchNorm backward, with the BN
+    reduction fused into the conv (stc_conv_bwd_bn), then the BN apply (stc_bn_bwd_apply):
+    dx = BN-backward of dn = out*act'(n, s_self) [+ g_other*act'(n, s_other)].
+    bn_state = (scale, shift, mean, rstd); returns (dgamma, dbeta)."""
+    dev = w_packed.device
+    l = lib()
+    gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
+    nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
+    ws, nb = _ws(nbytes, dev)
+    nch = l.stc_conv_bwd_bn_chunks(L.dtype_code(dt), kind, B, gh, gw, cin, cout, bn_x.H, bn_x.W)
+    part = torch.empty((nch, C, 2), dtype=torch.float32, device=dev)
+    scale, shift, mean, rstd = bn_state
+    fuse = L.BnbFuse(bn_x, g_other if g_other is not None else L.NULL_VIEW, scale.data_ptr(), shift.data_ptr(),
+                     mean.data_ptr(), rstd.data_ptr(), float(s_self), float(s_other), C, ch_off)
+    timer = _timer
+    if timer is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    check(l.stc_conv_bwd_bn(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse), ptr(part),
+                            nch, ptr(ws), nb, stream()), "stc_conv_bwd_bn")
+    if timer is not None:
+        e1.record()
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+    # apply: g1 = the conv output at the BN channels over the BN extent
+    g1 = L.View(yv.p, bn_x.H, bn_x.W, yv.bs, yv.rs, yv.ps, yv.co + ch_off, yv.cs, 0)
+    g1._keep = yv
+    dgamma = torch.empty(C, dtype=torch.float32, device=dev)
+    dbeta = torch.empty(C, dtype=torch.float32, device=dev)
+    check(l.stc_bn_bwd_apply(L.dtype_code(dt), B, bn_x, C, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), ptr(gamma),
+                             g1, float(s_self), g_other if g_other is not None else L.NULL_VIEW, float(s_other),
+                             ptr(part), nch, dxv, ptr(dgamma), ptr(dbeta), stream()), "stc_bn_bwd_apply")
+    return dgamma, dbeta
 
 
 def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True):

@@ -75,7 +75,7 @@ CASES = [  # B, Cin, Cout, H(grid), W(grid)
     (2, 8, 64, 64, 64),      # Cin = 8: a K-step spans 8 taps
     (1, 256, 64, 7, 9),
 ]
-CFGS = [None] + [(c, 1) for c in range(14)] + [(0, 2), (5, 4), (8, 2), (12, 4)]
+CFGS = [None] + [(c, 1) for c in range(20)] + [(0, 2), (5, 4), (8, 2), (12, 4), (14, 2), (17, 4)]
 
 
 @pytest.mark.parametrize("force", CFGS, ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
@@ -89,7 +89,8 @@ def test_conv_s2(case, force):
     check(y, ref, mean, var, f"conv s2 {case} {force}")
 
 
-@pytest.mark.parametrize("force", [None, (0, 1), (1, 1), (3, 1), (5, 2), (8, 1), (9, 1), (13, 1), (11, 2)],
+@pytest.mark.parametrize("force", [None, (0, 1), (1, 1), (3, 1), (5, 2), (8, 1), (9, 1), (13, 1), (11, 2), (14, 1),
+                                   (15, 1), (16, 1), (17, 2), (18, 1), (19, 1)],
                          ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 def test_convT_s2(case, force):
@@ -101,7 +102,7 @@ def test_convT_s2(case, force):
     check(y, ref, mean, var, f"convT {case} {force}")
 
 
-@pytest.mark.parametrize("force", [None, (0, 1), (6, 1), (0, 4)], ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
+@pytest.mark.parametrize("force", [None, (0, 1), (6, 1), (0, 4), (14, 1), (17, 1)], ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
 def test_conv_s1_and_dgrad(force):
     B, Cin, Cout, H = 2, 256, 512, 17   # PatchGAN layer 4 geometry (32x32 -> 31x31), smaller
     x = q(rnd(B, Cin, H, H, seed=5))
@@ -222,3 +223,63 @@ def test_wgrad_bf16_dma(case):
     err = float((got - gw).abs().max())
     scale = float(gw.abs().max())
     assert err <= 2e-5 * scale + 1e-6, f"wgrad {case}: {err:.3e} vs {scale:.3e}"  # exact products, fp32 sums
+
+
+class _BNT:
+    def __init__(self, C, seed):
+        g = torch.Generator().manual_seed(seed)
+        self.scale = (torch.rand(C, generator=g) + 0.5).to(DEV)
+        self.shift = (torch.randn(C, generator=g) * 0.2).to(DEV)
+        self.mean = (torch.randn(C, generator=g) * 0.1).to(DEV)
+        self.rstd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+        self.gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+
+
+FUSED = [  # kind, B, Cin(dy), Cout(conv out), grid H, W (GEMM grid), C (BN), ch_off, with g_other
+    ("convT", 2, 128, 64, 16, 16, 64, 0, True),     # G down path: conv-s2 dgrad, skip gradient as g_other
+    ("convT", 4, 512, 512, 2, 2, 512, 0, True),     # deep level: split-K reduction path
+    ("conv_s2", 2, 64, 256, 16, 16, 128, 128, False),  # G up path: second half of the concat gradient
+    ("s1_dgrad", 2, 256, 128, 15, 15, 128, 0, False),  # PatchGAN layer-4 input gradient
+]
+
+
+@pytest.mark.parametrize("case", FUSED, ids=lambda c: "_".join(map(str, c)))
+def test_conv_bn_backward_fused(case):
+    """stc_conv_bwd_bn (BN-backward reduction in the conv epilogue) == conv + separate BN backward."""
+    kind, B, Cin, Cout, GH, GW, C, ch_off, other = case
+    kd = {"convT": L.CONVT_S2, "conv_s2": L.CONV_S2, "s1_dgrad": L.CONV_S1_DGRAD}[kind]
+    if kd == L.CONVT_S2:
+        dy_hw, out_hw = (GH, GW), (2 * GH, 2 * GW)
+        w = ops.pack(L.PACK_CONVT_FWD, rnd(Cin, Cout, 4, 4, seed=51, scale=0.05).to(DEV), Cout, Cin, BF)
+    elif kd == L.CONV_S2:
+        dy_hw, out_hw = (2 * GH, 2 * GW), (GH, GW)
+        w = ops.pack(L.PACK_CONV_FWD, rnd(Cout, Cin, 4, 4, seed=51, scale=0.05).to(DEV), Cout, Cin, BF)
+    else:
+        dy_hw, out_hw = (GH - 1, GW - 1), (GH, GW)
+        w = ops.pack(L.PACK_CONV_S1_DGRAD, rnd(Cin, Cout, 4, 4, seed=51, scale=0.05).to(DEV), Cout, Cin, BF)
+    dy = (torch.randn((B, *dy_hw, Cin), generator=torch.Generator().manual_seed(52)) * 0.5).to(DEV, BF)
+    x = torch.randn((B, *out_hw, C), generator=torch.Generator().manual_seed(53)).to(DEV, BF)
+    go = torch.randn((B, *out_hw, C), generator=torch.Generator().manual_seed(54)).to(DEV, BF) if other else None
+    bn = _BNT(C, 55)
+    st = (bn.scale, bn.shift, bn.mean, bn.rstd)
+    # fused
+    out1 = torch.zeros((B, *out_hw, Cout), device=DEV, dtype=BF)
+    dx1 = torch.empty((B, *out_hw, C), device=DEV, dtype=BF)
+    dg1, db1 = ops.conv_bn_backward(kd, B, L.nhwc_view(dy), Cin, w, Cout, L.nhwc_view(out1), BF, bn_x=L.nhwc_view(x),
+                                    C=C, bn_state=st, gamma=bn.gamma, s_self=0.2, ch_off=ch_off,
+                                    g_other=None if go is None else L.nhwc_view(go), s_other=0.0,
+                                    dxv=L.nhwc_view(dx1))
+    # reference: conv, then the two-pass BN backward
+    out2 = torch.zeros((B, *out_hw, Cout), device=DEV, dtype=BF)
+    ops.conv(kd, B, L.nhwc_view(dy), Cin, w, Cout, L.nhwc_view(out2), BF)
+    dx2 = torch.empty((B, *out_hw, C), device=DEV, dtype=BF)
+    dg2, db2 = ops.bn_backward(B, L.nhwc_view(x), C, BF, L.nhwc_view(dx2), g1=L.nhwc_view(out2, ch_off), s1=0.2,
+                               g2=None if go is None else L.nhwc_view(go), s2=0.0,
+                               bn_state=(bn.scale, bn.shift, bn.mean, bn.rstd, bn.gamma))
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
+    for a, b_, nm in ((dg1, dg2, "dgamma"), (db1, db2, "dbeta")):
+        err = float((a - b_).abs().max())
+        assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm} {case}: {err:.3e}"
+    err = float((dx1.float() - dx2.float()).abs().max())
+    assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx {case}: {err:.3e}"
