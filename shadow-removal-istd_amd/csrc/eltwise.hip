@@ -39,11 +39,8 @@ __global__ void gather_kernel(int B, int H, int W, int nsrc, Src4 s, View d, int
 
 // Vectorised form for NHWC destinations (cs == 1, Cpad <= 16): one pixel per thread, the
 // channel -> (source, plane) map in kernel arguments, 16-byte stores.
-struct ChanMap {
-  int src[16], ch[16];
-};
 template <typename T>
-__global__ void gather_vec_kernel(int B, int H, int W, Src4 s, ChanMap cm, View d, int Cpad) {
+__global__ void gather_vec_kernel(int B, int H, int W, int nsrc, Src4 s, View d, int Cpad) {
   constexpr int N = 16 / sizeof(T);
   const long long HW = (long long)H * W, P = HW * B;
   for (long long pix = (long long)blockIdx.x * blockDim.x + threadIdx.x; pix < P;
@@ -51,23 +48,38 @@ __global__ void gather_vec_kernel(int B, int H, int W, Src4 s, ChanMap cm, View 
     const int b = (int)(pix / HW);
     const long long hw = pix - (long long)b * HW;
     const int y = (int)(hw / W), x = (int)(hw - (long long)y * W);
-    T* out = reinterpret_cast<T*>(d.p) + vidx(d, b, y, x, 0);
-    for (int g = 0; g < Cpad; g += N) {
-      float v[N];
+    float v[16];
 #pragma unroll
-      for (int e = 0; e < N; ++e) {
-        const int c = g + e;
-        const int k = c < 16 ? cm.src[c] : -1;
-        v[e] = k >= 0 ? s.p[k][((long long)b * s.c[k] + cm.ch[c]) * HW + hw] : 0.f;
+    for (int c = 0; c < 16; ++c) v[c] = 0.f;
+    int c0 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // sources unrolled: no dynamic indexing of kernel arguments
+      if (k < nsrc) {
+        const float* src = s.p[k] + (long long)b * s.c[k] * HW + hw;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (j < s.c[k]) {
+            const float t = src[(long long)j * HW];
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+              if (c == c0 + j) v[c] = t;
+          }
+        }
+        c0 += s.c[k];
       }
+    }
+    T* out = reinterpret_cast<T*>(d.p) + vidx(d, b, y, x, 0);
+#pragma unroll
+    for (int g = 0; g < 16; g += N) {
+      if (g >= Cpad) break;
       if constexpr (sizeof(T) == 4) {
-        *reinterpret_cast<float4*>(out + g) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(out + g) = make_float4(v[g], v[g + 1], v[g + 2], v[g + 3]);
       } else {
         uint4 o;
-        o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-        o.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-        o.z = (unsigned)f2bf(v[4]) | ((unsigned)f2bf(v[5]) << 16);
-        o.w = (unsigned)f2bf(v[6]) | ((unsigned)f2bf(v[7]) << 16);
+        o.x = (unsigned)f2bf(v[g]) | ((unsigned)f2bf(v[g + 1]) << 16);
+        o.y = (unsigned)f2bf(v[g + 2]) | ((unsigned)f2bf(v[g + 3]) << 16);
+        o.z = (unsigned)f2bf(v[g + 4]) | ((unsigned)f2bf(v[g + 5]) << 16);
+        o.w = (unsigned)f2bf(v[g + 6]) | ((unsigned)f2bf(v[g + 7]) << 16);
         *reinterpret_cast<uint4*>(out + g) = o;
       }
     }
@@ -257,13 +269,8 @@ extern "C" int stc_gather_nchw(int dtype, int B, int H, int W, int nsrc, const f
   const int N = dtype == STC_F32 ? 4 : 8;
   if (dst.cs == 1 && Cpad <= 16 && Cpad % N == 0 && dst.ps % N == 0 && dst.co % N == 0 && dst.rs % N == 0 &&
       dst.bs % N == 0) {
-    ChanMap cm{};
-    int c = 0;
-    for (int k = 0; k < nsrc; ++k)
-      for (int j = 0; j < src_c[k]; ++j, ++c) { cm.src[c] = k; cm.ch[c] = j; }
-    for (; c < 16; ++c) { cm.src[c] = -1; cm.ch[c] = 0; }
-    if (dtype == STC_F32) hipLaunchKernelGGL(gather_vec_kernel<float>, dim3(grid_for(P)), dim3(256), 0, st, B, H, W, s, cm, d, Cpad);
-    else hipLaunchKernelGGL(gather_vec_kernel<bf16>, dim3(grid_for(P)), dim3(256), 0, st, B, H, W, s, cm, d, Cpad);
+    if (dtype == STC_F32) hipLaunchKernelGGL(gather_vec_kernel<float>, dim3(grid_for(P)), dim3(256), 0, st, B, H, W, nsrc, s, d, Cpad);
+    else hipLaunchKernelGGL(gather_vec_kernel<bf16>, dim3(grid_for(P)), dim3(256), 0, st, B, H, W, nsrc, s, d, Cpad);
     STC_CHECK_LAUNCH();
     return 0;
   }

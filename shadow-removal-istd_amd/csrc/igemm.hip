@@ -858,11 +858,7 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
     int32_t need = 0;
     bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &need, nullptr);
     (void)g;
-    STC_REQUIRE(nchunks >= need, "stc_conv_bwd_bn: %d chunks < %d", nchunks, need);
-    // unused chunk rows (if the caller sized for the fallback) must read as zeros in the finalize
-    if (nchunks > need) {
-      (void)hipMemsetAsync(part2 + (size_t)need * bnb->C * 2, 0, (size_t)(nchunks - need) * bnb->C * 2 * 4, st);
-    }
+    STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks)", nchunks, need);
     return bf16_conv_fwd(kind, B, dy, Cin, w_packed, Cout, out, nullptr, 0, 0, nullptr, need, nullptr, workspace,
                          workspace_bytes, st, bnb, part2);
   }
@@ -874,8 +870,7 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
   g1.H = bnb->x.H;
   g1.W = bnb->x.W;
   const int need = stc_chan_stats_chunks(B, bnb->x.H, bnb->x.W);
-  STC_REQUIRE(nchunks >= need, "stc_conv_bwd_bn: %d chunks < %d", nchunks, need);
-  if (nchunks > need) (void)hipMemsetAsync(part2 + (size_t)need * bnb->C * 2, 0, (size_t)(nchunks - need) * bnb->C * 2 * 4, st);
+  STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks)", nchunks, need);
   return stc_bn_bwd_reduce(dtype, B, bnb->x, bnb->C, bnb->scale, bnb->shift, bnb->mean, bnb->rstd, g1, bnb->slope_self,
                            bnb->g_other, bnb->slope_other, part2, need, stream);
 }

@@ -107,7 +107,7 @@ __device__ __forceinline__ int kswz(int row) {
   else return (row >> 1) & 3;
 }
 
-template <int BM, int BN, int WM, int WN, int NST, int BK>
+template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB>
 __global__ void __launch_bounds__(64 * WM * WN)
 igemm_bf16_kernel(const GParams p) {
   constexpr int NW = WM * WN;
@@ -388,15 +388,33 @@ igemm_bf16_kernel(const GParams p) {
         }
     __syncthreads();
     constexpr int CPR = BN / 8;  // 16-byte chunks per row (64*NW is a multiple of CPR: fixed cc per thread)
+    constexpr int ITER = BM * CPR / (64 * NW);
+    static_assert(ITER * 64 * NW == BM * CPR, "whole store iterations");
+    const int cc = tid % CPR;
+    const int n = n0 + cc * 8;
+    if constexpr (!BNB) {
+#pragma unroll 4
+      for (int it = 0; it < ITER; ++it) {
+        const int row = (tid + it * 64 * NW) / CPR;
+        const int m = m0 + row;
+        if (m >= p.M || n >= p.N) continue;
+        const int b = m / GHW, rem = m - b * GHW;
+        const int y = rem / p.GW, x = rem - y * p.GW;
+        const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+        const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
+      }
+      return;
+    }
+    // fused BatchNorm-backward reduction: {sum dn, sum dn*xhat} of this thread's 8-channel chunk
     float sa[8], sb[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sa[e] = 0.f; sb[e] = 0.f; }
-    const int cc = tid % CPR;
-    const int nch = n0 + cc * 8 - p.bch_off;  // BN channel of this thread's chunk
-    const bool bnb_on = p.part2 != nullptr && nch >= 0 && nch < p.bC;
-    for (int q = tid; q < BM * CPR; q += 64 * NW) {
-      const int row = q / CPR;
-      const int m = m0 + row, n = n0 + cc * 8;
+    const int nch = n - p.bch_off;  // BN channel of this thread's chunk
+    const bool bnb_on = nch >= 0 && nch < p.bC;
+    for (int it = 0; it < ITER; ++it) {
+      const int row = (tid + it * 64 * NW) / CPR;
+      const int m = m0 + row;
       if (m >= p.M || n >= p.N) continue;
       const int b = m / GHW, rem = m - b * GHW;
       const int y = rem / p.GW, x = rem - y * p.GW;
@@ -405,14 +423,13 @@ igemm_bf16_kernel(const GParams p) {
       const uint4 t = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = t;
       if (bnb_on && oy < p.bxH && ox < p.bxW) {
-        float v[8];
         const unsigned w[4] = {t.x, t.y, t.z, t.w};
+        float v[8];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { v[2 * e] = __uint_as_float(w[e] << 16); v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u); }
+        for (int q = 0; q < 4; ++q) { v[2 * q] = __uint_as_float(w[q] << 16); v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
         bnb_accum(p, b, oy, ox, nch, v, sa, sb);
       }
     }
-    if (p.part2 == nullptr) return;
     // per-tile reduction over the threads sharing a channel chunk (fixed order)
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [threads][16]
@@ -742,7 +759,10 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
   const size_t lds = bf16_lds_bytes(pl.cfg);
 #define STC_B(I, BM_, BN_, WM_, WN_, NST_, BK_)                                                             \
   case I:                                                                                                   \
-    hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
+    if (p.part2)                                                                                            \
+      hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, true>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
+    else                                                                                                    \
+      hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, false>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
     break;
   switch (pl.cfg) {
     STC_B(0, 128, 128, 2, 2, 2, 64)
