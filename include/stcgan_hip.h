@@ -11,7 +11,10 @@
  *                    ConvTranspose2d 4x4 s2 p1 fwd   STCGAN/networks.py:112-114,119-121,126-128
  *                    and both layers' input gradient (conv dgrad == convT fwd geometry and vice versa)
  *   stc_conv_wgrad   weight gradient of both         (autograd of the same lines)
- *   stc_pack_weight  torch weight layout -> GEMM operand layout (per-op packing)
+ *   stc_conv_fwd_ex  the same forward with the BatchNorm batch statistics of its output fused in
+ *                    (Conv/ConvT -> BatchNorm2d pairs, networks.py:104-109,112-121,167-170,176-179)
+ *   stc_conv_bwd_bn  input-gradient conv with the consumer BatchNorm-backward reduction fused in
+ *   stc_pack_weight / stc_pack_weights  torch weight layout -> GEMM operand layout (one / many tensors)
  *   stc_chan_stats / stc_bn_finalize               BatchNorm2d train/eval forward, STCGAN/networks.py:107,109,170,179
  *   stc_bn_bwd_reduce / stc_bn_bwd_apply            BatchNorm2d backward fused with LeakyReLU/ReLU backward
  *                    (with mean == NULL: LeakyReLU(0.2)/ReLU backward alone, networks.py:106,108,158)
@@ -136,6 +139,9 @@ int stc_conv_wgrad(int dtype, int B, int stride,
                    const float* g_scale, const float* g_shift, int g_act, float g_slope,
                    float* dW, void* workspace, int64_t workspace_bytes, void* stream);
 int64_t stc_conv_wgrad_workspace(int dtype, int B, int Hd, int Wd, int R, int Cg);
+/* Tuning / test hook: force the bf16 weight-gradient plan {tile config 0..5, pixel splits (0 = auto)}
+ * of the following calls; cfg = -1 restores the automatic plan.  Process-global, not thread-safe. */
+int stc_conv_wgrad_force_plan(int cfg, int nsplit);
 
 /* ---- weight packing ----------------------------------------------------------
  * W is a torch weight [P][Q][4][4] fp32.  out is [phases][N_pad][T][C_pad] of dtype.

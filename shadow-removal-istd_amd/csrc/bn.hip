@@ -147,14 +147,13 @@ __global__ void __launch_bounds__(256) chan_stats_kernel(View x, PixDiv pd, long
 // chunk mean m_b = shift + S1/n, chunk M2_b = S2 - S1^2/n; then (exactly, in fp64)
 //   mean = sum n_b m_b / N,   M2 = sum [M2_b + n_b (m_b - mean)^2]
 // in two passes over the chunks (one block per channel, fixed-order tree -> deterministic).
+// (butterfly within each wave, then the 4 wave totals in a fixed order: deterministic, 2 barriers)
 __device__ __forceinline__ double block_sum256(double v, double* sh) {
-  sh[threadIdx.x] = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
-    __syncthreads();
-  }
-  const double r = sh[0];
+  const double r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
   __syncthreads();
   return r;
 }

@@ -645,11 +645,13 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
     cfg = force_cfg;
     ks = force_ks > 0 ? force_ks : 1;
   } else {
-    int order[4], no = 0;
+    int order[5], no = 0;
     if (N >= 256) {
-      if ((long long)M * nphase >= 8192) { order[0] = 6; order[1] = 0; order[2] = 4; order[3] = 5; }
+      if ((long long)M * nphase >= 8192 && K >= 8192) {  // long reductions: 8-wave 128x256 (s1 dgrad)
+        order[0] = 6; order[1] = 7; order[2] = 0; order[3] = 4; order[4] = 5; no = 5;
+      } else if ((long long)M * nphase >= 8192) { order[0] = 6; order[1] = 0; order[2] = 4; order[3] = 5; }
       else { order[0] = 0; order[1] = 4; order[2] = 12; order[3] = 5; }
-      no = 4;
+      if (no == 0) no = 4;
     } else if (N >= 128) {
       order[0] = 0; order[1] = 4; order[2] = 5; no = 3;
     } else if (K <= 512) {

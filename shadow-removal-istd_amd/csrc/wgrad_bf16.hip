@@ -4,14 +4,18 @@
 //   Gcol[p][tap, ci] = G[b, oy*s + kh - 1, ox*s + kw - 1, ci]      (tap = kh*4 + kw)
 //   Conv2d s2/s1 : D = dy (output grid), G = x (input);  ConvT s2 : D = x (input grid), G = dy.
 // The reduction runs over pixels.  Both operands are pixel-major in HBM (channels contiguous),
-// so each K-step (64 pixels) is DMA'd as [pixel][128 channels] 256-byte rows with the 16-byte
-// chunk index XOR-swizzled by ((row&3)<<2 | (row>>2)&3) on the source side, and the MFMA
-// operands (8 consecutive pixels of one channel per lane) come out of ds_read_b64_tr_b16
-// (4 rows x 16 columns per 16-lane group, transposed by the LDS) -- conflict-free for the
-// 16x16x32 operand with the two 4-row blocks of a 32-lane half 8 rows apart.
-// Tile 128 (r) x 128 (col), 4 waves of 64x64, 2-stage ring (DMA of step s+1 under the
-// MFMAs of step s).  The pixel range is split over blockIdx.z into fp32 slabs that
-// wgrad_reduce_kernel sums in a fixed order; a single split writes torch layout directly.
+// so each K-step (64 pixels) is DMA'd as [pixel][BM or BN channels] rows with the 16-byte chunk
+// index XOR-swizzled on the source side (wswz below), and the MFMA operands (8 consecutive
+// pixels of one channel per lane) come out of ds_read_b64_tr_b16 (4 rows x 16 columns per
+// 16-lane group, transposed by the LDS) -- conflict-free for the 16x16x32 operand with the two
+// 4-row blocks of a 32-lane half 8 rows apart.
+// Tiles: 128x128 (4 waves of 64x64), 64x128, a swapped 128x16 for R <= 16, and 8-wave
+// 256x256 / 256x128 / 128x256 tiles for the large layers (half the DMA bytes per MFMA of the
+// 128x128 tile: the L2->LDS stream, not the MFMA, bounds the small tiles).  2-stage ring (DMA of
+// step s+1 under the MFMAs of step s).  The pixel range is split over blockIdx.z into fp32 slabs
+// that wgrad_reduce_kernel sums in a fixed order; a single split writes torch layout directly.
+#include <atomic>
+
 #include "common.hpp"
 
 namespace stc {
@@ -52,15 +56,20 @@ __device__ __forceinline__ int fdiv(int n, int d, float inv) {
 
 // LDS image swizzle of a [pixel][W channels] operand row (W*2 bytes, CH = W/8 chunks):
 //   CH = 16 (256-B rows): chunk ^ ((row&3)<<2 | (row>>2)&3)   (T10 image (b))
+//   CH = 32 (512-B rows): the same XOR on the low 4 chunk bits -- the 64 banks span 256 B, so a
+//                         512-B row is bank-equivalent to two 256-B rows at the same offsets
 //   CH = 8  (128-B rows): chunk ^ (2*((row>>1)&1) + 4*((row>>3)&1))
 //   CH = 2  (32-B rows) : none (2-way conflicts on a small operand)
 // chosen so that the transposed 16x16x32 operand reads (rows 8g+q, g = 0/1 per 32-lane half) hit
 // distinct bank slots.
 template <int CH>
 __device__ __forceinline__ int wswz(int row) {
-  if constexpr (CH == 16) return ((row & 3) << 2) | ((row >> 2) & 3);
+  if constexpr (CH >= 16) return ((row & 3) << 2) | ((row >> 2) & 3);
   else if constexpr (CH == 8) return 2 * ((row >> 1) & 1) + 4 * ((row >> 3) & 1);
   else return 0;
+}
+__device__ __forceinline__ int wswz_rt(int ch, int row) {
+  return ch >= 16 ? wswz<16>(row) : (ch == 8 ? wswz<8>(row) : 0);
 }
 
 constexpr int WB_BK = 64;
@@ -111,10 +120,7 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
   auto role = [&](bool is_g, int ch_per_row, int piece, int first) -> Role {
     const int rows_pp = 64 / ch_per_row;
     const int row = piece * rows_pp + lane / ch_per_row;
-    int swz = 0;
-    if (ch_per_row == 16) swz = wswz<16>(row);
-    else if (ch_per_row == 8) swz = wswz<8>(row);
-    const int chunk = (lane % ch_per_row) ^ swz;
+    const int chunk = (lane % ch_per_row) ^ wswz_rt(ch_per_row, row);
     Role ro{};
     if (!is_g) {
       const int r = first + chunk * 8;
@@ -204,10 +210,7 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
   const int q = (lane & 15) >> 2, pcol = lane & 3;
   auto tr_off = [&](int row, int colbase, int rowbytes, int ch) {
     const int col = colbase + 4 * pcol;
-    int swz = 0;
-    if (ch == 16) swz = wswz<16>(row);
-    else if (ch == 8) swz = wswz<8>(row);
-    return row * rowbytes + 16 * ((col >> 3) ^ swz) + 2 * (col & 7);
+    return row * rowbytes + 16 * ((col >> 3) ^ wswz_rt(ch, row)) + 2 * (col & 7);
   };
 
   auto compute = [&](int stage) {
@@ -294,22 +297,60 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
 }
 
 // ------------------------------------------------------------------------- host
+// Tile configurations: {BM (rows), BN (columns), waves, swapped}
+struct WbCfg {
+  int BM, BN, waves;
+  bool swap;
+};
+constexpr WbCfg kWbCfg[] = {
+    {128, 128, 4, false},  // 0
+    {64, 128, 4, false},   // 1: R <= 64
+    {128, 16, 4, true},    // 2: R <= 16 (rows = im2col columns, columns = R)
+    {256, 256, 8, false},  // 3
+    {256, 128, 8, false},  // 4
+    {128, 256, 8, false},  // 5
+};
+constexpr int kNumWbCfg = sizeof(kWbCfg) / sizeof(kWbCfg[0]);
+
+// tuning / test hook (stc_conv_wgrad_force_plan): -1 = automatic plan
+static std::atomic<int> g_wb_force_cfg{-1}, g_wb_force_ns{0};
+
 struct WbPlan {
-  int cfg;  // 0: 128x128 (rows = D channels), 1: 64x128 (R <= 64), 2: swapped 128x16 (R <= 16)
-  int BM, BN, mtiles, ntiles, nsplit, pchunk;
+  int cfg, BM, BN, mtiles, ntiles, nsplit, pchunk;
 };
 
 static WbPlan wb_plan(int P, int R, int Cg) {
   WbPlan pl{};
   const long long ncol = 16LL * Cg;
-  if (R <= 16) { pl.cfg = 2; pl.BM = 128; pl.BN = 16; pl.mtiles = cdiv(ncol, 128); pl.ntiles = 1; }
-  else if (R <= 64) { pl.cfg = 1; pl.BM = 64; pl.BN = 128; pl.mtiles = cdiv(R, 64); pl.ntiles = cdiv(ncol, 128); }
-  else { pl.cfg = 0; pl.BM = 128; pl.BN = 128; pl.mtiles = cdiv(R, 128); pl.ntiles = cdiv(ncol, 128); }
-  const long long tiles = (long long)pl.mtiles * pl.ntiles;
   const int steps = cdiv(P, WB_BK);
+  int cfg = g_wb_force_cfg.load(std::memory_order_relaxed);
+  int force_ns = g_wb_force_ns.load(std::memory_order_relaxed);
+  if (cfg < 0 || cfg >= kNumWbCfg) {
+    force_ns = 0;
+    // (fitted to scripts/tune_wgrad.py over one train step: the 8-wave tiles pay off once each
+    // split still has a long pixel loop; 128x128 stays best for the shorter reductions)
+    if (R <= 16) cfg = 2;
+    else if (R <= 64) cfg = 1;
+    else if (ncol >= 1024 && ((R >= 512 && P >= 16384) || (R >= 256 && P >= 65536))) cfg = 3;
+    else if (R <= 128 && ncol >= 1024 && P >= 65536) cfg = 5;
+    else cfg = 0;
+  }
+  const WbCfg& c = kWbCfg[cfg];
+  pl.cfg = cfg;
+  pl.BM = c.BM;
+  pl.BN = c.BN;
+  if (c.swap) { pl.mtiles = (int)cdiv(ncol, c.BM); pl.ntiles = cdiv(R, c.BN); }
+  else { pl.mtiles = cdiv(R, c.BM); pl.ntiles = (int)cdiv(ncol, c.BN); }
+  const long long tiles = (long long)pl.mtiles * pl.ntiles;
   int ns = 1;
-  // ~2 blocks per CU, at least 8 K-steps (512 pixels) per split
-  while (tiles * ns < 512 && ns * 2 <= 256 && steps / (ns * 2) >= 8) ns *= 2;
+  if (force_ns > 0) {
+    ns = std::min(force_ns, std::max(steps, 1));
+  } else {
+    // about 2 four-wave blocks (one eight-wave block; 4 of the short swapped tile) per CU, at least
+    // 8 K-steps (512 pixels) per split
+    const long long target = c.waves == 8 ? 256 : (c.swap ? 1024 : 512);
+    while (tiles * ns < target && ns * 2 <= 256 && steps / (ns * 2) >= 8) ns *= 2;
+  }
   pl.pchunk = cdiv(steps, ns) * WB_BK;
   pl.nsplit = cdiv(P, pl.pchunk);
   return pl;
@@ -357,7 +398,10 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
   switch (pl.cfg) {
     case 0: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false>), grid, dim3(256), lds, st, p); break;
     case 1: hipLaunchKernelGGL((wgrad_bf16_kernel<64, 128, 1, 4, false>), grid, dim3(256), lds, st, p); break;
-    default: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 16, 4, 1, true>), grid, dim3(256), lds, st, p); break;
+    case 2: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 16, 4, 1, true>), grid, dim3(256), lds, st, p); break;
+    case 3: hipLaunchKernelGGL((wgrad_bf16_kernel<256, 256, 2, 4, false>), grid, dim3(512), lds, st, p); break;
+    case 4: hipLaunchKernelGGL((wgrad_bf16_kernel<256, 128, 4, 2, false>), grid, dim3(512), lds, st, p); break;
+    default: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 256, 2, 4, false>), grid, dim3(512), lds, st, p); break;
   }
   STC_CHECK_LAUNCH();
   if (pl.nsplit <= 1) return 0;
@@ -370,3 +414,13 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
 }
 
 }  // namespace stc
+
+// Tuning / test hook: force the bf16 weight-gradient plan {tile config 0..5, pixel splits (0 = auto)}
+// for the following calls (cfg = -1 restores the automatic plan).  Process-global; not for use
+// while other threads launch weight gradients.
+extern "C" int stc_conv_wgrad_force_plan(int cfg, int nsplit) {
+  if (cfg < -1 || cfg >= stc::kNumWbCfg || nsplit < 0) return 1;
+  stc::g_wb_force_cfg.store(cfg);
+  stc::g_wb_force_ns.store(nsplit);
+  return 0;
+}

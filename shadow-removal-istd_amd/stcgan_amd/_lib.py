@@ -10,7 +10,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstcgan_hip.so")
+LIB_PATH = os.environ.get("STC_LIB_PATH") or os.path.join(_HERE, "libstcgan_hip.so")  # override: A/B timing
 
 F32, BF16 = 0, 1
 CONV_S2, CONV_S1, CONVT_S2, CONV_S1_DGRAD = 0, 1, 2, 3
@@ -58,6 +58,7 @@ _SIGS = {
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
                               _f32, _vp, _vp, _i64, _vp]),
     "stc_conv_wgrad_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32]),
+    "stc_conv_wgrad_force_plan": (_i32, [_i32, _i32]),
     "stc_pack_weight": (_i32, [_i32, _i32, _vp, _i32, _i32, _vp, _i32, _i32, _vp]),
     "stc_pack_weights": (_i32, [_i32, _i32, _vp, _vp]),
     "stc_chan_stats": (_i32, [_i32, _i32, View, _i32, _vp, _i32, _vp]),

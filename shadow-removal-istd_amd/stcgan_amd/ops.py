@@ -119,8 +119,9 @@ _BF16_TILES = [(128, 128, 2, 2, 2, 64), (256, 128, 2, 2, 2, 64), (128, 64, 2, 2,
                (128, 256, 2, 4, 4, 32), (128, 128, 2, 2, 4, 32), (128, 64, 2, 2, 4, 32), (64, 64, 2, 2, 4, 32)]
 
 
-def kernel_name(kind, B, gh, gw, cin, cout, dt):
-    """(kernel symbol as rocprof shows it, launches-a-single-kernel) of one conv call."""
+def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
+    """(kernel symbol as rocprof shows it, launches-a-single-kernel) of one conv call
+    (bnb: the input-gradient form with the BatchNorm-backward reduction fused in)."""
     ws, _, plan = conv_query(kind, B, gh, gw, cin, cout, dt)
     bm, bn, ks, narrow, cfg = plan
     if narrow:
@@ -131,13 +132,13 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt):
         return "narrow_tiled_kernel", True
     if cfg >= 0:
         t = _BF16_TILES[cfg]
-        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}>", ks == 1
+        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}, {str(bnb).lower()}>", ks == 1
     tname = {torch.float32: "float", torch.bfloat16: "__hip_bfloat16"}[dt]
     return f"igemm_kernel<{tname}, {bm}, {bn}>", ks == 1
 
 
-def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1):
-    name, single = kernel_name(kind, B, gh, gw, cin, cout, dt)
+def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=False):
+    name, single = kernel_name(kind, B, gh, gw, cin, cout, dt, bnb)
     outs = B * gh * gw * (4 if kind == L.CONVT_S2 else 1)
     taps = 4 if kind == L.CONVT_S2 else 16
     timer.append((name, single, 2.0 * outs * cout * taps * cin, e0, e1,
@@ -169,7 +170,7 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
                             nch, ptr(ws), nb, stream()), "stc_conv_bwd_bn")
     if timer is not None:
         e1.record()
-        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=yv.cs == 1)
     # apply: g1 = the conv output at the BN channels over the BN extent
     g1 = L.View(yv.p, bn_x.H, bn_x.W, yv.bs, yv.rs, yv.ps, yv.co + ch_off, yv.cs, 0)
     g1._keep = yv

@@ -283,3 +283,28 @@ def test_conv_bn_backward_fused(case):
         assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm} {case}: {err:.3e}"
     err = float((dx1.float() - dx2.float()).abs().max())
     assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx {case}: {err:.3e}"
+
+
+WGRAD_FORCED = [  # (case, tile config, pixel splits): the 8-wave tiles on ragged / offset shapes
+    (("conv", 2, 2, 64, 256, 32, 32), 3, 0),
+    (("conv", 2, 2, 64, 256, 32, 32), 4, 2),
+    (("conv", 2, 2, 64, 256, 32, 32), 5, 1),
+    (("conv", 1, 2, 256, 512, 17, 17), 3, 0),
+    (("conv", 2, 3, 32, 96, 10, 14), 3, 3),    # R, columns and pixels all ragged for a 256 tile
+    (("conv", 2, 3, 32, 96, 10, 14), 5, 0),
+    (("convT", 2, 2, 128, 64, 16, 16), 4, 0),
+    (("convT", 2, 2, 1024, 512, 2, 2), 3, 1),
+    (("conv", 2, 2, 8, 64, 64, 64), 5, 0),      # Cg = 8: 16 taps per 128 columns
+    (("conv", 1, 2, 512, 8, 17, 17), 0, 4),     # R = 8 on a 128-row tile
+]
+
+
+@pytest.mark.parametrize("case,cfg,ns", WGRAD_FORCED, ids=lambda c: "_".join(map(str, c)) if isinstance(c, tuple) else str(c))
+def test_wgrad_bf16_forced_tiles(case, cfg, ns):
+    """Every weight-gradient tile configuration (stc_conv_wgrad_force_plan) against autograd."""
+    lib = L.lib()
+    assert lib.stc_conv_wgrad_force_plan(cfg, ns) == 0
+    try:
+        test_wgrad_bf16_dma(case)
+    finally:
+        lib.stc_conv_wgrad_force_plan(-1, 0)
