@@ -412,22 +412,52 @@ igemm_bf16_kernel(const GParams p) {
     for (int e = 0; e < 8; ++e) { sa[e] = 0.f; sb[e] = 0.f; }
     const int nch = n - p.bch_off;  // BN channel of this thread's chunk
     const bool bnb_on = nch >= 0 && nch < p.bC;
-    for (int it = 0; it < ITER; ++it) {
-      const int row = (tid + it * 64 * NW) / CPR;
-      const int m = m0 + row;
-      if (m >= p.M || n >= p.N) continue;
-      const int b = m / GHW, rem = m - b * GHW;
-      const int y = rem / p.GW, x = rem - y * p.GW;
-      const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
-      const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
-      const uint4 t = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = t;
-      if (bnb_on && oy < p.bxH && ox < p.bxW) {
-        const unsigned w[4] = {t.x, t.y, t.z, t.w};
-        float v[8];
+    const int nchc = bnb_on ? nch : 0;
+    // groups of G rows: the BN-input / second-gradient loads of a group are in flight together
+    // (one latency per group instead of one per row), then the reduction arithmetic
+    constexpr int G = ITER < 4 ? ITER : 4;
+    static_assert(ITER % G == 0, "whole groups");
+    for (int it0 = 0; it0 < ITER; it0 += G) {
+      uint4 tv[G], xr[G], gr[G];
+      bool ok[G];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { v[2 * q] = __uint_as_float(w[q] << 16); v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u); }
-        bnb_accum(p, b, oy, ox, nch, v, sa, sb);
+      for (int u = 0; u < G; ++u) {
+        const int row = (tid + (it0 + u) * 64 * NW) / CPR;
+        const int m = m0 + row;
+        const bool in = m < p.M && n < p.N;
+        const int mm = in ? m : m0;
+        const int b = mm / GHW, rem = mm - b * GHW;
+        const int y = rem / p.GW, x = rem - y * p.GW;
+        const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+        tv[u] = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
+        if (in) {
+          const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = tv[u];
+        }
+        ok[u] = in && bnb_on && oy < p.bxH && ox < p.bxW;
+        const int oyc = ok[u] ? oy : 0, oxc = ok[u] ? ox : 0;
+        xr[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.bx) + (long long)b * p.bx_bs +
+                                                (long long)oyc * p.bx_rs + (long long)oxc * p.bx_ps + p.bx_co + nchc);
+        gr[u] = p.bg ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.bg) + (long long)b * p.bg_bs +
+                                                       (long long)oyc * p.bg_rs + (long long)oxc * p.bg_ps + p.bg_co + nchc)
+                     : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        if (!ok[u]) continue;
+        const unsigned wt[4] = {tv[u].x, tv[u].y, tv[u].z, tv[u].w};
+        const unsigned wx[4] = {xr[u].x, xr[u].y, xr[u].z, xr[u].w};
+        const unsigned wg[4] = {gr[u].x, gr[u].y, gr[u].z, gr[u].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = __uint_as_float((e & 1) ? (wt[e >> 1] & 0xffff0000u) : (wt[e >> 1] << 16));
+          const float xv = __uint_as_float((e & 1) ? (wx[e >> 1] & 0xffff0000u) : (wx[e >> 1] << 16));
+          const float gv = __uint_as_float((e & 1) ? (wg[e >> 1] & 0xffff0000u) : (wg[e >> 1] << 16));
+          const float nn = fmaf(xv, p.bsc[nch + e], p.bsh[nch + e]);
+          const float dn = v * (nn > 0.f ? 1.f : p.bs_self) + gv * (nn > 0.f ? 1.f : p.bs_other);
+          sa[e] += dn;
+          sb[e] += dn * (xv - p.bmu[nch + e]) * p.brs[nch + e];
+        }
       }
     }
     // per-tile reduction over the threads sharing a channel chunk (fixed order)
