@@ -326,34 +326,47 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, PixDiv pd, lo
   const int CG = C / N;
   const long long total = P * CG;
   const float invP = 1.f / (float)P;
+  // per-channel coefficients of this thread's channel group, reloaded only when the group changes
+  // (never, when the grid stride is a multiple of CG -- the usual power-of-two channel counts):
+  // n = v*sc + sh;  dx = k1*dn - k0 - k2*v   with k1 = gamma*rstd, k2 = k1*rstd*dgamma/P,
+  // k0 = k1*(dbeta/P - mean*rstd*dgamma/P)
+  int cg_have = -1;
+  float sc[N], sh[N], k0[N], k1[N], k2[N];
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
     const int cg = (int)(idx % CG);
     const long long pix = idx / CG;
-    int b, yy, xx;
-    pix_bxy(pd, pix, b, yy, xx);
     const int c = N * cg;
-    float v[N], n[N], d[N];
-    VW<T>::load(vptr<T>(x, b, yy, xx, c), v);
-    if (scale) {
-      float sc[N], shf[N];
-      ldc<N>(scale + c, sc); ldc<N>(shift + c, shf);
+    if (cg != cg_have) {
+      cg_have = cg;
+      if (scale) { ldc<N>(scale + c, sc); ldc<N>(shift + c, sh); }
+      else {
 #pragma unroll
-      for (int e = 0; e < N; ++e) n[e] = fmaf(v[e], sc[e], shf[e]);
-    } else {
+        for (int e = 0; e < N; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+      }
+      if (mean) {
+        float mu[N], rs[N], gm[N], dg[N], db[N];
+        ldc<N>(mean + c, mu); ldc<N>(rstd + c, rs); ldc<N>(gamma + c, gm); ldc<N>(dgamma + c, dg); ldc<N>(dbeta + c, db);
 #pragma unroll
-      for (int e = 0; e < N; ++e) n[e] = v[e];
-    }
-    dn_of<T>(gi, b, yy, xx, c, n, d);
-    if (mean) {
-      float mu[N], rs[N], gm[N], dg[N], db[N];
-      ldc<N>(mean + c, mu); ldc<N>(rstd + c, rs); ldc<N>(gamma + c, gm); ldc<N>(dgamma + c, dg); ldc<N>(dbeta + c, db);
+        for (int e = 0; e < N; ++e) {
+          k1[e] = gm[e] * rs[e];
+          k2[e] = k1[e] * rs[e] * dg[e] * invP;
+          k0[e] = k1[e] * (db[e] * invP - mu[e] * rs[e] * dg[e] * invP);
+        }
+      } else {
 #pragma unroll
-      for (int e = 0; e < N; ++e) {
-        const float xh = (v[e] - mu[e]) * rs[e];
-        d[e] = gm[e] * rs[e] * (d[e] - db[e] * invP - xh * dg[e] * invP);
+        for (int e = 0; e < N; ++e) { k1[e] = 1.f; k2[e] = 0.f; k0[e] = 0.f; }
       }
     }
+    int b, yy, xx;
+    pix_bxy(pd, pix, b, yy, xx);
+    float v[N], n[N], d[N];
+    VW<T>::load(vptr<T>(x, b, yy, xx, c), v);
+#pragma unroll
+    for (int e = 0; e < N; ++e) n[e] = fmaf(v[e], sc[e], sh[e]);
+    dn_of<T>(gi, b, yy, xx, c, n, d);
+#pragma unroll
+    for (int e = 0; e < N; ++e) d[e] = fmaf(k1[e], d[e], -fmaf(k2[e], v[e], k0[e]));
     VW<T>::store(reinterpret_cast<T*>(dx.p) + vidx(dx, b, yy, xx, c), d);
   }
 }
@@ -370,21 +383,27 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(View x, PixDiv pd, long l
   constexpr int N = VW<T>::N;
   const int CG = C / N;
   const long long total = P * CG;
+  int cg_have = -1;
+  float sc[N], sh[N];
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
     const int cg = (int)(idx % CG);
     const long long pix = idx / CG;
+    const int c = N * cg;
+    if (cg != cg_have) {  // this thread's channel group's table, reloaded only when it changes
+      cg_have = cg;
+      if (scale) { ldc<N>(scale + c, sc); ldc<N>(shift + c, sh); }
+      else {
+#pragma unroll
+        for (int e = 0; e < N; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+      }
+    }
     int b, yy, xx;
     pix_bxy(pd, pix, b, yy, xx);
-    const int c = N * cg;
     float v[N], o[N];
     VW<T>::load(vptr<T>(x, b, yy, xx, c), v);
-    if (scale) {
-      float sc[N], sh[N];
-      ldc<N>(scale + c, sc); ldc<N>(shift + c, sh);
 #pragma unroll
-      for (int e = 0; e < N; ++e) v[e] = fmaf(v[e], sc[e], sh[e]);
-    }
+    for (int e = 0; e < N; ++e) v[e] = fmaf(v[e], sc[e], sh[e]);
 #pragma unroll
     for (int e = 0; e < N; ++e) o[e] = act(v[e], s1);
     VW<T>::store(reinterpret_cast<T*>(y1.p) + vidx(y1, b, yy, xx, c), o);

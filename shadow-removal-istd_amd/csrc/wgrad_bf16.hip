@@ -93,15 +93,20 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
+  // XCD-aware order over (split, tile): workgroups go round-robin to the 8 XCDs by linear id, so
+  // remap the linear id to give every XCD a contiguous run of (split-major) work -- the tiles of one
+  // pixel split then share their D / G rows in that XCD's L2 instead of every XCD streaming all splits.
   const int nwg = p.mtiles * p.ntiles;
-  int bid = blockIdx.x;
+  const int nlin = nwg * (int)gridDim.z;
+  int bid = blockIdx.x + (int)blockIdx.z * nwg;
   {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int xcd = bid & 7, q = nlin >> 3, r = nlin & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
+  const int split = bid / nwg;
+  bid -= split * nwg;
   const int mt = bid / p.ntiles, nt = bid % p.ntiles;
   const int a0 = mt * BM, b0 = nt * BN;  // first row / column of the tile
-  const int split = blockIdx.z;
   const int pbeg = split * p.pchunk;
   const int pend = min(p.P, pbeg + p.pchunk);
   const int nsteps = (pend - pbeg + WB_BK - 1) / WB_BK;
@@ -332,7 +337,6 @@ static WbPlan wb_plan(int P, int R, int Cg) {
     if (R <= 16) cfg = 2;
     else if (R <= 64) cfg = 1;
     else if (ncol >= 1024 && ((R >= 512 && P >= 16384) || (R >= 256 && P >= 65536))) cfg = 3;
-    else if (R <= 128 && ncol >= 1024 && P >= 65536) cfg = 5;
     else cfg = 0;
   }
   const WbCfg& c = kWbCfg[cfg];
