@@ -652,6 +652,10 @@ static const TileCfg kTiles[] = {
     {128, 128, 2, 2, 4, 32},  // 17
     {128, 64, 2, 2, 4, 32},   // 18
     {64, 64, 2, 2, 4, 32},    // 19
+    {128, 128, 2, 2, 3, 32},  // 20: 48 KiB -> 3 blocks/CU
+    {128, 128, 2, 2, 2, 32},  // 21
+    {256, 128, 4, 2, 3, 32},  // 22
+    {128, 64, 2, 2, 3, 32},   // 23
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -684,6 +688,8 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
       if (no == 0) no = 4;
     } else if (N >= 128) {
       order[0] = 0; order[1] = 4; order[2] = 5; no = 3;
+    } else if (K <= 128) {  // first layers (Cin = 8): 3-stage BK = 32, 3-4 blocks per CU
+      order[0] = 23; order[1] = 2; order[2] = 5; no = 3;
     } else if (K <= 512) {
       order[0] = 2; order[1] = 5; no = 2;
     } else {
@@ -817,6 +823,10 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     STC_B(17, 128, 128, 2, 2, 4, 32)
     STC_B(18, 128, 64, 2, 2, 4, 32)
     STC_B(19, 64, 64, 2, 2, 4, 32)
+    STC_B(20, 128, 128, 2, 2, 3, 32)
+    STC_B(21, 128, 128, 2, 2, 2, 32)
+    STC_B(22, 256, 128, 4, 2, 3, 32)
+    STC_B(23, 128, 64, 2, 2, 3, 32)
     default:
       return fail(-1, "bf16 igemm: bad tile config %d", pl.cfg);
   }
