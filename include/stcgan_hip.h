@@ -22,6 +22,8 @@
  *   stc_gather_nchw / stc_scatter_nchw              torch.cat input concat (stcgan.py:219-227,269-272) / its backward
  *   stc_loss_fwd / stc_loss_bwd                     DataLoss (L1) and AdversarialLoss (MSE / BCE-with-logits), loss.py:14-26,59-86
  *   stc_adam_step    torch.optim.Adam                STCGAN/stcgan.py:60-65
+ *   stc_infer_output infer() output stage: x*0.5+0.5, cv.resize INTER_LINEAR, float2uint
+ *                    (STCGAN/stcgan.py:355-377, STCGAN/utils.py:63-65)
  *
  * Conventions
  *   - Activations are NHWC ("view" = base pointer + explicit strides, so a
@@ -235,6 +237,14 @@ int stc_loss_fwd(int kind, const float* p, const float* t, float c, int64_t n,
                  float* part, float* out, void* stream);
 int stc_loss_bwd(int kind, const float* p, const float* t, float c, int64_t n,
                  const float* gout, float* grad, void* stream);
+
+/* ---- inference output stage ---------------------------------------------------
+ * src: generator output NCHW fp32 [B][C][H][W] (tanh range); dst: HWC uint8 [B][OH][OW][C],
+ * dst = uint8(trunc(255 * resize_linear(src * 0.5 + 0.5))) with OpenCV's float32 INTER_LINEAR
+ * geometry (exact 2x2 downscale: INTER_AREA block mean, as cv::resize does).  C in 1..4.
+ * Replaces the per-image numpy / cv.resize / float2uint loop of STCGAN.infer (stcgan.py:355-377). */
+int stc_infer_output(const float* src, int B, int C, int H, int W, int OH, int OW, unsigned char* dst,
+                     void* stream);
 
 /* ---- optimizer --------------------------------------------------------------------
  * One launch over many tensors.  table: device array of ntensors records

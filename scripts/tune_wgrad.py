@@ -19,7 +19,11 @@ from stcgan_amd.stcgan import STCGAN  # noqa: E402
 
 BF = torch.bfloat16
 CFGS = range(6)
-SPLITS = (0, 1, 2, 4, 8, 16, 32, 64)
+SPLITS = tuple(int(v) for v in os.environ.get("WG_SPLITS", "0,1,2,4,8,16,32,64").split(","))
+MIN_P = int(os.environ.get("WG_MIN_P", "0"))
+WG_CFGS = os.environ.get("WG_CFGS")
+if WG_CFGS:
+    CFGS = tuple(int(v) for v in WG_CFGS.split(","))
 
 
 def record():
@@ -101,6 +105,8 @@ def main():
     tot_auto = tot_best = 0.0
     for prob, count in sorted(probs.items(), key=lambda kv: -kv[0][0] * kv[0][2] * kv[0][3] * kv[0][6] * kv[0][7]):
         B, s, dh, dw, gh, gw, R, Cg, Cg_out = prob
+        if B * dh * dw < MIN_P:
+            continue
         flops = 2.0 * B * dh * dw * R * 16 * Cg
         t_auto = bench(prob, (-1, 0))
         res = {}

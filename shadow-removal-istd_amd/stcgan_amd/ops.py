@@ -394,3 +394,16 @@ def scatter(src_nhwc, dsts, chans, dt, H=None, W=None):
     cs = (ctypes.c_int * n)(*chans)
     check(lib().stc_scatter_nchw(L.dtype_code(dt), B, H, W, L.nhwc_view(src_nhwc, 0, H, W), n, arr, cs, stream()),
           "stc_scatter_nchw")
+
+
+def infer_output(net_out, oh=192, ow=256):
+    """STCGAN.infer output stage on the GPU (stc_infer_output): generator output [B, C, H, W] fp32
+    (tanh range) -> uint8 [B, oh, ow, C] = float2uint(cv.resize(x*0.5+0.5, (ow, oh), INTER_LINEAR)),
+    the arrays the reference hands to cv.imwrite (STCGAN/stcgan.py:355-377, utils.py:63-65)."""
+    if not net_out.is_cuda:
+        raise RuntimeError("stcgan_amd.infer_output: CUDA (HIP) tensors only")
+    x = net_out.detach().float().contiguous()
+    B, C, H, W = x.shape
+    out = torch.empty((B, oh, ow, C), dtype=torch.uint8, device=x.device)
+    check(lib().stc_infer_output(ptr(x), B, C, H, W, oh, ow, ptr(out), stream()), "stc_infer_output")
+    return out

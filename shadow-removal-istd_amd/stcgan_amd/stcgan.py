@@ -239,10 +239,15 @@ class STCGAN(object):
         return {"Loss": loss, "D1_out": D1_out, "D2_out": D2_out}
 
     # ------------------------------------------------------------------ inference
-    def infer(self):
-        """G1 -> G2 in eval mode over the validation loader (STCGAN/stcgan.py:332-381).
-        Writes ``{infered}/mask/<name>.npy`` and ``{infered}/shadowless/<name>.npy`` (values in [0,1],
-        the reference's ``x*0.5+0.5``); returns the list of (name, mask, shadowless) arrays."""
+    def infer(self, out_size=(256, 192)):
+        """G1 -> G2 in eval mode over the validation loader (STCGAN/stcgan.py:332-381), with the
+        reference's output stage on the GPU (ops.infer_output: x*0.5+0.5, cv.resize to
+        ``out_size`` = (width, height) INTER_LINEAR, float2uint truncation).  Writes
+        ``{infered}/mask/<name>.png`` and ``{infered}/shadowless/<name>.png`` (the uint8 arrays
+        cv.imwrite receives: mask single-channel, shadowless in the loader's BGR channel order);
+        returns the list of (name, mask uint8 [h, w], shadowless uint8 [h, w, 3])."""
+        from . import ops
+        ow, oh = out_size
         results = []
         with torch.no_grad():
             self.G1.eval()
@@ -251,17 +256,15 @@ class STCGAN(object):
                 x = x.to(self.device, non_blocking=True)
                 m_pred = self.G1(x)
                 y_pred = self.G2([x, m_pred])
-                m_np = m_pred.cpu().numpy() * 0.5 + 0.5
-                y_np = y_pred.cpu().numpy() * 0.5 + 0.5
+                m_u8 = ops.infer_output(m_pred, oh, ow).cpu().numpy()
+                y_u8 = ops.infer_output(y_pred, oh, ow).cpu().numpy()
                 for i, name in enumerate(filenames):
-                    mk = m_np[i].transpose(1, 2, 0)
-                    sl = y_np[i].transpose(1, 2, 0)
+                    mk = m_u8[i, :, :, 0]
+                    sl = y_u8[i]
                     results.append((name, mk, sl))
                     if self.inferd_dir:
-                        os.makedirs(os.path.join(self.inferd_dir, "mask"), exist_ok=True)
-                        os.makedirs(os.path.join(self.inferd_dir, "shadowless"), exist_ok=True)
-                        np.save(os.path.join(self.inferd_dir, "mask", name + ".npy"), mk)
-                        np.save(os.path.join(self.inferd_dir, "shadowless", name + ".npy"), sl)
+                        _write_png(os.path.join(self.inferd_dir, "mask", name + ".png"), mk)
+                        _write_png(os.path.join(self.inferd_dir, "shadowless", name + ".png"), sl)
         return results
 
     # ------------------------------------------------------------------ checkpoints
@@ -286,3 +289,12 @@ class STCGAN(object):
                 self.logger.info(f"Loaded {name} weights: {path}")
             else:
                 net.apply(networks.weights_init)
+
+
+def _write_png(path, img):
+    """cv.imwrite(path, img) for a uint8 HxW or HxWx3 (BGR) array, through PIL (cv2 is not a
+    dependency): the PNG holds the same pixel values cv.imwrite would store."""
+    from PIL import Image
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    arr = np.ascontiguousarray(img[:, :, ::-1]) if img.ndim == 3 else img
+    Image.fromarray(arr).save(path)
