@@ -107,6 +107,21 @@ __device__ __forceinline__ int kswz(int row) {
   else return (row >> 1) & 3;
 }
 
+// s_waitcnt that leaves the DMA pieces of the `ahead` youngest K-steps (P per step per wave) in
+// flight: vmcnt takes an immediate, so one arm per ring depth (ahead <= NST - 2 <= 6).
+template <int P>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+  switch (ahead) {
+    case 6: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(6 * P) : "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(5 * P) : "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * P) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(3 * P) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * P) : "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(P) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB>
 __global__ void __launch_bounds__(64 * WM * WN)
 igemm_bf16_kernel(const GParams p) {
@@ -121,7 +136,7 @@ igemm_bf16_kernel(const GParams p) {
   constexpr int KK = BK / 32;            // 16x16x32 MFMA sub-steps per K-step
   static_assert(AG * RPP * NW == BM && BG * RPP * NW == BN, "tile rows must split into whole pieces per wave");
   static_assert(FM >= 1 && FN >= 1, "wave tile >= 16x16");
-  static_assert(NST >= 2 && NST <= 4, "2..4-stage ring");
+  static_assert(NST >= 2 && NST <= 8, "2..8-stage ring (wait_ahead covers up to 6 steps ahead)");
   static_assert(BK == 64 || BK == 32, "BK");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -264,9 +279,7 @@ igemm_bf16_kernel(const GParams p) {
     int cur = 0;
     for (int s = 0; s < nsteps; ++s) {
       const int ahead = min(NST - 2, nsteps - 1 - s);  // steps already issued beyond s
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * P) : "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(P) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      wait_ahead<P>(ahead);
       __builtin_amdgcn_s_barrier();
       if (s + NST - 1 < nsteps) issue(cur == 0 ? NST - 1 : cur - 1);
       compute(cur);
@@ -530,7 +543,24 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
     const float* src = p.ws + ((long long)ph * p.ksplit * p.M + m) * p.N + n;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = bz[e];
-    for (int s = 0; s < p.ksplit; ++s) {
+    // slabs in groups of 4: the 8 loads of a group are in flight together (one memory latency
+    // per group, not per slab -- the deep layers run 8-64 slabs over a handful of rows); the sum
+    // order stays s = 0, 1, 2, ... per element
+    int s = 0;
+    for (; s + 4 <= p.ksplit; s += 4) {
+      float4 a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = *reinterpret_cast<const float4*>(src + (s + u) * MN);
+        b[u] = *reinterpret_cast<const float4*>(src + (s + u) * MN + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[0] += a[u].x; v[1] += a[u].y; v[2] += a[u].z; v[3] += a[u].w;
+        v[4] += b[u].x; v[5] += b[u].y; v[6] += b[u].z; v[7] += b[u].w;
+      }
+    }
+    for (; s < p.ksplit; ++s) {
       const float4 a = *reinterpret_cast<const float4*>(src + s * MN);
       const float4 b = *reinterpret_cast<const float4*>(src + s * MN + 4);
       v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
