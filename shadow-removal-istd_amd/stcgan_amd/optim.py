@@ -2,8 +2,8 @@
 
 Same constructor and ``step()/zero_grad()/state_dict()`` surface as
 torch.optim.Adam for the options the reference uses (lr, betas, eps;
-weight_decay=0, amsgrad=False).  The per-step pointer table is built on the
-host and copied with a non-blocking H2D copy, so ``step()`` never synchronises.
+weight_decay=0, amsgrad=False).  The pointer table lives on the device and is
+rebuilt only when a tensor moved; ``step()`` never synchronises.
 """
 import torch
 
@@ -26,10 +26,14 @@ class Adam(torch.optim.Optimizer):
                 loss = closure()
         if self._epb is None:
             self._epb = lib().stc_adam_elems_per_block()
-        for group in self.param_groups:
+            self._steps = {}    # id(param) -> (state step tensor, its value as a Python int)
+            self._tables = {}   # (group, step) -> (pointer key, device table, blocks)
+        for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
-            # group params by step count (all equal in practice)
-            by_step = {}
+            # group params by step count (all equal in practice).  The step count is mirrored in a
+            # Python int (no per-parameter tensor op / .item() on the host path), and the state's
+            # "step" tensors are advanced with one foreach call.
+            by_step, step_tensors = {}, []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -42,22 +46,29 @@ class Adam(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                by_step.setdefault(int(st["step"].item()), []).append(p)
+                mirror = self._steps.get(id(p))
+                n = mirror[1] + 1 if mirror is not None and mirror[0] is st["step"] else int(st["step"].item()) + 1
+                self._steps[id(p)] = (st["step"], n)
+                step_tensors.append(st["step"])
+                by_step.setdefault(n, []).append(p)
+            if step_tensors:
+                torch._foreach_add_(step_tensors, 1.0)
             for step, plist in by_step.items():
-                rows, blocks = [], 0
-                for p in plist:
-                    st = self.state[p]
-                    n = p.numel()
-                    rows.append([p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
-                                 st["exp_avg_sq"].data_ptr(), n, blocks])
-                    blocks += (n + self._epb - 1) // self._epb
-                table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(plist[0].device, non_blocking=True)
-                check(lib().stc_adam_step(ptr(table), len(rows), blocks, float(group["lr"]), float(b1), float(b2),
+                key = tuple((p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
+                             self.state[p]["exp_avg_sq"].data_ptr(), p.numel()) for p in plist)
+                cached = self._tables.get(gi)
+                if cached is not None and cached[0] == key:
+                    table, blocks = cached[1], cached[2]
+                else:
+                    # pointer table, rebuilt only when a tensor moved (the caching allocator hands the
+                    # gradients the same blocks step after step); the device copy is stream-ordered
+                    rows, blocks = [], 0
+                    for (pp, gp, mp, vp, n) in key:
+                        rows.append([pp, gp, mp, vp, n, blocks])
+                        blocks += (n + self._epb - 1) // self._epb
+                    table = torch.tensor(rows, dtype=torch.int64).to(plist[0].device)
+                    self._tables[gi] = (key, table, blocks)
+                check(lib().stc_adam_step(ptr(table), len(key), blocks, float(group["lr"]), float(b1), float(b2),
                                           float(group["eps"]), int(step), stream()), "stc_adam_step")
                 ops.bump(plist)
-                # keep every tensor the kernel reads alive until it ran on the stream
-                for p in plist:
-                    p.grad.record_stream(torch.cuda.current_stream())
-                table.record_stream(torch.cuda.current_stream())
         return loss
