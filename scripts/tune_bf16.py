@@ -112,6 +112,8 @@ def main():
     tot_auto = tot_best = 0.0
     for prob, (count, _) in sorted(probs.items(), key=lambda kv: -kv[0][1] * kv[0][2] * kv[0][3] * kv[0][8] * kv[0][9]):
         kind, B, gh, gw, xh, xw, yh, yw, cin, cout = prob
+        if os.environ.get("TUNE_COUT") and cout != int(os.environ["TUNE_COUT"]):
+            continue
         ws, nch, plan = ops.conv_query(kind, B, gh, gw, cin, cout, BF)
         if plan[4] < 0:
             continue

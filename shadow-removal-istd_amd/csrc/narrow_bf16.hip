@@ -125,6 +125,16 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
   if (cbeg < cend) issue(cbeg, 0);
   int stage = 0;
   for (int ch = cbeg; ch < cend; ++ch) {
+    // this chunk's B fragments go to registers BEFORE the next chunk's DMA is issued: vmcnt
+    // retires in issue order, so a weight load issued behind that DMA would make the MFMAs of
+    // this chunk wait for the next chunk's pixels (no DMA / compute overlap at all)
+    bf16x8_h bfr[2][NBR][NB];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nb = 0; nb < NBR; ++nb)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) bfr[kk][nb][j] = load_b(ch, nb, j, kk);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (ch + 1 < cend) issue(ch + 1, stage ^ 1);
@@ -136,16 +146,14 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
       for (int nb = 0; nb < NBR; ++nb) {
         const int dy = GEOM == 0 ? nb / 3 - 1 : nb / 4 - 1;
         const int dx = GEOM == 0 ? nb % 3 - 1 : nb % 4 - 1;
-        bf16x8_h bfr[NB];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) bfr[j] = load_b(ch, nb, j, kk);
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
           const int py = wave * ROWS + r + dy + 1, px = gx + dx + 1;
           const int pix = py * RX + px;
           const bf16x8_h af = *reinterpret_cast<const bf16x8_h*>(sT + pix * 128 + ((cslot ^ (pix & 7)) * 16));
 #pragma unroll
-          for (int j = 0; j < NB; ++j) acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[r][j], 0, 0, 0);
+          for (int j = 0; j < NB; ++j)
+            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[kk][nb][j], acc[r][j], 0, 0, 0);
         }
       }
     }
@@ -218,7 +226,7 @@ static size_t halo_lds(int geom, int ty) {
 
 // Narrow plan: {ty, nsplit}.  Enough blocks to cover the chip ~2x.
 static void narrow_plan(int geom, int B, int GH, int GW, int cin, int* ty, int* nsplit) {
-  *ty = 8;
+  *ty = 8;  // (TY = 16: fewer, larger halo tiles -- measured slower, occupancy-bound)
   const int nchunks = cin / 64;
   const long long blocks = (long long)B * cdiv(GH, *ty) * cdiv(GW, 16);
   int ns = 1;
