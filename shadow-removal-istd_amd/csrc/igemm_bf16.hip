@@ -720,8 +720,8 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
       order[0] = 0; order[1] = 4; order[2] = 5; no = 3;
     } else if (K <= 128) {  // first layers (Cin = 8): 3-stage BK = 32, 3-4 blocks per CU
       order[0] = 23; order[1] = 2; order[2] = 5; no = 3;
-    } else if (K <= 512) {
-      order[0] = 2; order[1] = 5; no = 2;
+    } else if (K <= 512) {  // (Cin = 128 ConvT-geometry dgrads: the 3-stage BK = 32 128x64 tile, -9 %)
+      order[0] = 23; order[1] = 2; order[2] = 5; no = 3;
     } else {
       order[0] = 5; order[1] = 2; no = 2;
     }
