@@ -165,24 +165,42 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int
                                                           float* mean_o, float* rstd_o, float* scale, float* shift) {
   const int c = blockIdx.x;
   __shared__ double sh[256];
+  // chunk partials are read in groups of 4 per thread (the 4 loads in flight together: one
+  // memory latency per group -- the first layers merge up to 4096 chunks per channel)
+  auto load4 = [&](int k0, float4* pp) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * 256;
+      pp[u] = k < nchunks ? *reinterpret_cast<const float4*>(part + ((long long)k * C + c) * 4)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
   double n = 0, sm = 0;
-  for (int k = threadIdx.x; k < nchunks; k += 256) {
-    const float4 pp = *reinterpret_cast<const float4*>(part + ((long long)k * C + c) * 4);
-    if (pp.x <= 0.f) continue;
-    n += pp.x;
-    sm += (double)pp.x * pp.w + (double)pp.y;  // n_b * m_b = n_b*shift + S1
+  for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {
+    float4 pp[4];
+    load4(k0, pp);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (pp[u].x <= 0.f) continue;
+      n += pp[u].x;
+      sm += (double)pp[u].x * pp[u].w + (double)pp[u].y;  // n_b * m_b = n_b*shift + S1
+    }
   }
   const double N = block_sum256(n, sh);
   const double mu = N > 0 ? block_sum256(sm, sh) / N : (block_sum256(sm, sh), 0.0);
   double m2 = 0;
-  for (int k = threadIdx.x; k < nchunks; k += 256) {
-    const float4 pp = *reinterpret_cast<const float4*>(part + ((long long)k * C + c) * 4);
-    if (pp.x <= 0.f) continue;
-    const double nb = pp.x, s1 = pp.y, r = s1 / nb;
-    double q = (double)pp.z - s1 * r;
-    if (q < 0) q = 0;
-    const double d = (double)pp.w + r - mu;
-    m2 += q + nb * d * d;
+  for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {
+    float4 pp[4];
+    load4(k0, pp);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (pp[u].x <= 0.f) continue;
+      const double nb = pp[u].x, s1 = pp[u].y, r = s1 / nb;
+      double q = (double)pp[u].z - s1 * r;
+      if (q < 0) q = 0;
+      const double d = (double)pp[u].w + r - mu;
+      m2 += q + nb * d * d;
+    }
   }
   const double M2 = block_sum256(m2, sh);
   if (threadIdx.x == 0) {
@@ -304,10 +322,18 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* part,
   const int c = blockIdx.x;
   __shared__ double sh[256];
   double a = 0, b = 0;
-  for (int k = threadIdx.x; k < nchunks; k += 256) {
-    const float2 pp = *reinterpret_cast<const float2*>(part + ((long long)k * C + c) * 2);
-    a += pp.x;
-    b += pp.y;
+  for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {  // groups of 4 loads in flight
+    float2 pp[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * 256;
+      pp[u] = k < nchunks ? *reinterpret_cast<const float2*>(part + ((long long)k * C + c) * 2) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a += pp[u].x;
+      b += pp[u].y;
+    }
   }
   const double ta = block_sum256(a, sh);
   const double tb = block_sum256(b, sh);
