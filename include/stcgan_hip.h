@@ -24,6 +24,8 @@
  *   stc_adam_step    torch.optim.Adam                STCGAN/stcgan.py:60-65
  *   stc_infer_output infer() output stage: x*0.5+0.5, cv.resize INTER_LINEAR, float2uint
  *                    (STCGAN/stcgan.py:355-377, STCGAN/utils.py:63-65)
+ *   stc_istd_errors  ISTD evaluation: masked LAB RMSE/MAE sums + PSNR squared error (src/eval.py:41-139)
+ *   stc_istd_ssim    ISTD evaluation: SSIM (src/eval.py:137-139)
  *
  * Conventions
  *   - Activations are NHWC ("view" = base pointer + explicit strides, so a
@@ -245,6 +247,21 @@ int stc_loss_bwd(int kind, const float* p, const float* t, float c, int64_t n,
  * Replaces the per-image numpy / cv.resize / float2uint loop of STCGAN.infer (stcgan.py:355-377). */
 int stc_infer_output(const float* src, int B, int C, int H, int W, int OH, int OW, unsigned char* dst,
                      void* stream);
+
+/* ---- ISTD evaluation errors ----------------------------------------------------
+ * img1, img2: uint8 RGB [B][H][W][3] (skimage.io.imread order); mask: uint8 [B][H][W] or NULL
+ * (shadow = mask/255 >= 0.5; NULL = every pixel is "shadow", eval.py's no-maskdir case).
+ * out: fp64 [B][7] = {sum |dLab|_2, sum |dLab|_1, count} over shadow pixels, the same over
+ * non-shadow pixels, and sum (v1 - v2)^2 over all pixels and channels (v = u/255), with
+ * Lab = skimage.color.rgb2lab (D65, 2 degrees).  ws: >= stc_istd_errors_workspace(B, H, W) bytes. */
+int64_t stc_istd_errors_workspace(int B, int H, int W);
+int stc_istd_errors(const unsigned char* img1, const unsigned char* img2, const unsigned char* mask, int B, int H,
+                    int W, double* out, void* ws, int64_t ws_bytes, void* stream);
+/* SSIM of each RGB pair as skimage 0.17 structural_similarity(X, Y, multichannel=True) computes it
+ * on float32 images (7x7 uniform window, sample covariance, data_range 2): out fp64 [B].
+ * H, W >= 7; ws as for stc_istd_errors (same workspace size query).                          */
+int stc_istd_ssim(const unsigned char* img1, const unsigned char* img2, int B, int H, int W, double* out, void* ws,
+                  int64_t ws_bytes, void* stream);
 
 /* ---- optimizer --------------------------------------------------------------------
  * One launch over many tensors.  table: device array of ntensors records
