@@ -99,3 +99,36 @@ class AdversarialLoss(nn.Module):
         if not self.ls:
             return mse_const(D_out, target)
         return bce_logits_const(D_out, target)
+
+
+class RelativisticAdversarialLoss(nn.Module):
+    """The ``src/`` line's AdversarialLoss (src/loss.py:59-112): SGAN / RpGAN (rel) / RaGAN
+    (rel + avg) objectives over a (C_real, C_fake) pair, for the discriminator (``D_loss=True``)
+    or the generator; labels real=1, fake=0 (MSE) or 1 / -1 with ``ls=True`` (BCE-with-logits),
+    as the reference.  The reductions and their gradients run in the HIP loss kernels; the
+    relativistic differences (C_real - C_fake, C - mean over dim 0) are torch ops on the
+    [B, 1, 30, 30] logits."""
+
+    def __init__(self, ls=False, rel=False, avg=False):
+        super().__init__()
+        self.register_buffer('real_label', torch.tensor(1.0))
+        self.register_buffer('fake_label', torch.tensor(-1.0 if ls else 0.0))
+        self.ls, self.rel, self.avg = ls, rel, avg
+        self._labels = (1.0, -1.0 if ls else 0.0)
+
+    def cal_loss(self, C_out, label):
+        return bce_logits_const(C_out, label) if self.ls else mse_const(C_out, label)
+
+    def forward(self, C_real, C_fake, D_loss=True):
+        real, fake = self._labels
+        if self.rel and self.avg:  # RaGAN
+            if D_loss:
+                return (self.cal_loss(C_real - C_fake.mean(dim=0), real)
+                        + self.cal_loss(C_fake - C_real.mean(dim=0), fake)) * 0.5
+            return (self.cal_loss(C_real - C_fake.mean(dim=0), fake)
+                    + self.cal_loss(C_fake - C_real.mean(dim=0), real)) * 0.5
+        if self.rel:  # RpGAN
+            return self.cal_loss(C_real - C_fake, real) if D_loss else self.cal_loss(C_fake - C_real, real)
+        if D_loss:  # SGAN
+            return (self.cal_loss(C_real, real) + self.cal_loss(C_fake, fake)) * 0.5
+        return self.cal_loss(C_fake, real)

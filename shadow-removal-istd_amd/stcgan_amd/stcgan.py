@@ -280,6 +280,29 @@ class STCGAN(object):
             module = module.module if isinstance(module, nn.DataParallel) else module
             torch.save(module.state_dict(), os.path.join(weights, f"{name}-{suffix}.pt"))
 
+    def save_checkpoint(self, epoch, path="./checkpoint.tar"):
+        """Full training state (src/cgan.py:494-511): epoch, the four state_dicts, both
+        optimisers (Adam moments + step counts) and both LR schedulers; rank 0 only."""
+        if parallel.rank() != 0:
+            return
+        mod = {k: (getattr(self, k).module if isinstance(getattr(self, k), nn.DataParallel) else getattr(self, k))
+               for k in ("G1", "G2", "D1", "D2")}
+        torch.save({"epoch": epoch, **{k: m.state_dict() for k, m in mod.items()},
+                    "optim_G": self.optim_G.state_dict(), "optim_D": self.optim_D.state_dict(),
+                    "decay_G": self.decay_G.state_dict(), "decay_D": self.decay_D.state_dict()}, path)
+
+    def load_checkpoint(self, path="./checkpoint.tar"):
+        """Resume from save_checkpoint (src/cgan.py:513-523; restores decay_G as well -- the
+        reference loads decay_D twice)."""
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.start_epoch = ck["epoch"]
+        for k in ("G1", "G2", "D1", "D2"):
+            getattr(self, k).load_state_dict(ck[k])
+        self.optim_G.load_state_dict(ck["optim_G"])
+        self.optim_D.load_state_dict(ck["optim_D"])
+        self.decay_G.load_state_dict(ck["decay_G"])
+        self.decay_D.load_state_dict(ck["decay_D"])
+
     def init_weight(self, g1_weights=None, g2_weights=None, d1_weights=None, d2_weights=None):
         for name, path in (("G1", g1_weights), ("G2", g2_weights), ("D1", d1_weights), ("D2", d2_weights)):
             net = getattr(self, name)
