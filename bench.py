@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--dtype", default=os.environ.get("STC_BENCH_DTYPE", "bf16"), choices=["fp32", "bf16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=4)
-    ap.add_argument("--cpu-iters", type=int, default=2)
+    ap.add_argument("--cpu-iters", type=int, default=12)  # ~10 s of host work on the GPU box
     return ap.parse_args()
 
 
