@@ -26,6 +26,8 @@
  *                    (STCGAN/stcgan.py:355-377, STCGAN/utils.py:63-65)
  *   stc_istd_errors  ISTD evaluation: masked LAB RMSE/MAE sums + PSNR squared error (src/eval.py:41-139)
  *   stc_istd_ssim    ISTD evaluation: SSIM (src/eval.py:137-139)
+ *   stc_prepare_batch training batch: uint2float, (v-0.5)*2, RandomHorizontalFlip, RandomCrop (STCGAN/dataset.py:89-147,
+ *                    STCGAN/transform.py:103-156)
  *
  * Conventions
  *   - Activations are NHWC ("view" = base pointer + explicit strides, so a
@@ -262,6 +264,14 @@ int stc_istd_errors(const unsigned char* img1, const unsigned char* img2, const 
  * H, W >= 7; ws as for stc_istd_errors (same workspace size query).                          */
 int stc_istd_ssim(const unsigned char* img1, const unsigned char* img2, int B, int H, int W, double* out, void* ws,
                   int64_t ws_bytes, void* stream);
+
+/* ---- training-batch preparation ---------------------------------------------------
+ * src: uint8 [B][H][W][C] (decoded images, the loader's channel order); params: device int32
+ * [B][3] = {flip, row_offset, col_offset} drawn on the host in the reference's order; pad_h /
+ * pad_w: the zero border RandomCrop adds when the image is smaller than the crop.
+ * dst: fp32 NCHW [B][C][OH][OW] = crop(flip((u / 255 - 0.5) * 2)), border value 0.              */
+int stc_prepare_batch(const unsigned char* src, int B, int H, int W, int C, const int* params, int pad_h, int pad_w,
+                      int OH, int OW, float* dst, void* stream);
 
 /* ---- optimizer --------------------------------------------------------------------
  * One launch over many tensors.  table: device array of ntensors records
