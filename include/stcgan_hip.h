@@ -26,8 +26,8 @@
  *                    (STCGAN/stcgan.py:355-377, STCGAN/utils.py:63-65)
  *   stc_istd_errors  ISTD evaluation: masked LAB RMSE/MAE sums + PSNR squared error (src/eval.py:41-139)
  *   stc_istd_ssim    ISTD evaluation: SSIM (src/eval.py:137-139)
- *   stc_prepare_batch training batch: uint2float, (v-0.5)*2, RandomHorizontalFlip, RandomCrop (STCGAN/dataset.py:89-147,
- *                    STCGAN/transform.py:103-156)
+ *   stc_prepare_batch / stc_prepare_batch_f32 / stc_resize_area  training batch: uint2float, (v-0.5)*2,
+ *                    Resize (INTER_AREA), RandomHorizontalFlip, RandomCrop (STCGAN/dataset.py:89-147, transform.py:103-181)
  *
  * Conventions
  *   - Activations are NHWC ("view" = base pointer + explicit strides, so a
@@ -272,6 +272,12 @@ int stc_istd_ssim(const unsigned char* img1, const unsigned char* img2, int B, i
  * dst: fp32 NCHW [B][C][OH][OW] = crop(flip((u / 255 - 0.5) * 2)), border value 0.              */
 int stc_prepare_batch(const unsigned char* src, int B, int H, int W, int C, const int* params, int pad_h, int pad_w,
                       int OH, int OW, float* dst, void* stream);
+/* The same flip / crop on an already normalised fp32 NHWC source (the output of stc_resize_area). */
+int stc_prepare_batch_f32(const float* src, int B, int H, int W, int C, const int* params, int pad_h, int pad_w,
+                          int OH, int OW, float* dst, void* stream);
+/* Resize of transform.py:159-181 when the image shrinks in both dimensions: cv.resize INTER_AREA of
+ * the normalised image ((u / 255 - 0.5) * 2), uint8 [B][H][W][C] -> fp32 NHWC [B][OH][OW][C]. */
+int stc_resize_area(const unsigned char* src, int B, int H, int W, int C, int OH, int OW, float* dst, void* stream);
 
 /* ---- optimizer --------------------------------------------------------------------
  * One launch over many tensors.  table: device array of ntensors records

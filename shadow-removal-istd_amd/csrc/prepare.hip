@@ -8,17 +8,21 @@
 //                                       image when it is smaller than the crop, transform.py:119-156)
 // in one pass: one thread per output element, reading its source byte (HBM-bound: 1 B read +
 // 4 B written per element).  The random parameters are drawn on the host in the reference's
-// call order and passed per image as {flip, row_offset, col_offset}.  Resize / RandomScale /
-// RandomRotate (cv.resize / cv.warpAffine) are not restated.
+// call order and passed per image as {flip, row_offset, col_offset}.  Resize (shrink: INTER_AREA)
+// runs first when requested (resize_area_kernel); RandomScale / RandomRotate (cv.warpAffine) are
+// not restated.
+#include <cfloat>
+
 #include "common.hpp"
 
 #pragma clang fp contract(off)  // (u / 255 - 0.5) * 2 rounded step by step, as numpy does
 
 namespace stc {
 
-__global__ void __launch_bounds__(256) prepare_kernel(const unsigned char* __restrict__ src, int B, int H, int W,
-                                                      int C, const int* __restrict__ params, int pad_h, int pad_w,
-                                                      int OH, int OW, float* __restrict__ dst) {
+template <typename T>
+__global__ void __launch_bounds__(256) prepare_kernel(const T* __restrict__ src, int B, int H, int W, int C,
+                                                      const int* __restrict__ params, int pad_h, int pad_w, int OH,
+                                                      int OW, float* __restrict__ dst) {
   const long long total = (long long)B * C * OH * OW;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int x = (int)(i % OW);
@@ -32,10 +36,73 @@ __global__ void __launch_bounds__(256) prepare_kernel(const unsigned char* __res
     float v = 0.f;  // the constant border of the normalised image
     if (Y >= 0 && Y < H && X >= 0 && X < W) {
       const int sx = flip ? W - 1 - X : X;
-      const float u = (float)src[(((long long)b * H + Y) * W + sx) * C + c];
-      v = (u / 255.f - 0.5f) * 2.f;
+      const T u = src[(((long long)b * H + Y) * W + sx) * C + c];
+      if constexpr (sizeof(T) == 1) v = ((float)u / 255.f - 0.5f) * 2.f;
+      else v = u;
     }
     dst[i] = v;
+  }
+}
+
+// Resize (transform.py:159-181) on the normalised image when it shrinks in both dimensions:
+// cv.resize INTER_AREA.  Generic scale: OpenCV's computeResizeAreaTab cells (partial first /
+// whole / partial last source pixel, weights in double rounded to float) and ResizeArea_Invoker's
+// order -- per source row of the cell a horizontal float sum buf = sum_k S[sx_k] * alpha_k, then
+// sum = sum + beta * buf over the rows.  Integer scales in both axes: resizeAreaFast, the block sum
+// in row-major order times float(1 / area).  Source = uint8, normalised on the fly exactly as the
+// reference normalises before resizing ((u / 255 - 0.5) * 2 per pixel).
+__device__ __forceinline__ int area_cells(int d, double scale, int ssize, int* sx, float* al) {
+  const double fsx1 = d * scale, fsx2 = fsx1 + scale;
+  const double cellWidth = fmin(scale, ssize - fsx1);
+  int sx1 = (int)ceil(fsx1), sx2 = (int)floor(fsx2);
+  sx2 = min(sx2, ssize - 1);
+  sx1 = min(sx1, sx2);
+  int k = 0;
+  if (sx1 - fsx1 > 1e-3) { sx[k] = sx1 - 1; al[k++] = (float)((sx1 - fsx1) / cellWidth); }
+  for (int s = sx1; s < sx2; ++s) { sx[k] = s; al[k++] = (float)(1.0 / cellWidth); }
+  if (fsx2 - sx2 > 1e-3) { sx[k] = sx2; al[k++] = (float)(fmin(fmin(fsx2 - sx2, 1.0), cellWidth) / cellWidth); }
+  return k;
+}
+
+constexpr int AREA_MAXK = 18;  // source pixels per cell (scale <= 16)
+
+__global__ void __launch_bounds__(256) resize_area_kernel(const unsigned char* __restrict__ src, int B, int H, int W,
+                                                          int C, int OH, int OW, double scale_y, double scale_x,
+                                                          int fast_y, int fast_x, float* __restrict__ dst) {
+  const long long total = (long long)B * OH * OW;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int dx = (int)(i % OW);
+    const long long t = i / OW;
+    const int dy = (int)(t % OH), b = (int)(t / OH);
+    const unsigned char* img = src + (long long)b * H * W * C;
+    for (int c = 0; c < C; ++c) {
+      float out;
+      if (fast_y > 0) {  // resizeAreaFast: integer scales in both axes
+        float s = 0.f;
+        for (int yy = 0; yy < fast_y; ++yy)
+          for (int xx = 0; xx < fast_x; ++xx) {
+            const float u = (float)img[((long long)(dy * fast_y + yy) * W + dx * fast_x + xx) * C + c];
+            s = s + (u / 255.f - 0.5f) * 2.f;
+          }
+        out = s * (1.f / (float)(fast_y * fast_x));
+      } else {
+        int xs[AREA_MAXK], ys[AREA_MAXK];
+        float ax[AREA_MAXK], ay[AREA_MAXK];
+        const int kx = area_cells(dx, scale_x, W, xs, ax), ky = area_cells(dy, scale_y, H, ys, ay);
+        float sum = 0.f;
+        for (int j = 0; j < ky; ++j) {
+          const unsigned char* row = img + (long long)ys[j] * W * C + c;
+          float buf = 0.f;
+          for (int k = 0; k < kx; ++k) {
+            const float v = ((float)row[(long long)xs[k] * C] / 255.f - 0.5f) * 2.f;
+            buf = buf + v * ax[k];
+          }
+          sum = sum + ay[j] * buf;
+        }
+        out = sum;
+      }
+      dst[i * C + c] = out;
+    }
   }
 }
 
@@ -51,8 +118,40 @@ extern "C" int stc_prepare_batch(const unsigned char* src, int B, int H, int W, 
   STC_REQUIRE(src && params && dst, "stc_prepare_batch: null pointer");
   const long long total = (long long)B * C * OH * OW;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(prepare_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, B, H, W, C, params, pad_h,
-                     pad_w, OH, OW, dst);
+  hipLaunchKernelGGL(prepare_kernel<unsigned char>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, B, H, W, C,
+                     params, pad_h, pad_w, OH, OW, dst);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_prepare_batch_f32(const float* src, int B, int H, int W, int C, const int* params, int pad_h,
+                                     int pad_w, int OH, int OW, float* dst, void* stream) {
+  STC_REQUIRE(B >= 0 && H >= 1 && W >= 1 && C >= 1 && OH >= 1 && OW >= 1 && pad_h >= 0 && pad_w >= 0,
+              "stc_prepare_batch_f32: bad shape B=%d H=%d W=%d C=%d OH=%d OW=%d", B, H, W, C, OH, OW);
+  if (B == 0) return 0;
+  STC_REQUIRE(src && params && dst, "stc_prepare_batch_f32: null pointer");
+  const long long total = (long long)B * C * OH * OW;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(prepare_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, B, H, W, C, params,
+                     pad_h, pad_w, OH, OW, dst);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_resize_area(const unsigned char* src, int B, int H, int W, int C, int OH, int OW, float* dst,
+                               void* stream) {
+  STC_REQUIRE(B >= 0 && C >= 1 && OH >= 1 && OW >= 1 && OH < H && OW < W,
+              "stc_resize_area: INTER_AREA shrink only (B=%d %dx%d -> %dx%d)", B, H, W, OH, OW);
+  if (B == 0) return 0;
+  STC_REQUIRE(src && dst, "stc_resize_area: null pointer");
+  const double scale_x = 1.0 / ((double)OW / W), scale_y = 1.0 / ((double)OH / H);
+  const int iscale_x = (int)lround(scale_x), iscale_y = (int)lround(scale_y);
+  const bool fast = fabs(scale_x - iscale_x) < DBL_EPSILON && fabs(scale_y - iscale_y) < DBL_EPSILON;
+  STC_REQUIRE(fast || (scale_x < AREA_MAXK - 2 && scale_y < AREA_MAXK - 2), "stc_resize_area: scale too large");
+  const long long total = (long long)B * OH * OW;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(resize_area_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, B, H, W, C, OH, OW,
+                     scale_y, scale_x, fast ? iscale_y : 0, fast ? iscale_x : 0, dst);
   STC_CHECK_LAUNCH();
   return 0;
 }

@@ -83,6 +83,8 @@ _SIGS = {
     "stc_istd_errors": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp]),
     "stc_istd_ssim": (_i32, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp]),
     "stc_prepare_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "stc_prepare_batch_f32": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "stc_resize_area": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "stc_last_error": (ctypes.c_char_p, []),
     "stc_version": (_i32, []),
 }

@@ -29,3 +29,16 @@ def test_oracle_hand_case():
     np.testing.assert_array_equal(out[0], want)
     padded = P.prepare_one(img, 0, 0, 0, 1, 1, 2, 2)  # top-left corner of the 1-pixel zero border
     assert padded[0, 0, 0] == 0.0 and padded[0, 0, 1] == 0.0 and padded[0, 1, 0] == 0.0 and padded[0, 1, 1] == -1.0
+
+
+def test_area_oracle_cells_and_fast_path():
+    # 4 -> 2 per axis is an integer scale: the block mean
+    img = np.arange(16, dtype=np.uint8).reshape(4, 4) * 16
+    r = P.resize_area_one(img, 2, 2)[:, :, 0]
+    v = (img.astype(np.float32) / np.float32(255) - np.float32(0.5)) * np.float32(2)
+    np.testing.assert_allclose(r, v.reshape(2, 2, 2, 2).mean(axis=(1, 3)), atol=2e-7)
+    # 5 -> 2 (scale 2.5): cells [0,2.5) and [2.5,5): weights 0.4, 0.4, 0.2 | 0.2, 0.4, 0.4
+    tab = P._area_tab(2, 5, 2.5)
+    assert [s for s, _ in tab[0]] == [0, 1, 2] and [s for s, _ in tab[1]] == [2, 3, 4]
+    np.testing.assert_allclose([a for _, a in tab[0]], [0.4, 0.4, 0.2], rtol=1e-6)
+    np.testing.assert_allclose([a for _, a in tab[1]], [0.2, 0.4, 0.4], rtol=1e-6)
