@@ -5,14 +5,28 @@ A "step" is one full ST-CGAN training iteration (STCGAN.run_epoch body,
 STCGAN/stcgan.py:208-312): 6 network forwards + D backward + Adam(D), then 4
 discriminator forwards + G backward + Adam(G), on a resident synthetic batch of
 256x256 triplets (x, y ~ U(-1,1), m = +-1), batch 32 per GPU (BASELINE config 3/4).
-Multi-GPU: one process per GPU (torchrun), batch sharded (32 per rank, weak
-scaling), RCCL all-reduce of the G/D gradients.
+Multi-GPU: one process per GPU, batch sharded (32 per rank, weak scaling), RCCL
+all-reduce of the G/D gradients.  ``--gpus N`` with N > 1 and no torchrun environment
+starts the N rank processes itself (a child ``torch.distributed.run``, launched before
+this process touches the GPU) and relays rank 0's line.
 
-Prints ONE JSON line on rank 0 (see the driver contract in the task statement).
+Prints ONE JSON line on rank 0 (the driver contract), with:
+  roofline      the dominant kernel by summed device time over every conv-family launch of
+                one train step (HIP events bracketing each MAIN kernel, not the reductions
+                enqueued after it), its algorithmic TFLOP/s vs the bf16/fp32 MFMA peak, its HBM
+                bytes per launch from the committed rocprofv3 PMC passes; the whole step's and
+                the north-star G1+G2 forward's MFMA fractions;
+  parity        the metric's "G2 max-abs vs CPU": G1 -> G2 at ngf=64 (256x256) on this GPU vs the
+                CPU oracle, fp32 (BASELINE target 1e-4) and bf16;
+  configs       the other BASELINE configs' throughput (C2 fp32 G1+G2 fwd+bwd bs=16, C5 480x640
+                inference bs=8);
+  cpu_baseline  the oracle (a torch-CPU restatement of the reference, pinned by the reference's
+                goldens) on this host's cores at BASELINE's units (C3 bs=32 step; C1, C2, C5).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -20,11 +34,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "shadow-removal-istd_amd"))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 METRIC = "ST-CGAN train images/s at 256×256 bs=32, 1/2/4/8 MI355X; G2 max-abs vs CPU"
 PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2516.0}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+STEP_GFLOP_PER_IMG = 186.23  # conv + convT fwd/bwd FLOPs of one train step
 
 
 def gen_fwd_flops(in_c, out_c, ngf, B, H, W, num_downs=8):
@@ -54,25 +66,53 @@ def parse():
     ap.add_argument("--ngf", type=int, default=64)
     ap.add_argument("--dtype", default=os.environ.get("STC_BENCH_DTYPE", "bf16"), choices=["fp32", "bf16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=4)
-    ap.add_argument("--cpu-iters", type=int, default=12)  # ~10 s of host work on the GPU box
+    ap.add_argument("--no-extras", action="store_true", help="skip the parity / other-config measurements")
+    ap.add_argument("--cpu-batch", type=int, default=32, help="batch of the timed CPU train step (C3: 32)")
     return ap.parse_args()
 
 
+def spawn_ranks(n):
+    """--gpus N > 1 without a torchrun environment: run N rank processes (one per GPU) under
+    torch.distributed.run as a CHILD process -- started before this process touches the GPU, so
+    nothing is exec'd from an initialised process -- and relay its output and exit code."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def host_cores():
+    """Cores this process may use: the affinity set, capped by a cgroup CPU quota if one is set."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = max(1, min(n, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(args):
-    """The CPU oracle (oracle/stcgan_ref.py, a torch-CPU restatement of the reference
-    run_epoch, parity-pinned by tests/golden) timed on this host's cores."""
+    """The CPU oracle (oracle/stcgan_ref.py, a torch-CPU restatement of the reference run_epoch,
+    parity-pinned by tests/golden) on this host's cores, at BASELINE's units: C3 = one full train
+    step at batch 32 (after one warm-up step at batch 4), plus C1 (G1 forward bs=4), C2 (G1+G2
+    forward+backward bs=16) and C5 (480x640 G1->G2 inference bs=8)."""
+    import torch
     from oracle import stcgan_ref as ref
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     from fixture_init import fixture_state, pm_one, uniform
-    try:
-        ncores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncores = os.cpu_count() or 1
-    threads = max(1, min(16, ncores))
+    threads = host_cores()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
-    ngf, bs, s = args.ngf, args.cpu_batch, args.size
+    ngf, s = args.ngf, args.size
     states = {
         "G1": fixture_state(ref.generator_state_template(3, 1, ngf), 11, "ref"),
         "G2": fixture_state(ref.generator_state_template(4, 3, ngf), 12, "ref"),
@@ -80,20 +120,226 @@ def cpu_baseline(args):
         "D2": fixture_state(ref.discriminator_state_template(7, ngf), 14, "ref"),
     }
     tr = ref.OracleSTCGAN(states)
-    batch = [([], uniform((bs, 3, s, s), 1), pm_one((bs, 1, s, s), 2), uniform((bs, 3, s, s), 3))]
-    tr.run_epoch(batch)  # warm-up iteration
+
+    def batch(bs):
+        return [([], uniform((bs, 3, s, s), 1), pm_one((bs, 1, s, s), 2), uniform((bs, 3, s, s), 3))]
+
+    t_all = time.perf_counter()
+    tr.run_epoch(batch(4))  # warm-up (allocator, kernels)
+    bs = args.cpu_batch
+    b = batch(bs)
     t0 = time.perf_counter()
-    for _ in range(args.cpu_iters):
-        tr.run_epoch(batch)
-    dt = time.perf_counter() - t0
+    tr.run_epoch(b)
+    c3 = bs / (time.perf_counter() - t0)
+    # C1: G1 forward bs=4 (train-mode BN), 2 timed iterations
+    x4 = uniform((4, 3, s, s), 4)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        for _ in range(2):
+            ref.generator_forward(states["G1"], x4, True)
+        c1 = 8 / (time.perf_counter() - t0)
+    # C2: G1 + G2 forward + backward (L1 data losses) bs=16, 1 timed iteration
+    x16, m16, y16 = uniform((16, 3, s, s), 5), pm_one((16, 1, s, s), 6), uniform((16, 3, s, s), 7)
+    t0 = time.perf_counter()
+    mp = ref.generator_forward(states["G1"], x16, True)
+    yp = ref.generator_forward(states["G2"], torch.cat((x16, mp), 1), True)
+    (ref.data_loss(mp, m16) + 5 * ref.data_loss(yp, y16)).backward()
+    c2 = 16 / (time.perf_counter() - t0)
+    # C5: 480x640 eval-mode inference bs=8
+    x8 = uniform((8, 3, 480, 640), 8)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        mp = ref.generator_forward(states["G1"], x8, False)
+        ref.generator_forward(states["G2"], torch.cat((x8, mp), 1), False)
+        c5 = 8 / (time.perf_counter() - t0)
+    total = time.perf_counter() - t_all
     torch.set_num_threads(prev)
-    return {"value": round(bs * args.cpu_iters / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle run_epoch (full D+G train step, fp32, ngf={ngf}) at batch {bs} {s}x{s}, "
-                      f"{args.cpu_iters} timed iterations after 1 warm-up ({dt:.1f} s)"}
+    return {"value": round(c3, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle run_epoch (full D+G train step, fp32, ngf={ngf}) at batch {bs} {s}x{s}: one "
+                      f"timed iteration after a batch-4 warm-up; whole CPU leg {total:.1f} s",
+            "configs": {"C1_g1_fwd_bs4_img_s": round(c1, 3), "C2_g1g2_fwd_bwd_bs16_img_s": round(c2, 3),
+                        "C3_train_step_bs32_img_s": round(c3, 4), "C5_infer_480x640_bs8_img_s": round(c5, 3)}}
+
+
+def make_trainer(ngf, dtype, local):
+    import types
+    from stcgan_amd.stcgan import STCGAN
+    a = types.SimpleNamespace(devices=[f"cuda:{local}"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5,
+                              beta2=0.999, D_loss_fn="standard", D_loss_type="normal", ngf=ngf,
+                              dtype=dtype, load_weights_g1=None, load_weights_g2=None,
+                              load_weights_d1=None, load_weights_d2=None)
+    return STCGAN(a)
+
+
+def roofline_of_step(tr, x, m, y, args, B, s):
+    """Dominant kernel of one (untimed) train step by summed device time, and the north-star set."""
+    import torch
+    from stcgan_amd import ops
+    ops._timer = []
+    tr.train_step(x, m, y)
+    torch.cuda.synchronize()
+    launches, ops._timer = ops._timer, None
+    per, shapes = {}, {}
+    for name, _single, fl, e0, e1, desc in launches:
+        ms = e0.elapsed_time(e1)
+        a = per.setdefault(name, [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += fl
+        a[2] += ms
+        shapes.setdefault(name, []).append((round(ms * 1e3, 1), desc))
+    dom = max(per, key=lambda k: per[k][2])
+    n_dom, fl_dom, ms_dom = per[dom]
+    peak = PEAK_TFLOPS[args.dtype]
+    achieved = fl_dom / (ms_dom * 1e-3) / 1e12
+    # the north-star kernel set: one train-mode G1+G2 forward (770.95 GFLOP at bs=32, 256^2), HIP events
+    flops = gen_fwd_flops(3, 1, args.ngf, B, s, s) + gen_fwd_flops(4, 3, args.ngf, B, s, s)
+    with torch.no_grad():
+        mp = tr.G1(x)
+        tr.G2([x, mp])
+        reps = 3
+        st = torch.cuda.current_stream()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(st)
+        for _ in range(reps):
+            mp = tr.G1(x)
+            tr.G2([x, mp])
+        ev1.record(st)
+        ev1.synchronize()
+        fwd_ms = ev0.elapsed_time(ev1) / reps
+    set_tf = flops / (fwd_ms * 1e-3) / 1e12
+    top = sorted(per.items(), key=lambda kv: -kv[1][2])[:10]
+    # HBM traffic per launch of the dominant kernel: rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; gfx950
+    # FETCH_SIZE x2 correction) over the bench command, committed under profiles/<round>/pmc_traffic.json
+    traffic, traffic_src = None, None
+    import glob
+    for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        try:
+            tab = json.load(open(fpath))
+        except (OSError, ValueError):
+            continue
+        hit = [v for k, v in tab.items() if dom in k]
+        if hit and args.dtype == "bf16":
+            traffic = int(hit[0]["hbm_bytes_per_launch"])
+            traffic_src = os.path.relpath(fpath, ROOT) + f" (mean over {hit[0]['launches']} launches, all shapes)"
+            break
+    conv_ms = sum(v[2] for v in per.values())
+    conv_gf = sum(v[1] for v in per.values()) / 1e9
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+            "traffic_src": traffic_src,
+            "kernel": f"{dom}: {n_dom} launches in one train step, {fl_dom / 1e9:.2f} GFLOP, {ms_dom:.3f} ms, "
+                      f"avg {ms_dom / n_dom * 1e3:.1f} us/launch (HIP events around the main kernel)",
+            "dominant_launches_us": shapes[dom][:40],
+            "per_kernel": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 2), "ms": round(v[2], 3),
+                               "avg_us": round(v[2] / v[0] * 1e3, 1),
+                               "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2)} for k, v in top},
+            "gemm_kernels_all": {"launches": len(launches), "gflop": round(conv_gf, 2), "ms": round(conv_ms, 3),
+                                 "frac": round(conv_gf / conv_ms / peak, 4)},
+            "g1g2_forward": {"gflop": round(flops / 1e9, 2), "ms": round(fwd_ms, 3), "tflops": round(set_tf, 2),
+                             "frac": round(set_tf / peak, 4)},
+            "g1g2_forward_frac": round(set_tf / peak, 4)}
+
+
+def g2_parity(args, local):
+    """The metric's 'G2 max-abs vs CPU': G1 -> G2 (train-mode BN, fixture weights with BN gamma ~ 1 so
+    the outputs span the tanh range) at ngf=64, 256x256, bs=1 on this GPU vs the CPU oracle."""
+    import torch
+    from oracle import stcgan_ref as ref
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from fixture_init import fixture_state, uniform
+    from stcgan_amd import networks
+    dev = torch.device("cuda", local)
+    s1 = fixture_state(ref.generator_state_template(3, 1, args.ngf), 11, "one")
+    s2 = fixture_state(ref.generator_state_template(4, 3, args.ngf), 12, "one")
+    x = uniform((1, 3, args.size, args.size), 311)
+    with torch.no_grad():
+        mr = ref.generator_forward({k: v.clone() for k, v in s1.items()}, x, True)
+        yr = ref.generator_forward({k: v.clone() for k, v in s2.items()}, torch.cat((x, mr), 1), True)
+    out = {"config": f"G1->G2 train-mode forward, ngf={args.ngf}, 1x{args.size}x{args.size}, fixture weights"}
+    for dt in ("fp32", "bf16"):
+        g1 = networks.get_generator(3, 1, ngf=args.ngf)
+        g2 = networks.get_generator(4, 3, ngf=args.ngf)
+        g1.load_state_dict(s1)
+        g2.load_state_dict(s2)
+        g1.to(dev).set_compute_dtype(dt).train()
+        g2.to(dev).set_compute_dtype(dt).train()
+        with torch.no_grad():
+            xd = x.to(dev)
+            m = g1(xd)
+            y = g2([xd, m])
+        out[f"g2_maxabs_{dt}"] = float((y.cpu() - yr).abs().max())
+        out[f"g1_maxabs_{dt}"] = float((m.cpu() - mr).abs().max())
+    out["tolerance_fp32"] = 1e-4
+    out["pass_fp32"] = out["g2_maxabs_fp32"] <= 1e-4
+    return out
+
+
+def other_configs(args, local):
+    """C2: G1+G2 forward+backward with the L1 data losses, bs=16, fp32 (parity mode); C5: 480x640
+    G1->G2 eval-mode inference, bs=8, in the bench dtype.  images/s, HIP events, random init."""
+    import torch
+    from stcgan_amd import loss, networks
+    dev = torch.device("cuda", local)
+    res = {}
+    g1 = networks.get_generator(3, 1, ngf=args.ngf)
+    g2 = networks.get_generator(4, 3, ngf=args.ngf)
+    g1.apply(networks.weights_init)
+    g2.apply(networks.weights_init)
+    g1.to(dev).set_compute_dtype("fp32").train()
+    g2.to(dev).set_compute_dtype("fp32").train()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(77)
+    x = torch.rand((16, 3, 256, 256), generator=gen, device=dev) * 2 - 1
+    m = (torch.rand((16, 1, 256, 256), generator=gen, device=dev) < 0.5).float() * 2 - 1
+    y = torch.rand((16, 3, 256, 256), generator=gen, device=dev) * 2 - 1
+    l1 = loss.DataLoss()
+
+    def c2_step():
+        for p in list(g1.parameters()) + list(g2.parameters()):
+            p.grad = None
+        mp = g1(x)
+        yp = g2([x, mp])
+        (l1(mp, m) + 5 * l1(yp, y)).backward()
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    ms = timed(c2_step, 5)
+    res["C2_g1g2_fwd_bwd_bs16_fp32"] = {"images_per_s": round(16 / (ms * 1e-3), 2), "ms_per_iter": round(ms, 3),
+                                         "tflops": round(72.18e9 * 16 / (ms * 1e-3) / 1e12, 2),
+                                         "frac_fp32_mfma": round(72.18e9 * 16 / (ms * 1e-3) / 1e12 / 157.3, 4)}
+    g1.set_compute_dtype(args.dtype).eval()
+    g2.set_compute_dtype(args.dtype).eval()
+    x5 = torch.rand((8, 3, 480, 640), generator=gen, device=dev) * 2 - 1
+
+    def c5():
+        with torch.no_grad():
+            mp = g1(x5)
+            g2([x5, mp])
+
+    ms = timed(c5, 5)
+    res[f"C5_infer_480x640_bs8_{args.dtype}"] = {"images_per_s": round(8 / (ms * 1e-3), 2),
+                                                  "ms_per_iter": round(ms, 3),
+                                                  "tflops": round(113.29e9 * 8 / (ms * 1e-3) / 1e12, 2)}
+    return res
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+
+    import torch
+    import torch.distributed as dist
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -107,15 +353,11 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    import types
-    from stcgan_amd.stcgan import STCGAN
 
-    a = types.SimpleNamespace(devices=[f"cuda:{local}"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5,
-                              beta2=0.999, D_loss_fn="standard", D_loss_type="normal", ngf=args.ngf,
-                              dtype=args.dtype, load_weights_g1=None, load_weights_g2=None,
-                              load_weights_d1=None, load_weights_d2=None)
-    torch.manual_seed(1234 + rank)
-    tr = STCGAN(a)
+    # one initialisation (rank 0's weights are broadcast to every rank in STCGAN.__init__); each rank
+    # draws its own synthetic shard
+    torch.manual_seed(1234)
+    tr = make_trainer(args.ngf, args.dtype, local)
     dev = torch.device("cuda", local)
     B, s = args.batch, args.size
     g = torch.Generator(device=dev)
@@ -147,73 +389,20 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
-    # ---- roofline.  (1) Dominant kernel: every conv-family launch of one extra (untimed) train step
-    # is bracketed by HIP events on the stream it is enqueued on (torch's current stream); the kernel
-    # template with the largest summed time is the dominant one; achieved = its algorithmic FLOPs
-    # (2*MACs of the launch's GEMM view) / its summed time.  Launches that enqueue a second kernel
-    # (split-K / split-pixel reductions) are excluded, so each event pair times exactly one kernel and
-    # the per-launch average is comparable with rocprofv3's for the same symbol.
-    from stcgan_amd import ops
-    ops._timer = []
-    tr.train_step(x, m, y)
-    torch.cuda.synchronize()
-    launches, ops._timer = ops._timer, None
-    per = {}
-    for name, single, fl, e0, e1, _ in launches:
-        if not single:
-            continue
-        a = per.setdefault(name, [0, 0.0, 0.0])
-        a[0] += 1
-        a[1] += fl
-        a[2] += e0.elapsed_time(e1)
-    dom = max(per, key=lambda k: per[k][2])
-    n_dom, fl_dom, ms_dom = per[dom]
-    achieved = fl_dom / (ms_dom * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[args.dtype]
-    # (2) north-star kernel set: one train-mode G1+G2 forward (770.95 GFLOP at bs=32, 256^2), HIP events
-    flops = gen_fwd_flops(3, 1, args.ngf, B, s, s) + gen_fwd_flops(4, 3, args.ngf, B, s, s)
-    with torch.no_grad():
-        mp = tr.G1(x)
-        tr.G2([x, mp])
-        reps = 3
-        st = torch.cuda.current_stream()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record(st)
-        for _ in range(reps):
-            mp = tr.G1(x)
-            tr.G2([x, mp])
-        ev1.record(st)
-        ev1.synchronize()
-        fwd_ms = ev0.elapsed_time(ev1) / reps
-    set_tf = flops / (fwd_ms * 1e-3) / 1e12
-    top = sorted(per.items(), key=lambda kv: -kv[1][2])[:8]
-    # HBM traffic per launch of the dominant kernel: rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE;
-    # gfx950 FETCH_SIZE x2 correction) over the same bench command, committed under profiles/
-    # (scripts/profile_round.sh -> profiles/<round>/pmc_traffic.json); mean over all its launches.
-    traffic, traffic_src = None, None
-    import glob
-    for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
-        try:
-            tab = json.load(open(fpath))
-        except (OSError, ValueError):
-            continue
-        hit = [v for k, v in tab.items() if dom in k]
-        if hit and args.dtype == "bf16":
-            traffic = int(hit[0]["hbm_bytes_per_launch"])
-            traffic_src = os.path.relpath(fpath, ROOT) + f" (mean over {hit[0]['launches']} launches, all shapes)"
-            break
-    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_src": traffic_src,
-                "kernel": f"{dom}: {n_dom} single-kernel launches in one train step, {fl_dom / 1e9:.2f} GFLOP, "
-                          f"{ms_dom:.3f} ms, avg {ms_dom / n_dom * 1e3:.1f} us/launch (HIP events)",
-                "per_kernel": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 2), "ms": round(v[2], 3),
-                                   "avg_us": round(v[2] / v[0] * 1e3, 1),
-                                   "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2)} for k, v in top},
-                "g1g2_forward": {"gflop": round(flops / 1e9, 2), "ms": round(fwd_ms, 3),
-                                 "tflops": round(set_tf, 2), "frac": round(set_tf / peak, 4)}}
+    roofline = roofline_of_step(tr, x, m, y, args, B, s)
+    step_tf = STEP_GFLOP_PER_IMG * B / (ms_per_step * 1e-3) / 1e3
+    roofline["whole_step"] = {"gflop": round(STEP_GFLOP_PER_IMG * B, 1), "ms": round(ms_per_step, 3),
+                              "tflops": round(step_tf, 2), "frac": round(step_tf / PEAK_TFLOPS[args.dtype], 4)}
+    roofline["whole_step_frac"] = roofline["whole_step"]["frac"]
+    if world > 1:
+        dist.barrier()
 
-    cpu = None
+    extras, cpu = {}, None
+    if rank == 0 and world == 1 and not args.no_extras:
+        del tr
+        torch.cuda.empty_cache()
+        extras["parity"] = g2_parity(args, local)
+        extras["configs"] = other_configs(args, local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
     if rank == 0:
@@ -224,7 +413,7 @@ def main():
                "config": {"workload": "full ST-CGAN train step (G1,G2,D1,D2 fwd/bwd + MSE-cGAN/L1 + Adam), "
                                       f"{s}x{s}", "global_batch": B * world, "per_gpu_batch": B,
                           "image_size": s, "ngf": args.ngf, "parallelism": f"dp{world}"},
-               "roofline": roofline, "cpu_baseline": cpu}
+               "roofline": roofline, "cpu_baseline": cpu, **extras}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

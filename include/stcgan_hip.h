@@ -290,7 +290,13 @@ int stc_adam_step(const int64_t* table, int ntensors, int64_t total_blocks,
                   float lr, float beta1, float beta2, float eps, int step, void* stream);
 int stc_adam_elems_per_block(void);
 
-/* ---- misc ------------------------------------------------------------------------ */
+/* ---- misc ------------------------------------------------------------------------
+ * stc_time_next_main_kernel: instrumentation (bench.py).  The next call ON THIS THREAD that launches a
+ * GEMM-family main kernel (stc_conv_fwd, stc_conv_fwd_ex, stc_conv_bwd_bn, stc_conv_wgrad) records
+ * ev_begin / ev_end (hipEvent_t, timing enabled) on its stream immediately before and after that kernel
+ * -- not around the split-K / split-pixel reduction it may enqueue afterwards -- then disarms.  Both
+ * NULL disarms.  Thread-local one-shot state: calls on other threads are unaffected.               */
+int stc_time_next_main_kernel(void* ev_begin, void* ev_end);
 const char* stc_last_error(void);
 int stc_version(void);
 

@@ -19,10 +19,9 @@ if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
   step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
-if [ "$MODE" = debug ]; then
-  step debug 300 python scripts/debug_nets.py G1 G2
-  step pytest_gpu 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
-  step bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline
+if [ "$MODE" = quick ]; then  # selected test files (TESTS=...), then the default bench line
+  step pytest_sel 600 python -u -m pytest ${TESTS:-tests/test_gpu_configs.py} -m gpu -v -rf -s --timeout 300 --timeout-method thread
+  step bench 600 python bench.py
 fi
 if [ "$MODE" = prof ] || [ "$MODE" = all_prof ]; then
   export TMPDIR=/tmp

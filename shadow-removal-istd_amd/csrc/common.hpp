@@ -20,6 +20,9 @@ typedef short shortx4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------- errors
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);
+// stc_time_next_main_kernel instrumentation: record around the main kernel of a call
+void main_timer_begin(hipStream_t st);
+void main_timer_end(hipStream_t st);
 
 #define STC_CHECK_LAUNCH()                                                     \
   do {                                                                         \

@@ -581,6 +581,7 @@ static bool launch_narrow_tiled(int kind, int B, ConvParams& p, hipStream_t st) 
   const int tpi = tiles_x * tiles_y;
   dim3 grid((unsigned)(B * tpi));
   const bool n4 = p.N <= 4;
+  main_timer_begin(st);
   if (geom == 0) {
     if (n4) hipLaunchKernelGGL((narrow_tiled_kernel<T, 0, 4>), grid, dim3(256), 0, st, p, tiles_x, tpi);
     else hipLaunchKernelGGL((narrow_tiled_kernel<T, 0, 8>), grid, dim3(256), 0, st, p, tiles_x, tpi);
@@ -588,6 +589,7 @@ static bool launch_narrow_tiled(int kind, int B, ConvParams& p, hipStream_t st) 
     if (n4) hipLaunchKernelGGL((narrow_tiled_kernel<T, 1, 4>), grid, dim3(64), 0, st, p, tiles_x, tpi);
     else hipLaunchKernelGGL((narrow_tiled_kernel<T, 1, 8>), grid, dim3(64), 0, st, p, tiles_x, tpi);
   }
+  main_timer_end(st);
   return true;
 }
 
@@ -630,6 +632,7 @@ static int launch_igemm(const Plan& pl, ConvParams& p, hipStream_t st) {
   dim3 grid(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
   const size_t lds = lds_bytes(pl.BM, pl.BN);
   const bool pro = p.sc != nullptr || p.pro_act != 0;
+  main_timer_begin(st);
 #define STC_L(BM_, BN_, WM_, WN_)                                                                  \
   if (pl.BM == BM_ && pl.BN == BN_) {                                                              \
     if (pro) hipLaunchKernelGGL((igemm_kernel<T, BM_, BN_, WM_, WN_, true>), grid, dim3(256), lds, st, p); \
@@ -642,6 +645,7 @@ static int launch_igemm(const Plan& pl, ConvParams& p, hipStream_t st) {
   STC_L(32, 128, 1, 4)
   { return fail(-1, "igemm: no kernel for tile %dx%d", pl.BM, pl.BN); }
 #undef STC_L
+  main_timer_end(st);
   STC_CHECK_LAUNCH();
   if (p.ws) {
     const long long total = (long long)p.nphase * p.M * p.N;
@@ -810,8 +814,10 @@ extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
     }
     dim3 grid((unsigned)std::min(cdiv(p.M, 4), 4096), g.nphase);
     const size_t lds = (size_t)Cout * K * esz;
+    main_timer_begin(st0);
     if (dtype == STC_F32) hipLaunchKernelGGL(smalln_kernel<float>, grid, dim3(256), lds, st0, p);
     else hipLaunchKernelGGL(smalln_kernel<bf16>, grid, dim3(256), lds, st0, p);
+    main_timer_end(st0);
     STC_CHECK_LAUNCH();
     return 0;
   }

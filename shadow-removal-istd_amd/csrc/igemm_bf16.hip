@@ -832,6 +832,7 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     else                                                                                                    \
       hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, false>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
     break;
+  main_timer_begin(st);
   switch (pl.cfg) {
     STC_B(0, 128, 128, 2, 2, 2, 64)
     STC_B(1, 256, 128, 2, 2, 2, 64)
@@ -861,6 +862,7 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
       return fail(-1, "bf16 igemm: bad tile config %d", pl.cfg);
   }
 #undef STC_B
+  main_timer_end(st);
   STC_CHECK_LAUNCH();
   if (pl.ksplit > 1) {
     STC_REQUIRE(p.vec_out, "bf16 igemm: split-K needs a 16-byte aligned NHWC bf16 output");

@@ -284,12 +284,14 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
   if ((long long)B * p.GH * p.GW == 0) return 0;
   dim3 grid((unsigned)(B * p.tiles_per_img), (unsigned)p.nsplit);
   const size_t lds = halo_lds(geom, ty);
+  main_timer_begin(st);
   if (geom == 0) {
     if (p.NP <= 16) hipLaunchKernelGGL((narrow_halo_kernel<0, 1, 8>), grid, dim3(256), lds, st, p);
     else hipLaunchKernelGGL((narrow_halo_kernel<0, 2, 8>), grid, dim3(256), lds, st, p);
   } else {
     hipLaunchKernelGGL((narrow_halo_kernel<1, 1, 8>), grid, dim3(256), lds, st, p);
   }
+  main_timer_end(st);
   STC_CHECK_LAUNCH();
   if (p.nsplit > 1) {
     const long long total = (long long)B * p.GH * p.GW * p.NP;

@@ -366,8 +366,10 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
   dim3 grid(pl.mtiles * pl.ntiles, 1, pl.nsplit);
   if (pl.nsplit <= 1) {
     p.dW = dW;
+    main_timer_begin(st);
     if (dtype == STC_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, p);
+    main_timer_end(st);
     STC_CHECK_LAUNCH();
     return 0;
   }
@@ -375,8 +377,10 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
   STC_REQUIRE(workspace && workspace_bytes >= need, "stc_conv_wgrad: workspace %lld < %lld",
               (long long)workspace_bytes, (long long)need);
   p.ws = (float*)workspace;
+  main_timer_begin(st);
   if (dtype == STC_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, p);
   else hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, p);
+  main_timer_end(st);
   STC_CHECK_LAUNCH();
   const long long total = (long long)R * 16 * Cg_out;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);

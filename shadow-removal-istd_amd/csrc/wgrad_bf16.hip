@@ -399,6 +399,7 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
                 (long long)need);
     p.ws = (float*)workspace;
   }
+  main_timer_begin(st);
   switch (pl.cfg) {
     case 0: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false>), grid, dim3(256), lds, st, p); break;
     case 1: hipLaunchKernelGGL((wgrad_bf16_kernel<64, 128, 1, 4, false>), grid, dim3(256), lds, st, p); break;
@@ -407,6 +408,7 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
     case 4: hipLaunchKernelGGL((wgrad_bf16_kernel<256, 128, 4, 2, false>), grid, dim3(512), lds, st, p); break;
     default: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 256, 2, 4, false>), grid, dim3(512), lds, st, p); break;
   }
+  main_timer_end(st);
   STC_CHECK_LAUNCH();
   if (pl.nsplit <= 1) return 0;
   const long long total = (long long)R * 16 * Cg_out;

@@ -41,8 +41,25 @@ def _pro(pro):
     return ptr(sc), ptr(sh)
 
 
-_timer = None  # when a list: conv()/conv_stats()/wgrad() append (kernel, single-kernel launch, flops, start, end)
-_DEBUG_NO_PROLOGUE = False
+# Instrumentation (bench.py / scripts): when a list, conv()/conv_stats()/conv_bn_backward()/wgrad() append
+# (kernel, single-kernel call, flops, start event, end event, description); the events bracket the call's
+# MAIN kernel only (stc_time_next_main_kernel), not a split-K / split-pixel reduction it enqueues after it.
+_timer = None
+
+
+def _main_events():
+    """A pair of timing events armed to bracket the next main kernel this thread launches."""
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()  # creates the events; the library records them again around the kernel
+    e1.record()
+    check(lib().stc_time_next_main_kernel(ctypes.c_void_p(e0.cuda_event), ctypes.c_void_p(e1.cuda_event)),
+          "stc_time_next_main_kernel")
+    return e0, e1
+
+
+def _disarm():
+    lib().stc_time_next_main_kernel(None, None)
 
 
 def plan_of(kind, B, gh, gw, cin, cout, dt):
@@ -61,20 +78,17 @@ def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=No
     l = lib()
     nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
     ws, nb = _ws(nbytes, dev)
-    if _DEBUG_NO_PROLOGUE:  # timing experiments only (wrong numerics); never set in tests/bench
-        pro, slope = None, None
     sc, sh = _pro(pro)
     timer = _timer
     if timer is not None:
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
+        e0, e1 = _main_events()
     rc = l.stc_conv_fwd(L.dtype_code(dt), kind, B, xv, cin, sc, sh, 0 if slope is None else 1,
                         0.0 if slope is None else float(slope), ptr(w_packed), cout, yv, ptr(bias), int(tanh),
                         int(out_f32), ptr(ws), nb, stream())
+    if timer is not None:
+        _disarm()
     check(rc, "stc_conv_fwd")
     if timer is not None:
-        e1.record()
         _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
 
 
@@ -100,13 +114,13 @@ def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
     fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
     timer = _timer
     if timer is not None:
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-    check(lib().stc_conv_fwd_ex(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ptr(bias), 0, 0,
-                                ptr(part), nch, fp, ptr(ws), nb, stream()), "stc_conv_fwd_ex")
+        e0, e1 = _main_events()
+    rc = lib().stc_conv_fwd_ex(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ptr(bias), 0, 0,
+                               ptr(part), nch, fp, ptr(ws), nb, stream())
     if timer is not None:
-        e1.record()
+        _disarm()
+    check(rc, "stc_conv_fwd_ex")
+    if timer is not None:
         _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
     return part, nch
 
@@ -164,13 +178,13 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
                      mean.data_ptr(), rstd.data_ptr(), float(s_self), float(s_other), C, ch_off)
     timer = _timer
     if timer is not None:
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-    check(l.stc_conv_bwd_bn(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse), ptr(part),
-                            nch, ptr(ws), nb, stream()), "stc_conv_bwd_bn")
+        e0, e1 = _main_events()
+    rc = l.stc_conv_bwd_bn(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse), ptr(part),
+                           nch, ptr(ws), nb, stream())
     if timer is not None:
-        e1.record()
+        _disarm()
+    check(rc, "stc_conv_bwd_bn")
+    if timer is not None:
         _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=yv.cs == 1)
     # apply: g1 = the conv output at the BN channels over the BN extent
     g1 = L.View(yv.p, bn_x.H, bn_x.W, yv.bs, yv.rs, yv.ps, yv.co + ch_off, yv.cs, 0)
@@ -208,16 +222,15 @@ def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=Non
     gsc, gsh = _pro(gpro)
     timer = _timer
     if timer is not None:
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
+        e0, e1 = _main_events()
     rc = l.stc_conv_wgrad(L.dtype_code(dt), B, stride, Dv, R, dsc, dsh, 0 if dslope is None else 1,
                           0.0 if dslope is None else float(dslope), Gv, Cg, Cg_out, gsc, gsh,
                           0 if gslope is None else 1, 0.0 if gslope is None else float(gslope), ptr(dW), ptr(ws), nb,
                           stream())
+    if timer is not None:
+        _disarm()
     check(rc, "stc_conv_wgrad")
     if timer is not None:
-        e1.record()
         dma = dt == torch.bfloat16 and dpro is None and gpro is None and dslope is None and gslope is None
         name = "wgrad_bf16_kernel" if dma else "wgrad_kernel"
         timer.append((name, nbytes == 0, 2.0 * B * Dv.H * Dv.W * R * 16 * Cg, e0, e1,

@@ -76,6 +76,9 @@ class STCGAN(object):
         for net in (self.G1, self.G2, self.D1, self.D2):
             net.to(self.device)
             net.set_compute_dtype(dtype)
+        # every rank starts from rank 0's weights (DataParallel replicates dev0's module)
+        parallel.broadcast_state([self.G1, self.G2, self.D1, self.D2])
+        self.start_epoch = 0
         self.optim_G = Adam(list(self.G1.parameters()) + list(self.G2.parameters()),
                             lr=args.lr_G, betas=(args.beta1, args.beta2))
         self.optim_D = Adam(list(self.D1.parameters()) + list(self.D2.parameters()),
@@ -115,7 +118,7 @@ class STCGAN(object):
         self.logger.info("Start training")
         best_loss = 100000.0
         start_time = time.time()
-        for epoch in range(epochs):
+        for epoch in range(self.start_epoch, epochs):
             measures = self.run_epoch()
             if epoch % self.log_interval == 0:
                 self.logger.info(f"epoch {epoch}: {measures['Loss']}")
@@ -135,6 +138,7 @@ class STCGAN(object):
     def _d_losses(self, C1_real, C1_fake, C2_real, C2_fake):
         adv = self.adv_loss
         t = self.d_loss_type
+        mean0 = parallel.global_mean0  # C.mean(dim=0) over the global batch (DataParallel gathers)
         if t == "normal":
             D1_loss = (adv(C1_fake, is_real=False) + adv(C1_real, is_real=True)) * 0.5
             D2_loss = (adv(C2_fake, is_real=False) + adv(C2_real, is_real=True)) * 0.5
@@ -142,10 +146,10 @@ class STCGAN(object):
             D1_loss = adv(C1_real - C1_fake, is_real=True)
             D2_loss = adv(C2_real - C2_fake, is_real=True)
         else:  # "rel_avg"
-            D1_loss = (adv(C1_fake - C1_real.mean(dim=0), is_real=False)
-                       + adv(C1_real - C1_fake.mean(dim=0), is_real=True)) * 0.5
-            D2_loss = (adv(C2_fake - C2_real.mean(dim=0), is_real=False)
-                       + adv(C2_real - C2_fake.mean(dim=0), is_real=True)) * 0.5
+            D1_loss = (adv(C1_fake - mean0(C1_real), is_real=False)
+                       + adv(C1_real - mean0(C1_fake), is_real=True)) * 0.5
+            D2_loss = (adv(C2_fake - mean0(C2_real), is_real=False)
+                       + adv(C2_real - mean0(C2_fake), is_real=True)) * 0.5
         return D1_loss, D2_loss
 
     def _g_losses(self, C1_real, C1_fake, C2_real, C2_fake):
@@ -155,11 +159,12 @@ class STCGAN(object):
             return adv(C1_fake, is_real=True), adv(C2_fake, is_real=True)
         if t == "rel":
             return adv(C1_fake - C1_real, is_real=True), adv(C2_fake - C2_real, is_real=True)
-        G1_loss = (adv(C1_fake - C1_real.mean(dim=0), is_real=True)
-                   + adv(C1_real - C1_fake.mean(dim=0), is_real=False)) * 0.5
+        mean0 = parallel.global_mean0
+        G1_loss = (adv(C1_fake - mean0(C1_real), is_real=True)
+                   + adv(C1_real - mean0(C1_fake), is_real=False)) * 0.5
         # as the reference: the rel_avg G2 loss is computed from the D1 outputs (STCGAN/stcgan.py:286-290)
-        G2_loss = (adv(C1_fake - C1_real.mean(dim=0), is_real=True)
-                   + adv(C1_real - C1_fake.mean(dim=0), is_real=False)) * 0.5
+        G2_loss = (adv(C1_fake - mean0(C1_real), is_real=True)
+                   + adv(C1_real - mean0(C1_fake), is_real=False)) * 0.5
         return G1_loss, G2_loss
 
     def train_step(self, x, m, y, training=True, acc=None):
@@ -215,6 +220,8 @@ class STCGAN(object):
     def run_epoch(self, training=True):
         for net in (self.G1, self.G2, self.D1, self.D2):
             net.train(training)
+        if not training:  # eval-mode replicas use dev0's running statistics
+            parallel.broadcast_buffers([self.G1, self.G2, self.D1, self.D2])
         keys = ["G", "D", "D1", "D2", "G1", "G2", "data1", "data2"]
         acc = {k: torch.zeros((), device=self.device) for k in keys + ["D1_real", "D1_fake", "D2_real", "D2_fake"]}
         data_loader = self.train_loader if training else self.valid_loader
@@ -225,7 +232,10 @@ class STCGAN(object):
             y = y.to(self.device, non_blocking=True)
             self.train_step(x, m, y, training=training, acc=acc)
             n_batches += 1
-        host = {k: float(v) for k, v in acc.items()}  # the one host sync of the epoch
+        # global-batch values on every rank (DataParallel computes the losses on the gathered
+        # batch), so each rank's ReduceLROnPlateau sees the same sums: one collective, one host sync
+        acc = parallel.average_scalars(acc)
+        host = {k: float(v) for k, v in acc.items()}
         loss = {k: host[k] for k in keys}
         if training:
             self.decay_G.step(loss["G"])
@@ -252,6 +262,7 @@ class STCGAN(object):
         with torch.no_grad():
             self.G1.eval()
             self.G2.eval()
+            parallel.broadcast_buffers([self.G1, self.G2])
             for (filenames, x, _, _) in self.valid_loader:
                 x = x.to(self.device, non_blocking=True)
                 m_pred = self.G1(x)

@@ -131,3 +131,17 @@ def compare(d, key, t, atol, rtol=0.0):
     assert abs(float((f * f).sum()) - q_ref) <= (atol * 4) * float(f.abs().sum()) + rtol * q_ref * 2 + 1e-12, \
         key + "::sqsum"
     return err
+
+
+def golden_rms(d, key):
+    """Root-mean-square of fixture entry ``key`` (full tensor or summary): a scale for tolerances."""
+    if key in d:
+        a = np.asarray(d[key], dtype=np.float64)
+        return float(np.sqrt((a * a).mean())) if a.size else 0.0
+    n = int(np.prod(d[key + "::shape"]))
+    return float(np.sqrt(float(d[key + "::sqsum"]) / max(n, 1)))
+
+
+def compare_rel(d, key, t, rel):
+    """compare() with the tolerance scaled by the golden's RMS: atol = rel * rms(golden)."""
+    return compare(d, key, t, atol=rel * golden_rms(d, key) + 1e-12)

@@ -232,6 +232,50 @@ def gen_ngf64(networks):
     return d
 
 
+def gen_ngf64_grad(networks, loss, bs=2, hw=256):
+    """Full-width (ngf=64) G1 -> G2 forward + backward through the reference's DataLoss
+    (data1 + 5 * data2, STCGAN/stcgan.py:292-303 without the adversarial terms): outputs,
+    every parameter gradient and the input gradient as summaries (sum, |sum|, sum of squares,
+    512 fixed samples), BN buffers after the train-mode forward in full."""
+    d = {}
+    g1 = net_specs(networks, 64)["G1"]()
+    g2 = net_specs(networks, 64)["G2"]()
+    s1 = fixture_state(g1.state_dict(), NET_SEED["G1"], "one")
+    s2 = fixture_state(g2.state_dict(), NET_SEED["G2"], "one")
+    g1.load_state_dict(s1)
+    g2.load_state_dict(s2)
+    d["G1/checksum"] = np.array(state_checksum(s1))
+    d["G2/checksum"] = np.array(state_checksum(s2))
+    # deep levels (<= 8x8 at ngf=64 widths) kept away from the ReLU kink, as for the ngf=8 goldens
+    xseed = pick_input_seed(g1, s1, (bs, 3, hw, hw), 900, bs * 512 * 8 * 8)
+    d["meta/x_seed"] = np.array(xseed)
+    x = uniform((bs, 3, hw, hw), xseed).requires_grad_(True)
+    m = pm_one((bs, 1, hw, hw), xseed + 1)
+    y = uniform((bs, 3, hw, hw), xseed + 2)
+    g1.train()
+    g2.train()
+    dl = loss.DataLoss()
+    m_pred = g1(x)
+    y_pred = g2(torch.cat((x, m_pred), dim=1))
+    data1 = dl(m_pred, m)
+    data2 = dl(y_pred, y)
+    total = data1 + 5 * data2
+    total.backward()
+    d["data1"] = np.array(float(data1))
+    d["data2"] = np.array(float(data2))
+    put(d, "m_pred", m_pred)
+    put(d, "y_pred", y_pred)
+    put(d, "input_grad", x.grad)
+    for name, net in (("G1", g1), ("G2", g2)):
+        for k, p in net.named_parameters():
+            put(d, f"{name}/grad/{k}", p.grad)
+        for k, b in net.named_buffers():
+            put(d, f"{name}/buf_after_train/{k}", b)
+    d["meta/bs"] = np.array(bs)
+    d["meta/hw"] = np.array(hw)
+    return d
+
+
 def load_istd():
     from PIL import Image
     base = os.path.join(REF, "color_adjustment_code")
@@ -303,6 +347,7 @@ def main():
         ("nets_ngf8.npz", lambda: gen_nets(networks)),
         ("run_epoch_ngf8.npz", lambda: gen_run_epoch(networks, loss, stcgan)),
         ("g_ngf64.npz", lambda: gen_ngf64(networks)),
+        ("g_ngf64_grad.npz", lambda: gen_ngf64_grad(networks, loss)),
         ("istd_114_5.npz", lambda: gen_istd(networks, stcgan_g)),
     ]
     only = set(sys.argv[1:])

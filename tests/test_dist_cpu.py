@@ -1,9 +1,17 @@
-"""World-size-2 gloo test of the data-parallel gradient exchange (parallel.py), on CPU.
+"""World-size-2 gloo tests of the data-parallel layer (parallel.py), on CPU.
 
-Checks the reference's DataParallel semantics that the RCCL path keeps: with
-per-shard BN, the averaged per-rank gradient of the per-rank mean loss equals
-the gradient of the global-batch mean loss (equal shards).  The networks here
-are the CPU oracle (test infrastructure) -- only the exchange logic is under test.
+Checks the reference's DataParallel semantics that the RCCL path keeps
+(STCGAN/stcgan.py:53-59):
+  * with per-shard BN, the averaged per-rank gradient of the per-rank mean loss
+    equals the gradient of the global-batch mean loss (equal shards);
+  * the rel_avg loss (STCGAN/stcgan.py:240-250) uses C.mean(dim=0) over the GLOBAL
+    batch -- ``global_mean0`` -- and its gradients match the single-process loss;
+  * ranks that initialise from different seeds hold rank 0's weights after
+    ``broadcast_state`` (DataParallel replicates dev0's module);
+  * the epoch loss sums fed to ReduceLROnPlateau are the global ones on every rank;
+  * gradient groups are exchanged in index order whatever order they complete in.
+The networks here are the CPU oracle (test infrastructure) -- only the exchange
+logic is under test.
 """
 import os
 import socket
@@ -98,3 +106,123 @@ def test_grad_allreduce_matches_global_batch():
     want = [v.grad for k, v in params.items() if v.requires_grad]
     for g, w in zip(got, want):
         assert torch.allclose(g, w, atol=1e-6, rtol=1e-5)
+
+
+def _run_world(target, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue
+    import time
+    got, t0 = {}, time.time()
+    while len(got) < world and time.time() - t0 < 300:
+        try:
+            r, val = q.get(timeout=1)
+            got[r] = val
+        except queue.Empty:
+            assert all(p.exitcode in (None, 0) for p in procs), [p.exitcode for p in procs]
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    return got
+
+
+def _rel_avg_loss(params, x, z, mean0):
+    """The reference's rel_avg D1 loss on a (real, fake) pair (STCGAN/stcgan.py:240-245)."""
+    from oracle import stcgan_ref as ref
+    c_real = ref.discriminator_forward(params, x, True)
+    c_fake = ref.discriminator_forward(params, z, True)
+    return (ref.adversarial_loss(c_fake - mean0(c_real), False)
+            + ref.adversarial_loss(c_real - mean0(c_fake), True)) * 0.5
+
+
+def _worker_semantics(rank, world, port, out):
+    import sys
+    for p in (ROOT, PKG_DIR, GOLDEN):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    from fixture_init import fixture_state, uniform
+    from oracle import stcgan_ref as ref
+    from stcgan_amd import parallel
+    res = {}
+    # (1) broadcast_state: different seeds per rank -> rank 0's weights everywhere
+    torch.manual_seed(100 + rank)
+    net = torch.nn.Sequential(torch.nn.Conv2d(4, 8, 4, 2, 1), torch.nn.BatchNorm2d(8))
+    with torch.no_grad():
+        net[1].running_mean.normal_()
+    parallel.broadcast_state([net])
+    res["state"] = {k: v.clone() for k, v in net.state_dict().items()}
+    # (2) rel_avg with the global batch mean: gradients averaged over ranks
+    st = fixture_state(ref.discriminator_state_template(4, 8), 13, "one")
+    params = {k: v.clone().requires_grad_(not ref._is_buffer(k)) for k, v in st.items()}
+    x = uniform((4, 4, 64, 64), 7)
+    z = uniform((4, 4, 64, 64), 8)
+    sl = slice(rank * 2, (rank + 1) * 2)
+    loss = _rel_avg_loss(params, x[sl], z[sl], parallel.global_mean0)
+    loss.backward()
+    plist = [v for k, v in params.items() if v.requires_grad]
+    sync = parallel.GradAllReduce([plist])
+    sync()
+    res["rel_avg_grads"] = [p.grad.clone() for p in plist]
+    res["rel_avg_loss"] = parallel.average_scalars({"l": loss.detach()})["l"].clone()
+    # (3) scheduler inputs: every rank sees the global sums
+    acc = {"G": torch.tensor(float(rank + 1)), "D": torch.tensor(10.0 * (rank + 1))}
+    avg = parallel.average_scalars(acc)
+    res["sched"] = (float(avg["G"]), float(avg["D"]))
+    # (4) launch order: group 1 completes first, is held until group 0 has launched
+    a = torch.ones(3, requires_grad=True)
+    b = torch.ones(3, requires_grad=True)
+    sync2 = parallel.GradAllReduce([[a], [b]])
+    sync2.enable_overlap()
+    order = []
+    orig = sync2._launch
+    sync2._launch = lambda gi: (order.append(gi), orig(gi))
+    (b * (rank + 1)).sum().backward()  # only group 1 completes
+    held = list(order)
+    (a * 2.0).sum().backward()
+    sync2()
+    res["order"] = (held, order, a.grad.clone(), b.grad.clone())
+    import io
+    buf = io.BytesIO()
+    torch.save(res, buf)  # bytes, not shared-memory tensors: the worker exits before the parent reads
+    out.put((rank, buf.getvalue()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dataparallel_semantics_world2():
+    import sys
+    for p in (ROOT, PKG_DIR, GOLDEN):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from fixture_init import fixture_state, uniform
+    from oracle import stcgan_ref as ref
+    import io
+    got = _run_world(_worker_semantics)
+    r0, r1 = (torch.load(io.BytesIO(got[r]), weights_only=True) for r in (0, 1))
+    for k in r0["state"]:
+        assert torch.equal(r0["state"][k], r1["state"][k]), k
+    # single process, global batch of 4, per-shard BN (two shards), global C.mean(dim=0)
+    st = fixture_state(ref.discriminator_state_template(4, 8), 13, "one")
+    params = {k: v.clone().requires_grad_(not ref._is_buffer(k)) for k, v in st.items()}
+    x = uniform((4, 4, 64, 64), 7)
+    z = uniform((4, 4, 64, 64), 8)
+    cr = torch.cat([ref.discriminator_forward(params, x[i * 2:(i + 1) * 2], True) for i in range(2)])
+    cf = torch.cat([ref.discriminator_forward(params, z[i * 2:(i + 1) * 2], True) for i in range(2)])
+    loss = (ref.adversarial_loss(cf - cr.mean(dim=0), False) + ref.adversarial_loss(cr - cf.mean(dim=0), True)) * 0.5
+    loss.backward()
+    want = [v.grad for k, v in params.items() if v.requires_grad]
+    for r in (r0, r1):
+        assert abs(float(r["rel_avg_loss"]) - float(loss)) <= 1e-6 * abs(float(loss)) + 1e-7
+        for g, w in zip(r["rel_avg_grads"], want):
+            assert torch.allclose(g, w, atol=1e-6, rtol=1e-5)
+        assert r["sched"] == (1.5, 15.0)
+        held, order, ga, gb = r["order"]
+        assert held == [] and order == [0, 1]
+        assert torch.allclose(ga, torch.full((3,), 2.0)) and torch.allclose(gb, torch.full((3,), 1.5))

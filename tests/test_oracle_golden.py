@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from fixture_init import compare, fixture_state, normal, pm_one, state_checksum, uniform
+from fixture_init import compare, compare_rel, fixture_state, normal, pm_one, state_checksum, uniform
 from oracle import stcgan_ref as ref
 
 NET_IN = {"G1": 3, "G2": 4, "D1": 4, "D2": 7}
@@ -162,3 +162,36 @@ def test_oracle_losses_match_torch():
                               torch.nn.functional.binary_cross_entropy_with_logits(x, t), atol=1e-6)
     y = normal((2, 3, 8, 8), 2)
     assert torch.allclose(ref.data_loss(x[:, :, :8, :8], y[:, :1]), torch.nn.functional.l1_loss(x[:, :, :8, :8], y[:, :1]))
+
+
+def test_oracle_generators_ngf64_backward(golden):
+    """Full-width G1 -> G2 forward + backward through DataLoss (data1 + 5 data2) at bs=2 vs the
+    reference's own run (tests/golden/g_ngf64_grad.npz): outputs, every parameter gradient, the
+    input gradient and the BN buffers."""
+    torch.set_num_threads(8)
+    d = golden("g_ngf64_grad.npz")
+    bs, hw, xs = int(d["meta/bs"]), int(d["meta/hw"]), int(d["meta/x_seed"])
+    st = {}
+    for name in ("G1", "G2"):
+        s = fixture_state(template(name, 64), NET_SEED[name], "one")
+        assert abs(state_checksum(s) - float(d[f"{name}/checksum"])) < 1e-6 * float(d[f"{name}/checksum"])
+        st[name] = {k: v.clone().requires_grad_(not ref._is_buffer(k) and v.is_floating_point()) for k, v in s.items()}
+    x = uniform((bs, 3, hw, hw), xs).requires_grad_(True)
+    m = pm_one((bs, 1, hw, hw), xs + 1)
+    y = uniform((bs, 3, hw, hw), xs + 2)
+    mp = ref.generator_forward(st["G1"], x, True)
+    yp = ref.generator_forward(st["G2"], torch.cat((x, mp), 1), True)
+    d1, d2 = ref.data_loss(mp, m), ref.data_loss(yp, y)
+    (d1 + 5 * d2).backward()
+    assert abs(float(d1) - float(d["data1"])) <= 1e-6 and abs(float(d2) - float(d["data2"])) <= 1e-6
+    compare(d, "m_pred", mp.detach(), atol=1e-5)
+    compare(d, "y_pred", yp.detach(), atol=1e-5)
+    # fp32 vs fp32 in another summation order: the deep levels' BN at bs=2 (2x2 / 1x1 maps) is ill-conditioned,
+    # so the innermost gradients move by up to ~1.2e-2 of their RMS (measured); shallow ones by < 3e-3
+    compare_rel(d, "input_grad", x.grad, 1e-2)
+    for name in ("G1", "G2"):
+        for k, p in st[name].items():
+            if p.requires_grad:
+                compare_rel(d, f"{name}/grad/{k}", p.grad, 3e-2)
+            else:
+                compare(d, f"{name}/buf_after_train/{k}", p, atol=1e-5)
