@@ -145,9 +145,19 @@ int stc_conv_wgrad(int dtype, int B, int stride,
                    const float* g_scale, const float* g_shift, int g_act, float g_slope,
                    float* dW, void* workspace, int64_t workspace_bytes, void* stream);
 int64_t stc_conv_wgrad_workspace(int dtype, int B, int Hd, int Wd, int R, int Cg);
-/* Tuning / test hook: force the bf16 weight-gradient plan {tile config 0..5, pixel splits (0 = auto)}
- * of the following calls; cfg = -1 restores the automatic plan.  Process-global, not thread-safe. */
-int stc_conv_wgrad_force_plan(int cfg, int nsplit);
+/* The same with an optional per-call plan (tuning / tests): force_plan = {tile config 0..5, pixel
+ * splits (0 = auto)} for the bf16 LDS-DMA kernel, NULL = automatic.  No global state.
+ * stc_conv_wgrad_query: workspace bytes and plan_out[5] = {tile config (-1: fp32 / prologue kernel),
+ * BM, BN, pixel splits, slab (1: fp32 split slabs + the fixed-order transposing reduction)} for the
+ * same arguments (bf16 assumes the LDS-DMA kernel's eligibility: aligned NHWC views, no prologue). */
+int stc_conv_wgrad_ex(int dtype, int B, int stride,
+                      stc_view D, int R,
+                      const float* d_scale, const float* d_shift, int d_act, float d_slope,
+                      stc_view G, int Cg, int Cg_out,
+                      const float* g_scale, const float* g_shift, int g_act, float g_slope,
+                      float* dW, const int32_t* force_plan, void* workspace, int64_t workspace_bytes, void* stream);
+int stc_conv_wgrad_query(int dtype, int B, int Hd, int Wd, int R, int Cg, const int32_t* force_plan,
+                         int64_t* workspace_bytes, int32_t* plan_out);
 
 /* ---- weight packing ----------------------------------------------------------
  * W is a torch weight [P][Q][4][4] fp32.  out is [phases][N_pad][T][C_pad] of dtype.

@@ -3,6 +3,7 @@ one ST-CGAN train step (bs=32, 256x256).  Records the problems by running one st
 ops.wgrad, then times each forced (tile config, pixel splits) with HIP events over a captured HIP
 graph.  Prints one line per problem: the auto plan's time and the best forced plan.
 Output: JSON to argv[1]."""
+import ctypes
 import json
 import os
 import sys
@@ -61,42 +62,41 @@ def bench(prob, force, reps=10):
     g = (torch.randn((B, gh, gw, Cg), device=dev) * 0.5).to(BF)
     dv, gv = L.nhwc_view(d), L.nhwc_view(g)
     lib = L.lib()
-    if lib.stc_conv_wgrad_force_plan(force[0], force[1]) != 0:
+    fp = None if force is None else (ctypes.c_int32 * 2)(*force)
+    ws_b = ctypes.c_int64()
+    if lib.stc_conv_wgrad_query(L.BF16, B, dh, dw, R, Cg, fp, ctypes.byref(ws_b), None) != 0:
         return None
+    nbytes = ws_b.value
+    ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
+    dW = torch.empty((R, Cg_out, 4, 4), device=dev)
+
+    def call():
+        rc = lib.stc_conv_wgrad_ex(L.BF16, B, s, dv, R, None, None, 0, 0.0, gv, Cg, Cg_out, None, None, 0, 0.0,
+                                   L.ptr(dW), fp, L.ptr(ws), int(nbytes), L.stream())
+        if rc != 0:
+            raise RuntimeError(lib.stc_last_error().decode())
+
     try:
-        nbytes = lib.stc_conv_wgrad_workspace(L.BF16, B, dh, dw, R, Cg)
-        ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
-        dW = torch.empty((R, Cg_out, 4, 4), device=dev)
-
-        def call():
-            rc = lib.stc_conv_wgrad(L.BF16, B, s, dv, R, None, None, 0, 0.0, gv, Cg, Cg_out, None, None, 0, 0.0,
-                                    L.ptr(dW), L.ptr(ws), int(nbytes), L.stream())
-            if rc != 0:
-                raise RuntimeError(lib.stc_last_error().decode())
-
-        try:
-            call()
-            torch.cuda.synchronize()
-        except RuntimeError:
-            return None
-        gr = torch.cuda.CUDAGraph()
-        st = torch.cuda.Stream()
-        st.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(st):
-            with torch.cuda.graph(gr, stream=st):
-                for _ in range(reps):
-                    call()
+        call()
         torch.cuda.synchronize()
-        gr.replay()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        gr.replay()
-        e1.record()
-        e1.synchronize()
-        return e0.elapsed_time(e1) / reps * 1e3
-    finally:
-        lib.stc_conv_wgrad_force_plan(-1, 0)
+    except RuntimeError:
+        return None
+    gr = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(gr, stream=st):
+            for _ in range(reps):
+                call()
+    torch.cuda.synchronize()
+    gr.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    gr.replay()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
 
 
 def main():

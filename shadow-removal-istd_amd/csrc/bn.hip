@@ -175,23 +175,20 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int
                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  double n = 0, sm = 0;
-  for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {
+  double n = 0, sm = 0, m2 = 0;
+  if (nchunks <= 1024) {
+    // one load: every thread keeps its (up to) 4 chunk partials in registers for both passes
     float4 pp[4];
-    load4(k0, pp);
+    load4(threadIdx.x, pp);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (pp[u].x <= 0.f) continue;
       n += pp[u].x;
       sm += (double)pp[u].x * pp[u].w + (double)pp[u].y;  // n_b * m_b = n_b*shift + S1
     }
-  }
-  const double N = block_sum256(n, sh);
-  const double mu = N > 0 ? block_sum256(sm, sh) / N : (block_sum256(sm, sh), 0.0);
-  double m2 = 0;
-  for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {
-    float4 pp[4];
-    load4(k0, pp);
+    const double N = block_sum256(n, sh);
+    const double S = block_sum256(sm, sh);
+    const double mu = N > 0 ? S / N : 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (pp[u].x <= 0.f) continue;
@@ -201,7 +198,39 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int
       const double d = (double)pp[u].w + r - mu;
       m2 += q + nb * d * d;
     }
+    n = N;
+    sm = mu;
+  } else {
+    for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {
+      float4 pp[4];
+      load4(k0, pp);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pp[u].x <= 0.f) continue;
+        n += pp[u].x;
+        sm += (double)pp[u].x * pp[u].w + (double)pp[u].y;
+      }
+    }
+    const double N = block_sum256(n, sh);
+    const double S = block_sum256(sm, sh);
+    const double mu = N > 0 ? S / N : 0.0;
+    for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {
+      float4 pp[4];
+      load4(k0, pp);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pp[u].x <= 0.f) continue;
+        const double nb = pp[u].x, s1 = pp[u].y, r = s1 / nb;
+        double q = (double)pp[u].z - s1 * r;
+        if (q < 0) q = 0;
+        const double d = (double)pp[u].w + r - mu;
+        m2 += q + nb * d * d;
+      }
+    }
+    n = N;
+    sm = mu;
   }
+  const double N = n, mu = sm;
   const double M2 = block_sum256(m2, sh);
   if (threadIdx.x == 0) {
     const double var = N > 0 ? M2 / N : 0.0;
@@ -343,7 +372,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* part,
   }
 }
 
-template <typename T>
+template <typename T, bool DENSE>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, PixDiv pd, long long P, int C, const float* scale,
                                                            const float* shift, const float* mean, const float* rstd,
                                                            const float* gamma, GradIn gi, const float* dgamma,
@@ -351,6 +380,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, PixDiv pd, lo
   constexpr int N = VW<T>::N;
   const int CG = C / N;
   const long long total = P * CG;
+  const long long stride = (long long)gridDim.x * blockDim.x;
   const float invP = 1.f / (float)P;
   // per-channel coefficients of this thread's channel group, reloaded only when the group changes
   // (never, when the grid stride is a multiple of CG -- the usual power-of-two channel counts):
@@ -358,42 +388,88 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, PixDiv pd, lo
   // k0 = k1*(dbeta/P - mean*rstd*dgamma/P)
   int cg_have = -1;
   float sc[N], sh[N], k0[N], k1[N], k2[N];
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
+  auto table = [&](int cg) {
+    if (cg == cg_have) return;
+    cg_have = cg;
+    const int c = N * cg;
+    if (scale) { ldc<N>(scale + c, sc); ldc<N>(shift + c, sh); }
+    else {
+#pragma unroll
+      for (int e = 0; e < N; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+    }
+    if (mean) {
+      float mu[N], rs[N], gm[N], dg[N], db[N];
+      ldc<N>(mean + c, mu); ldc<N>(rstd + c, rs); ldc<N>(gamma + c, gm); ldc<N>(dgamma + c, dg); ldc<N>(dbeta + c, db);
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        k1[e] = gm[e] * rs[e];
+        k2[e] = k1[e] * rs[e] * dg[e] * invP;
+        k0[e] = k1[e] * (db[e] * invP - mu[e] * rs[e] * dg[e] * invP);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < N; ++e) { k1[e] = 1.f; k2[e] = 0.f; k0[e] = 0.f; }
+    }
+  };
+  struct Off {
+    long long x, g1, g2, dx;
+    int c;
+  };
+  auto offs = [&](long long idx) {
+    Off o;
     const int cg = (int)(idx % CG);
     const long long pix = idx / CG;
-    const int c = N * cg;
-    if (cg != cg_have) {
-      cg_have = cg;
-      if (scale) { ldc<N>(scale + c, sc); ldc<N>(shift + c, sh); }
-      else {
-#pragma unroll
-        for (int e = 0; e < N; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
-      }
-      if (mean) {
-        float mu[N], rs[N], gm[N], dg[N], db[N];
-        ldc<N>(mean + c, mu); ldc<N>(rstd + c, rs); ldc<N>(gamma + c, gm); ldc<N>(dgamma + c, dg); ldc<N>(dbeta + c, db);
-#pragma unroll
-        for (int e = 0; e < N; ++e) {
-          k1[e] = gm[e] * rs[e];
-          k2[e] = k1[e] * rs[e] * dg[e] * invP;
-          k0[e] = k1[e] * (db[e] * invP - mu[e] * rs[e] * dg[e] * invP);
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < N; ++e) { k1[e] = 1.f; k2[e] = 0.f; k0[e] = 0.f; }
-      }
+    o.c = N * cg;
+    if constexpr (DENSE) {
+      o.x = pix * x.ps + x.co + o.c;
+      o.g1 = pix * gi.g1.ps + gi.g1.co + o.c;
+      o.g2 = pix * gi.g2.ps + gi.g2.co + o.c;
+      o.dx = pix * dx.ps + dx.co + o.c;
+    } else {
+      int b, yy, xx;
+      pix_bxy(pd, pix, b, yy, xx);
+      o.x = vidx(x, b, yy, xx, o.c);
+      o.g1 = vidx(gi.g1, b, yy, xx, o.c);
+      o.g2 = vidx(gi.g2, b, yy, xx, o.c);
+      o.dx = vidx(dx, b, yy, xx, o.c);
     }
-    int b, yy, xx;
-    pix_bxy(pd, pix, b, yy, xx);
-    float v[N], n[N], d[N];
-    VW<T>::load(vptr<T>(x, b, yy, xx, c), v);
+    return o;
+  };
+  struct In {
+    float v[N], g1[N], g2[N];
+  };
+  auto load = [&](const Off& o, In& in) {
+    VW<T>::load(reinterpret_cast<const T*>(x.p) + o.x, in.v);
+    if (gi.has1) VW<T>::load(reinterpret_cast<const T*>(gi.g1.p) + o.g1, in.g1);
+    if (gi.has2) VW<T>::load(reinterpret_cast<const T*>(gi.g2.p) + o.g2, in.g2);
+  };
+  auto emit = [&](const Off& o, const In& in) {
+    table(o.c / N);
+    float d[N];
 #pragma unroll
-    for (int e = 0; e < N; ++e) n[e] = fmaf(v[e], sc[e], sh[e]);
-    dn_of<T>(gi, b, yy, xx, c, n, d);
-#pragma unroll
-    for (int e = 0; e < N; ++e) d[e] = fmaf(k1[e], d[e], -fmaf(k2[e], v[e], k0[e]));
-    VW<T>::store(reinterpret_cast<T*>(dx.p) + vidx(dx, b, yy, xx, c), d);
+    for (int e = 0; e < N; ++e) {
+      const float n = fmaf(in.v[e], sc[e], sh[e]);
+      float dn = 0.f;
+      if (gi.has1) dn += in.g1[e] * dact(n, gi.s1);
+      if (gi.has2) dn += in.g2[e] * dact(n, gi.s2);
+      d[e] = fmaf(k1[e], dn, -fmaf(k2[e], in.v[e], k0[e]));
+    }
+    VW<T>::store(reinterpret_cast<T*>(dx.p) + o.dx, d);
+  };
+  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; idx + stride < total; idx += 2 * stride) {  // both elements' loads in flight before either is used
+    const Off oa = offs(idx), ob = offs(idx + stride);
+    In a, b;
+    load(oa, a);
+    load(ob, b);
+    emit(oa, a);
+    emit(ob, b);
+  }
+  if (idx < total) {
+    const Off oa = offs(idx);
+    In a;
+    load(oa, a);
+    emit(oa, a);
   }
 }
 
@@ -402,42 +478,76 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, PixDiv pd, lo
 // LeakyReLU of the reference, 1 = identity).  Applied once per element, so the GEMMs
 // that consume y1/y2 (each input element is re-read 4-16x by the im2col) stage plain
 // operands with no per-load transform.
-template <typename T>
+template <typename T, bool DENSE>
 __global__ void __launch_bounds__(256) bn_apply_kernel(View x, PixDiv pd, long long P, int C, const float* scale,
                                                        const float* shift, View y1, float s1, View y2, float s2,
                                                        int has2) {
   constexpr int N = VW<T>::N;
   const int CG = C / N;
   const long long total = P * CG;
+  const long long stride = (long long)gridDim.x * blockDim.x;
   int cg_have = -1;
   float sc[N], sh[N];
-  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
+  auto table = [&](int cg) {  // this thread's channel group's table, reloaded only when it changes
+    if (cg == cg_have) return;
+    cg_have = cg;
+    if (scale) { ldc<N>(scale + N * cg, sc); ldc<N>(shift + N * cg, sh); }
+    else {
+#pragma unroll
+      for (int e = 0; e < N; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+    }
+  };
+  auto offs = [&](long long idx, long long& ox, long long& o1, long long& o2, int& c) {
     const int cg = (int)(idx % CG);
     const long long pix = idx / CG;
-    const int c = N * cg;
-    if (cg != cg_have) {  // this thread's channel group's table, reloaded only when it changes
-      cg_have = cg;
-      if (scale) { ldc<N>(scale + c, sc); ldc<N>(shift + c, sh); }
-      else {
-#pragma unroll
-        for (int e = 0; e < N; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
-      }
+    c = N * cg;
+    if constexpr (DENSE) {  // every view dense in pixels: element (pix, c) at pix*ps + co + c
+      ox = pix * x.ps + x.co + c;
+      o1 = pix * y1.ps + y1.co + c;
+      o2 = pix * y2.ps + y2.co + c;
+    } else {
+      int b, yy, xx;
+      pix_bxy(pd, pix, b, yy, xx);
+      ox = vidx(x, b, yy, xx, c);
+      o1 = vidx(y1, b, yy, xx, c);
+      o2 = vidx(y2, b, yy, xx, c);
     }
-    int b, yy, xx;
-    pix_bxy(pd, pix, b, yy, xx);
+  };
+  auto emit = [&](const float* v0, long long o1, long long o2) {
     float v[N], o[N];
-    VW<T>::load(vptr<T>(x, b, yy, xx, c), v);
 #pragma unroll
-    for (int e = 0; e < N; ++e) v[e] = fmaf(v[e], sc[e], sh[e]);
+    for (int e = 0; e < N; ++e) v[e] = fmaf(v0[e], sc[e], sh[e]);
 #pragma unroll
     for (int e = 0; e < N; ++e) o[e] = act(v[e], s1);
-    VW<T>::store(reinterpret_cast<T*>(y1.p) + vidx(y1, b, yy, xx, c), o);
+    VW<T>::store(reinterpret_cast<T*>(y1.p) + o1, o);
     if (has2) {
 #pragma unroll
       for (int e = 0; e < N; ++e) o[e] = act(v[e], s2);
-      VW<T>::store(reinterpret_cast<T*>(y2.p) + vidx(y2, b, yy, xx, c), o);
+      VW<T>::store(reinterpret_cast<T*>(y2.p) + o2, o);
     }
+  };
+  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; idx + stride < total; idx += 2 * stride) {  // two 16-byte loads in flight per thread
+    long long ax, a1, a2, bx, b1, b2;
+    int ca, cb;
+    offs(idx, ax, a1, a2, ca);
+    offs(idx + stride, bx, b1, b2, cb);
+    float va[N], vb[N];
+    VW<T>::load(reinterpret_cast<const T*>(x.p) + ax, va);
+    VW<T>::load(reinterpret_cast<const T*>(x.p) + bx, vb);
+    table(ca / N);
+    emit(va, a1, a2);
+    table(cb / N);
+    emit(vb, b1, b2);
+  }
+  if (idx < total) {
+    long long ax, a1, a2;
+    int ca;
+    offs(idx, ax, a1, a2, ca);
+    float va[N];
+    VW<T>::load(reinterpret_cast<const T*>(x.p) + ax, va);
+    table(ca / N);
+    emit(va, a1, a2);
   }
 }
 
@@ -510,6 +620,9 @@ using namespace stc;
 
 extern "C" int stc_chan_stats_chunks(int B, int H, int W) { return stat_chunks((long long)B * H * W); }
 
+// pixel-dense view: rows and images follow each other without gaps, so pixel p sits at p * ps
+static bool pix_dense(const stc_view& v) { return v.rs == (int64_t)v.W * v.ps && v.bs == (int64_t)v.H * v.rs; }
+
 static bool vec_ok(int dtype, int C, const stc_view& v) {
   const int N = dtype == STC_F32 ? 4 : 8;
   return C % N == 0 && C / N <= 256 && v.cs == 1 && v.co % N == 0 && v.ps % N == 0 && v.rs % N == 0 && v.bs % N == 0;
@@ -538,10 +651,12 @@ extern "C" int stc_bn_apply(int dtype, int B, stc_view x, int C, const float* sc
   const long long P = (long long)B * x.H * x.W;
   const int N = dtype == STC_F32 ? 4 : 8;
   const int blocks = grid_for(P * (C / N));
-  if (dtype == STC_F32)
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(blocks), dim3(256), 0, st, v, pd, P, C, scale, shift, o1, slope1, o2, slope2, y2.p != nullptr ? 1 : 0);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(blocks), dim3(256), 0, st, v, pd, P, C, scale, shift, o1, slope1, o2, slope2, y2.p != nullptr ? 1 : 0);
+  const bool dense = pix_dense(x) && pix_dense(y1) && (!y2.p || pix_dense(y2));
+  const int h2 = y2.p != nullptr ? 1 : 0;
+#define STC_BA(T_, D_) hipLaunchKernelGGL((bn_apply_kernel<T_, D_>), dim3(blocks), dim3(256), 0, st, v, pd, P, C, scale, shift, o1, slope1, o2, slope2, h2)
+  if (dtype == STC_F32) { if (dense) STC_BA(float, true); else STC_BA(float, false); }
+  else { if (dense) STC_BA(bf16, true); else STC_BA(bf16, false); }
+#undef STC_BA
   STC_CHECK_LAUNCH();
   return 0;
 }
@@ -615,10 +730,11 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
   const PixDiv pd = mkpix(B, x.H, x.W);
   const long long P = (long long)B * x.H * x.W;
   const long long work = P * (C / (dtype == STC_F32 ? 4 : 8));
-  if (dtype == STC_F32)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(grid_for(work)), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(grid_for(work)), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o);
+  const bool dense = pix_dense(x) && pix_dense(dx) && (!g1.p || pix_dense(g1)) && (!g2.p || pix_dense(g2));
+#define STC_BB(T_, D_) hipLaunchKernelGGL((bn_bwd_apply_kernel<T_, D_>), dim3(grid_for(work)), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o)
+  if (dtype == STC_F32) { if (dense) STC_BB(float, true); else STC_BB(float, false); }
+  else { if (dense) STC_BB(bf16, true); else STC_BB(bf16, false); }
+#undef STC_BB
   STC_CHECK_LAUNCH();
   return 0;
 }

@@ -273,28 +273,43 @@ wgrad_kernel(const WgradParams p) {
 
 // dW[r][ci][kh][kw] = sum_s ws[s][r][(kh*4+kw)*Cg + ci]: one thread per (r, tap, ci) with ci fastest
 // (coalesced slab reads), the splits summed in a fixed order with 4 independent partial sums.
-__global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int R, int Cg, int Cg_out, float* dW) {
-  const long long total = (long long)R * 16 * Cg_out;
+// Fixed-order sum of the split slabs (row-major [split][R][16*Cg], GEMM column n = tap*Cg + ci) into
+// torch layout dW[R][Cg_out][16].  One thread = (r, ci, 4 consecutive taps): it reads each slab at
+// columns tap*Cg + ci (consecutive threads -> consecutive ci, coalesced) and writes the 4 taps as one
+// float4, so a warp's stores are one contiguous run of dW (the transposition costs no scattered stores).
+__global__ void __launch_bounds__(128) wgrad_reduce_kernel(const float* __restrict__ ws, int nsplit, int R, int Cg,
+                                                           int Cg_out, float* __restrict__ dW) {
+  const long long total = (long long)R * Cg_out * 4;
   const long long Ncol = 16LL * Cg;
   const long long slab = (long long)R * Ncol;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
-    const int ci = (int)(idx % Cg_out);
-    const long long rt = idx / Cg_out;
-    const int tap = (int)(rt & 15);
-    const int r = (int)(rt >> 4);
-    const float* src = ws + (long long)r * Ncol + (long long)tap * Cg + ci;
-    float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+    const int g = (int)(idx & 3);
+    const long long rc = idx >> 2;
+    const int ci = (int)(rc % Cg_out);
+    const int r = (int)(rc / Cg_out);
+    const float* src = ws + (long long)r * Ncol + (long long)(4 * g) * Cg + ci;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int sp = 0;
-    for (; sp + 4 <= nsplit; sp += 4) {
-      v0 += src[(long long)sp * slab];
-      v1 += src[(long long)(sp + 1) * slab];
-      v2 += src[(long long)(sp + 2) * slab];
-      v3 += src[(long long)(sp + 3) * slab];
+    for (; sp + 2 <= nsplit; sp += 2) {  // two slabs' loads in flight; the sum order stays split order
+      const float* a = src + (long long)sp * slab;
+      const float* b = a + slab;
+      const float a0 = a[0], a1 = a[Cg], a2 = a[2 * Cg], a3 = a[3 * Cg];
+      const float b0 = b[0], b1 = b[Cg], b2 = b[2 * Cg], b3 = b[3 * Cg];
+      acc.x += a0; acc.y += a1; acc.z += a2; acc.w += a3;
+      acc.x += b0; acc.y += b1; acc.z += b2; acc.w += b3;
     }
-    for (; sp < nsplit; ++sp) v0 += src[(long long)sp * slab];
-    dW[((long long)r * Cg_out + ci) * 16 + tap] = (v0 + v1) + (v2 + v3);
+    for (; sp < nsplit; ++sp) {
+      const float* a = src + (long long)sp * slab;
+      acc.x += a[0]; acc.y += a[Cg]; acc.z += a[2 * Cg]; acc.w += a[3 * Cg];
+    }
+    *reinterpret_cast<float4*>(dW + ((long long)r * Cg_out + ci) * 16 + 4 * g) = acc;
   }
+}
+
+int64_t wgrad_reduce_blocks(int R, int Cg_out) {
+  const long long total = (long long)R * Cg_out * 4;
+  return std::min<long long>((total + 127) / 128, 16384);
 }
 
 struct WgPlan {
@@ -317,19 +332,35 @@ static WgPlan wg_plan(int P, int R, int Cg) {
 
 namespace stc {
 bool wgrad_bf16_eligible(int B, const stc_view& D, int R, const stc_view& G, int Cg);
-int64_t wgrad_bf16_workspace(int B, int Hd, int Wd, int R, int Cg);
+int64_t wgrad_bf16_workspace(int B, int Hd, int Wd, int R, int Cg, const int32_t* force);
+void wgrad_bf16_plan(int B, int Hd, int Wd, int R, int Cg, const int32_t* force, int32_t* plan_out);
 int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_out, float* dW, void* workspace,
-               int64_t workspace_bytes, hipStream_t st);
+               int64_t workspace_bytes, hipStream_t st, const int32_t* force);
 }  // namespace stc
 
 using namespace stc;
 
-extern "C" int64_t stc_conv_wgrad_workspace(int dtype, int B, int Hd, int Wd, int R, int Cg) {
+extern "C" int stc_conv_wgrad_query(int dtype, int B, int Hd, int Wd, int R, int Cg, const int32_t* force_plan,
+                                    int64_t* workspace_bytes, int32_t* plan_out) {
   const WgPlan pl = wg_plan(B * Hd * Wd, R, Cg);
   const int64_t ws_reg = pl.nsplit <= 1 ? 0 : (int64_t)pl.nsplit * R * 16LL * Cg * 4;  // 0: straight into dW
   // bf16 without prologues runs the LDS-DMA kernel (wgrad_bf16.hip); the prologue form the register-staged one
-  const int64_t ws_dma = dtype == STC_BF16 ? wgrad_bf16_workspace(B, Hd, Wd, R, Cg) : 0;
-  return std::max(ws_reg, ws_dma);
+  const int64_t ws_dma = dtype == STC_BF16 ? wgrad_bf16_workspace(B, Hd, Wd, R, Cg, force_plan) : 0;
+  if (workspace_bytes) *workspace_bytes = std::max(ws_reg, ws_dma);
+  if (plan_out) {
+    if (dtype == STC_BF16) {
+      wgrad_bf16_plan(B, Hd, Wd, R, Cg, force_plan, plan_out);
+    } else {
+      plan_out[0] = -1; plan_out[1] = WG_BM; plan_out[2] = WG_BN; plan_out[3] = pl.nsplit; plan_out[4] = pl.nsplit > 1;
+    }
+  }
+  return 0;
+}
+
+extern "C" int64_t stc_conv_wgrad_workspace(int dtype, int B, int Hd, int Wd, int R, int Cg) {
+  int64_t ws = 0;
+  stc_conv_wgrad_query(dtype, B, Hd, Wd, R, Cg, nullptr, &ws, nullptr);
+  return ws;
 }
 
 extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
@@ -337,6 +368,16 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
                               stc_view G, int Cg, int Cg_out,
                               const float* g_scale, const float* g_shift, int g_act, float g_slope,
                               float* dW, void* workspace, int64_t workspace_bytes, void* stream) {
+  return stc_conv_wgrad_ex(dtype, B, stride, D, R, d_scale, d_shift, d_act, d_slope, G, Cg, Cg_out, g_scale, g_shift,
+                           g_act, g_slope, dW, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int stc_conv_wgrad_ex(int dtype, int B, int stride, stc_view D, int R,
+                                 const float* d_scale, const float* d_shift, int d_act, float d_slope,
+                                 stc_view G, int Cg, int Cg_out,
+                                 const float* g_scale, const float* g_shift, int g_act, float g_slope,
+                                 float* dW, const int32_t* force_plan, void* workspace, int64_t workspace_bytes,
+                                 void* stream) {
   STC_REQUIRE(dtype == STC_F32 || dtype == STC_BF16, "stc_conv_wgrad: bad dtype");
   const int VEC = dtype == STC_F32 ? 4 : 8;
   STC_REQUIRE(Cg >= VEC && Cg % VEC == 0, "stc_conv_wgrad: Cg=%d must be a multiple of %d", Cg, VEC);
@@ -359,7 +400,7 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
     return 0;
   }
   if (dtype == STC_BF16 && !d_scale && !d_act && !g_scale && !g_act && wgrad_bf16_eligible(B, D, R, G, Cg))
-    return wgrad_bf16(B, stride, D, R, G, Cg, Cg_out, dW, workspace, workspace_bytes, st);
+    return wgrad_bf16(B, stride, D, R, G, Cg, Cg_out, dW, workspace, workspace_bytes, st, force_plan);
   const WgPlan pl = wg_plan(p.P, R, Cg);
   p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.nsplit = pl.nsplit; p.pchunk = pl.pchunk;
   p.Cg_out = Cg_out;
@@ -382,10 +423,8 @@ extern "C" int stc_conv_wgrad(int dtype, int B, int stride, stc_view D, int R,
   else hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, p);
   main_timer_end(st);
   STC_CHECK_LAUNCH();
-  const long long total = (long long)R * 16 * Cg_out;
-  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)p.ws, pl.nsplit, R, Cg,
-                     Cg_out, dW);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)wgrad_reduce_blocks(R, Cg_out)), dim3(128), 0, st,
+                     (const float*)p.ws, pl.nsplit, R, Cg, Cg_out, dW);
   STC_CHECK_LAUNCH();
   return 0;
 }

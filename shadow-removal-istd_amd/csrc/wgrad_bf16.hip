@@ -14,7 +14,7 @@
 // 128x128 tile: the L2->LDS stream, not the MFMA, bounds the small tiles).  2-stage ring (DMA of
 // step s+1 under the MFMAs of step s).  The pixel range is split over blockIdx.z into fp32 slabs
 // that wgrad_reduce_kernel sums in a fixed order; a single split writes torch layout directly.
-#include <atomic>
+#include <algorithm>
 
 #include "common.hpp"
 
@@ -31,6 +31,11 @@ struct WbParams {
   int R, Cg, Ncol, Cg_out;
   int P, pchunk, nsplit;
   float inv_ghw, inv_gw;  // fast exact division by GH*GW and GW (p < 2^24)
+  // pixel mapping of a 64-pixel K-step (host-chosen, wb_pmode): 0 general (per-lane division every
+  // step); 1 a step stays inside one image row (GW % 64 == 0); 2 a step is whole rows of one image
+  // (GW | 64, 64 | GH*GW); 3 a step is whole images (GH*GW | 64).  Modes 1-3: lane pixel = the step's
+  // (b0, oy0, ox0), advanced in scalar registers, plus a per-lane constant -- no per-step VALU division.
+  int pmode, lg_gw, lg_ghw;
   int mtiles, ntiles;
   float* ws;
   float* dW;
@@ -78,7 +83,7 @@ constexpr int WB_BK = 64;
 // D (plain pixel-major channels r) or Gcol (im2col columns tap*Cg + ci).  SWAP = false: rows = D
 // (r), columns = Gcol; SWAP = true (R <= 16): rows = Gcol, columns = D, so the tiny R dimension
 // becomes a 16-wide MFMA N tile instead of wasting 7/8 of a 128-row tile.
-template <int BM, int BN, int WM, int WN, bool SWAP>
+template <int BM, int BN, int WM, int WN, bool SWAP, bool FAST>
 __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams p) {
   constexpr int NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -176,10 +181,94 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
     }
   };
 
+  // ---- fast mapping (pmode 1..3): per-piece lane constants; the step base lives in scalar registers
+  struct Lc {
+    unsigned off;  // element offset of this lane's source relative to the step base (wraps mod 2^32)
+    int cy, cx;    // G: tap-shifted pixel coordinates relative to (oy0*s, ox0*s); a column past Ncol
+                   // gets cy = 2^30, so the bounds check that every G piece makes rejects it
+    unsigned pen;  // D: the row penalty (r >= R)
+  };
+  auto lane_const = [&](bool is_g, const Role& ro, int rows_pp, int piece) -> Lc {
+    const int d = piece * rows_pp + lane / (64 / rows_pp);
+    int db = 0, doy = 0, dox = d;
+    if (p.pmode == 2) { doy = d >> p.lg_gw; dox = d & (p.GW - 1); }
+    else if (p.pmode == 3) { db = d >> p.lg_ghw; const int r = d & (GHW - 1); doy = r >> p.lg_gw; dox = r & (p.GW - 1); }
+    Lc c;
+    if (!is_g) {
+      c.off = (unsigned)db * (unsigned)p.d_bs + (unsigned)doy * (unsigned)p.d_rs + (unsigned)dox * (unsigned)p.d_ps +
+              (unsigned)ro.chan_off;
+      c.cy = 0; c.cx = 0;
+      c.pen = ro.pen;
+    } else {
+      c.cy = doy * p.stride + ro.dy;
+      c.cx = dox * p.stride + ro.dx;
+      c.off = (unsigned)db * (unsigned)p.g_bs + (unsigned)c.cy * (unsigned)p.g_rs + (unsigned)c.cx * (unsigned)p.g_ps +
+              (unsigned)ro.chan_off;
+      if (ro.pen) c.cy = 1 << 30;
+      c.pen = 0;
+    }
+    return c;
+  };
+  Lc la_[IA], lb_[IB];
+  if constexpr (FAST) {
+#pragma unroll
+    for (int i = 0; i < IA; ++i) la_[i] = lane_const(SWAP, ra_[i], 64 / CHA, wave + NW * i);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) lb_[i] = lane_const(!SWAP, rb_[i], 64 / CHB, wave + NW * i);
+  }
+  // scalar step base (sb0, soy0, sox0) of pixel pbeg, advanced by 64 pixels per issued step
+  int sb0 = 0, soy0 = 0, sox0 = 0;
+  if constexpr (FAST) {
+    sb0 = pbeg / GHW;
+    const int r0 = pbeg - sb0 * GHW;
+    soy0 = r0 / p.GW;
+    sox0 = r0 - soy0 * p.GW;
+  }
+  auto fast_piece = [&](bool is_g, int rows_pp, const Lc& c, unsigned sbase, int sy, int sx, unsigned tail,
+                        int piece, char* dst) {
+    unsigned pen = is_g ? 0u : c.pen;
+    if (tail) {  // only the last, partial step of the range
+      const int d = piece * rows_pp + lane / (64 / rows_pp);
+      pen |= (unsigned)d < tail ? 0u : OOBV;
+    }
+    if (!is_g) {
+      wdma16(rd, dst + piece * 1024, ((sbase + c.off) * 2u) | pen);
+    } else {
+      const unsigned ipen = ((unsigned)(sy + c.cy) < (unsigned)p.IH && (unsigned)(sx + c.cx) < (unsigned)p.IW) ? 0u : OOBV;
+      wdma16(rg, dst + piece * 1024, ((sbase + c.off) * 2u) | pen | ipen);
+    }
+  };
+
   auto issue = [&](int s, int stage) {
     char* sA = smem + stage * STAGE;
     char* sB = sA + TILEA;
-    if constexpr (CHA == CHB && IA == IB) {  // A and B pieces cover the same pixel rows
+    if constexpr (FAST) {
+      const int p0 = pbeg + s * WB_BK;
+      const unsigned tail = p0 + WB_BK > pend ? (unsigned)(pend - p0) : 0u;
+      const int sy = soy0 * p.stride, sx = sox0 * p.stride;
+      const unsigned sd = (unsigned)sb0 * (unsigned)p.d_bs + (unsigned)soy0 * (unsigned)p.d_rs + (unsigned)sox0 * (unsigned)p.d_ps;
+      const unsigned sg = (unsigned)sb0 * (unsigned)p.g_bs + (unsigned)sy * (unsigned)p.g_rs + (unsigned)sx * (unsigned)p.g_ps;
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const int pc = wave + NW * i;
+        if (pc < PA) fast_piece(SWAP, 64 / CHA, la_[i], SWAP ? sg : sd, sy, sx, tail, pc, sA);
+      }
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int pc = wave + NW * i;
+        if (pc < PB) fast_piece(!SWAP, 64 / CHB, lb_[i], SWAP ? sd : sg, sy, sx, tail, pc, sB);
+      }
+      // advance the base by one step (64 pixels)
+      if (p.pmode == 1) {
+        sox0 += WB_BK;
+        if (sox0 >= p.GW) { sox0 = 0; if (++soy0 >= p.GH) { soy0 = 0; ++sb0; } }
+      } else if (p.pmode == 2) {
+        soy0 += WB_BK >> p.lg_gw;
+        if (soy0 >= p.GH) { soy0 = 0; ++sb0; }
+      } else {
+        sb0 += WB_BK >> p.lg_ghw;
+      }
+    } else if constexpr (CHA == CHB && IA == IB) {  // A and B pieces cover the same pixel rows
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
         const int pc = wave + NW * i;
@@ -317,19 +406,20 @@ constexpr WbCfg kWbCfg[] = {
 };
 constexpr int kNumWbCfg = sizeof(kWbCfg) / sizeof(kWbCfg[0]);
 
-// tuning / test hook (stc_conv_wgrad_force_plan): -1 = automatic plan
-static std::atomic<int> g_wb_force_cfg{-1}, g_wb_force_ns{0};
 
 struct WbPlan {
   int cfg, BM, BN, mtiles, ntiles, nsplit, pchunk;
+  bool slab;  // partial sums go to fp32 slabs + wgrad_reduce_kernel (always when nsplit > 1)
 };
 
-static WbPlan wb_plan(int P, int R, int Cg) {
+// force (optional, per call: stc_conv_wgrad_ex / stc_conv_wgrad_query): {tile config 0..5, pixel
+// splits (0 = auto)}; NULL or a config outside 0..5 = the automatic plan
+static WbPlan wb_plan(int P, int R, int Cg, const int32_t* force) {
   WbPlan pl{};
   const long long ncol = 16LL * Cg;
   const int steps = cdiv(P, WB_BK);
-  int cfg = g_wb_force_cfg.load(std::memory_order_relaxed);
-  int force_ns = g_wb_force_ns.load(std::memory_order_relaxed);
+  int cfg = force ? force[0] : -1;
+  int force_ns = force ? std::max(force[1], 0) : 0;
   if (cfg < 0 || cfg >= kNumWbCfg) {
     force_ns = 0;
     // (fitted to scripts/tune_wgrad.py over one train step: the 8-wave tiles pay off once each
@@ -357,6 +447,10 @@ static WbPlan wb_plan(int P, int R, int Cg) {
   }
   pl.pchunk = cdiv(steps, ns) * WB_BK;
   pl.nsplit = cdiv(P, pl.pchunk);
+  // A single split writes torch layout dW[r][ci][tap] from the tile directly only when a tile column
+  // range covers every tap of its channels (16*Cg <= BN); otherwise those stores are 4-byte scatters at
+  // a 64-byte stride (measured ~30 us for a 16.8 MB dW) and the slab + coalesced transposing reduce wins.
+  pl.slab = pl.nsplit > 1 || (!c.swap && 16LL * Cg > c.BN);
   return pl;
 }
 
@@ -367,16 +461,24 @@ bool wgrad_bf16_eligible(int B, const stc_view& D, int R, const stc_view& G, int
          G.ps % 8 == 0 && dbytes < (1ll << 31) && gbytes < (1ll << 31) && P < (1 << 24);
 }
 
-int64_t wgrad_bf16_workspace(int B, int Hd, int Wd, int R, int Cg) {
-  const WbPlan pl = wb_plan(B * Hd * Wd, R, Cg);
-  if (pl.nsplit <= 1) return 0;
+int64_t wgrad_bf16_workspace(int B, int Hd, int Wd, int R, int Cg, const int32_t* force) {
+  const WbPlan pl = wb_plan(B * Hd * Wd, R, Cg, force);
+  if (!pl.slab) return 0;
   return (int64_t)pl.nsplit * R * 16LL * Cg * 4;
 }
 
-__global__ void wgrad_reduce_kernel(const float* ws, int nsplit, int R, int Cg, int Cg_out, float* dW);
+__global__ void __launch_bounds__(128) wgrad_reduce_kernel(const float* ws, int nsplit, int R, int Cg, int Cg_out,
+                                                           float* dW);
+int64_t wgrad_reduce_blocks(int R, int Cg_out);
+
+// plan_out = {tile config, BM, BN, pixel splits, slab (1: slabs + reduce kernel)}
+void wgrad_bf16_plan(int B, int Hd, int Wd, int R, int Cg, const int32_t* force, int32_t* plan_out) {
+  const WbPlan pl = wb_plan(B * Hd * Wd, R, Cg, force);
+  plan_out[0] = pl.cfg; plan_out[1] = pl.BM; plan_out[2] = pl.BN; plan_out[3] = pl.nsplit; plan_out[4] = pl.slab;
+}
 
 int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_out, float* dW, void* workspace,
-               int64_t workspace_bytes, hipStream_t st) {
+               int64_t workspace_bytes, hipStream_t st, const int32_t* force) {
   WbParams p{};
   p.d = (const char*)D.p; p.d_bytes = (unsigned)((long long)B * D.bs * 2);
   p.d_bs = (int)D.bs; p.d_rs = (int)D.rs; p.d_ps = D.ps; p.d_co = D.co;
@@ -387,11 +489,21 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
   p.P = B * D.H * D.W;
   p.inv_ghw = 1.0f / (float)(D.H * D.W);
   p.inv_gw = 1.0f / (float)D.W;
-  const WbPlan pl = wb_plan(p.P, R, Cg);
+  {
+    auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
+    const int ghw = D.H * D.W, lgw = lg2(D.W), lghw = lg2(ghw);
+    p.pmode = 0;
+    if (D.W % WB_BK == 0) p.pmode = 1;
+    else if (lgw >= 0 && ghw % WB_BK == 0) p.pmode = 2;
+    else if (lghw >= 0 && lgw >= 0 && WB_BK % ghw == 0) p.pmode = 3;
+    p.lg_gw = lgw < 0 ? 0 : lgw;
+    p.lg_ghw = lghw < 0 ? 0 : lghw;
+  }
+  const WbPlan pl = wb_plan(p.P, R, Cg, force);
   p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.nsplit = pl.nsplit; p.pchunk = pl.pchunk;
   dim3 grid(pl.mtiles * pl.ntiles, 1, pl.nsplit);
   const size_t lds = 2 * (size_t)WB_BK * (pl.BM + pl.BN) * 2;
-  if (pl.nsplit <= 1) {
+  if (!pl.slab) {
     p.dW = dW;
   } else {
     const int64_t need = (int64_t)pl.nsplit * R * 16LL * Cg * 4;
@@ -400,33 +512,27 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
     p.ws = (float*)workspace;
   }
   main_timer_begin(st);
+#define STC_WB(BM_, BN_, WM_, WN_, SW_, T_)                                                                   \
+  if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_kernel<BM_, BN_, WM_, WN_, SW_, true>), grid, dim3(T_), lds, st, p); \
+  else hipLaunchKernelGGL((wgrad_bf16_kernel<BM_, BN_, WM_, WN_, SW_, false>), grid, dim3(T_), lds, st, p);
   switch (pl.cfg) {
-    case 0: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false>), grid, dim3(256), lds, st, p); break;
-    case 1: hipLaunchKernelGGL((wgrad_bf16_kernel<64, 128, 1, 4, false>), grid, dim3(256), lds, st, p); break;
-    case 2: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 16, 4, 1, true>), grid, dim3(256), lds, st, p); break;
-    case 3: hipLaunchKernelGGL((wgrad_bf16_kernel<256, 256, 2, 4, false>), grid, dim3(512), lds, st, p); break;
-    case 4: hipLaunchKernelGGL((wgrad_bf16_kernel<256, 128, 4, 2, false>), grid, dim3(512), lds, st, p); break;
-    default: hipLaunchKernelGGL((wgrad_bf16_kernel<128, 256, 2, 4, false>), grid, dim3(512), lds, st, p); break;
+    case 0: STC_WB(128, 128, 2, 2, false, 256) break;
+    case 1: STC_WB(64, 128, 1, 4, false, 256) break;
+    case 2: STC_WB(128, 16, 4, 1, true, 256) break;
+    case 3:  // (the fast addressing would spill this 256-VGPR kernel: it keeps the per-step division)
+      hipLaunchKernelGGL((wgrad_bf16_kernel<256, 256, 2, 4, false, false>), grid, dim3(512), lds, st, p);
+      break;
+    case 4: STC_WB(256, 128, 4, 2, false, 512) break;
+    default: STC_WB(128, 256, 2, 4, false, 512) break;
   }
+#undef STC_WB
   main_timer_end(st);
   STC_CHECK_LAUNCH();
-  if (pl.nsplit <= 1) return 0;
-  const long long total = (long long)R * 16 * Cg_out;
-  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, (const float*)p.ws, pl.nsplit, R, Cg, Cg_out,
-                     dW);
+  if (!pl.slab) return 0;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)wgrad_reduce_blocks(R, Cg_out)), dim3(128), 0, st,
+                     (const float*)p.ws, pl.nsplit, R, Cg, Cg_out, dW);
   STC_CHECK_LAUNCH();
   return 0;
 }
 
 }  // namespace stc
-
-// Tuning / test hook: force the bf16 weight-gradient plan {tile config 0..5, pixel splits (0 = auto)}
-// for the following calls (cfg = -1 restores the automatic plan).  Process-global; not for use
-// while other threads launch weight gradients.
-extern "C" int stc_conv_wgrad_force_plan(int cfg, int nsplit) {
-  if (cfg < -1 || cfg >= stc::kNumWbCfg || nsplit < 0) return 1;
-  stc::g_wb_force_cfg.store(cfg);
-  stc::g_wb_force_ns.store(nsplit);
-  return 0;
-}

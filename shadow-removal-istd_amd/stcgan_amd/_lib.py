@@ -58,7 +58,9 @@ _SIGS = {
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
                               _f32, _vp, _vp, _i64, _vp]),
     "stc_conv_wgrad_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32]),
-    "stc_conv_wgrad_force_plan": (_i32, [_i32, _i32]),
+    "stc_conv_wgrad_ex": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
+                                 _f32, _vp, _vp, _vp, _i64, _vp]),
+    "stc_conv_wgrad_query": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "stc_pack_weight": (_i32, [_i32, _i32, _vp, _i32, _i32, _vp, _i32, _i32, _vp]),
     "stc_pack_weights": (_i32, [_i32, _i32, _vp, _vp]),
     "stc_chan_stats": (_i32, [_i32, _i32, View, _i32, _vp, _i32, _vp]),

@@ -212,28 +212,57 @@ def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True
     return mean, rstd
 
 
-def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None):
-    """Weight gradient [R][Cg_out][4][4] fp32 (stc_conv_wgrad)."""
+# bf16 weight-gradient tile configurations (csrc/wgrad_bf16.hip kWbCfg): cfg -> (BM, BN, WM, WN, swapped)
+_WB_TILES = [(128, 128, 2, 2, "false"), (64, 128, 1, 4, "false"), (128, 16, 4, 1, "true"), (256, 256, 2, 4, "false"),
+             (256, 128, 4, 2, "false"), (128, 256, 2, 4, "false")]
+
+
+def wgrad_query(B, Hd, Wd, R, Cg, dt, force=None):
+    """(workspace bytes, plan (cfg, BM, BN, splits, slab)) of stc_conv_wgrad_ex for these arguments."""
+    ws = ctypes.c_int64()
+    po = (ctypes.c_int32 * 5)()
+    fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
+    check(lib().stc_conv_wgrad_query(L.dtype_code(dt), B, Hd, Wd, R, Cg, fp, ctypes.byref(ws), po),
+          "stc_conv_wgrad_query")
+    return ws.value, tuple(po)
+
+
+def _wgrad_kernel_name(plan, Hd, Wd):
+    cfg = plan[0]
+    if cfg < 0:
+        return "wgrad_kernel"
+    bm, bn, wm, wn, sw = _WB_TILES[cfg]
+    ghw = Hd * Wd
+    pow2 = lambda v: v > 0 and (v & (v - 1)) == 0  # noqa: E731
+    fast = Wd % 64 == 0 or (pow2(Wd) and ghw % 64 == 0) or (pow2(ghw) and pow2(Wd) and 64 % ghw == 0)
+    fast = fast and cfg != 3  # the 256x256 tile keeps the general addressing (register budget)
+    return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}>"
+
+
+def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None,
+          force=None):
+    """Weight gradient [R][Cg_out][4][4] fp32 (stc_conv_wgrad_ex; force = optional {tile config, splits})."""
     l = lib()
-    nbytes = l.stc_conv_wgrad_workspace(L.dtype_code(dt), B, Dv.H, Dv.W, R, Cg)
+    nbytes, plan = wgrad_query(B, Dv.H, Dv.W, R, Cg, dt, force)
     ws, nb = _ws(nbytes, device)
     dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)
     dsc, dsh = _pro(dpro)
     gsc, gsh = _pro(gpro)
+    fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
     timer = _timer
     if timer is not None:
         e0, e1 = _main_events()
-    rc = l.stc_conv_wgrad(L.dtype_code(dt), B, stride, Dv, R, dsc, dsh, 0 if dslope is None else 1,
-                          0.0 if dslope is None else float(dslope), Gv, Cg, Cg_out, gsc, gsh,
-                          0 if gslope is None else 1, 0.0 if gslope is None else float(gslope), ptr(dW), ptr(ws), nb,
-                          stream())
+    rc = l.stc_conv_wgrad_ex(L.dtype_code(dt), B, stride, Dv, R, dsc, dsh, 0 if dslope is None else 1,
+                             0.0 if dslope is None else float(dslope), Gv, Cg, Cg_out, gsc, gsh,
+                             0 if gslope is None else 1, 0.0 if gslope is None else float(gslope), ptr(dW), fp,
+                             ptr(ws), nb, stream())
     if timer is not None:
         _disarm()
-    check(rc, "stc_conv_wgrad")
+    check(rc, "stc_conv_wgrad_ex")
     if timer is not None:
         dma = dt == torch.bfloat16 and dpro is None and gpro is None and dslope is None and gslope is None
-        name = "wgrad_bf16_kernel" if dma else "wgrad_kernel"
-        timer.append((name, nbytes == 0, 2.0 * B * Dv.H * Dv.W * R * 16 * Cg, e0, e1,
+        name = _wgrad_kernel_name(plan, Dv.H, Dv.W) if dma else "wgrad_kernel"
+        timer.append((name, not plan[4], 2.0 * B * Dv.H * Dv.W * R * 16 * Cg, e0, e1,
                       f"wgrad s{stride} P={B * Dv.H * Dv.W} R{R} Cg{Cg}"))
     return dW
 

@@ -194,11 +194,16 @@ WGRAD = [  # kind, stride, B, Cin, Cout, H, W (input grid of the forward layer)
     ("conv", 1, 2, 512, 8, 17, 17),    # PatchGAN logits (N = 8 padded): R <= 16 -> swapped 128x16 tile
     ("conv", 1, 1, 64, 8, 9, 11),      # R = 8, ragged
     ("conv", 2, 2, 16, 64, 40, 24),    # R = 64 with Cg = 16
+    # pixel-mapping modes of the K-step addressing (wgrad_bf16.hip WbParams::pmode)
+    ("conv", 2, 1, 16, 128, 128, 128),  # mode 1: 64 x 64 grid (a step inside one row), many splits
+    ("conv", 2, 5, 16, 64, 8, 8),       # mode 3: 4 x 4 grids, 80 pixels (partial last step)
+    ("convT", 2, 3, 64, 32, 1, 1),      # mode 3: 1 x 1 grids, 3 pixels
+    ("conv", 2, 2, 32, 64, 256, 16),    # mode 2 with GW = 8 (8 rows per step)
 ]
 
 
 @pytest.mark.parametrize("case", WGRAD, ids=lambda c: "_".join(map(str, c)))
-def test_wgrad_bf16_dma(case):
+def test_wgrad_bf16_dma(case, force=None):
     """bf16 weight gradient on the LDS-DMA / transposed-read kernel (csrc/wgrad_bf16.hip)."""
     kind, s, B, Cin, Cout, H, W = case
     x = q(rnd(B, Cin, H, W, seed=41))
@@ -209,7 +214,7 @@ def test_wgrad_bf16_dma(case):
         (gw,) = torch.autograd.grad(y, w, dy)
         # D = dy (R = Cout), G = x (Cg = Cin)
         dW = ops.wgrad(B, s, L.nhwc_view(nhwc(dy).to(DEV, BF)), Cout, L.nhwc_view(nhwc(x).to(DEV, BF)), Cin, Cin, BF,
-                       device=DEV)
+                       device=DEV, force=force)
     else:
         w = torch.zeros(Cin, Cout, 4, 4, requires_grad=True)
         y = F.conv_transpose2d(x, w, None, 2, 1)
@@ -217,7 +222,7 @@ def test_wgrad_bf16_dma(case):
         (gw,) = torch.autograd.grad(y, w, dy)
         # D = x (R = Cin), G = dy (Cg = Cout)
         dW = ops.wgrad(B, 2, L.nhwc_view(nhwc(x).to(DEV, BF)), Cin, L.nhwc_view(nhwc(dy).to(DEV, BF)), Cout, Cout, BF,
-                       device=DEV)
+                       device=DEV, force=force)
     torch.cuda.synchronize()
     got = dW.cpu()
     err = float((got - gw).abs().max())
@@ -296,15 +301,12 @@ WGRAD_FORCED = [  # (case, tile config, pixel splits): the 8-wave tiles on ragge
     (("convT", 2, 2, 1024, 512, 2, 2), 3, 1),
     (("conv", 2, 2, 8, 64, 64, 64), 5, 0),      # Cg = 8: 16 taps per 128 columns
     (("conv", 1, 2, 512, 8, 17, 17), 0, 4),     # R = 8 on a 128-row tile
+    (("conv", 2, 1, 16, 128, 128, 128), 0, 3),  # mode 1 with an odd split count
+    (("conv", 2, 5, 16, 64, 8, 8), 0, 2),       # mode 3, split boundary inside the pixel range
 ]
 
 
 @pytest.mark.parametrize("case,cfg,ns", WGRAD_FORCED, ids=lambda c: "_".join(map(str, c)) if isinstance(c, tuple) else str(c))
 def test_wgrad_bf16_forced_tiles(case, cfg, ns):
-    """Every weight-gradient tile configuration (stc_conv_wgrad_force_plan) against autograd."""
-    lib = L.lib()
-    assert lib.stc_conv_wgrad_force_plan(cfg, ns) == 0
-    try:
-        test_wgrad_bf16_dma(case)
-    finally:
-        lib.stc_conv_wgrad_force_plan(-1, 0)
+    """Every weight-gradient tile configuration (a per-call plan of stc_conv_wgrad_ex) against autograd."""
+    test_wgrad_bf16_dma(case, force=(cfg, ns))
