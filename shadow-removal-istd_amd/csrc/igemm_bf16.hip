@@ -28,6 +28,7 @@ struct GParams {
   int offy[4], offx[4];
   int stepy, stepx;
   int GH, GW, M, N, K;
+  float inv_ghw, inv_gw;  // 1/(GH*GW), 1/GW for fast_div (M < 2^24 is checked on the host)
   int ksplit, kchunk;
   const char* b;
   unsigned b_bytes;
@@ -178,8 +179,8 @@ igemm_bf16_kernel(const GParams p) {
   for (int g = 0; g < AG; ++g) {
     const int m = m0 + (wave * AG + g) * RPP + prow;
     const int mm = m < p.M ? m : 0;
-    const int b = mm / GHW, rem = mm - b * GHW;
-    const int y = rem / p.GW, x = rem - y * p.GW;
+    const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
+    const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
     const int ay = y * p.in_stride + p.offy[ph], ax = x * p.in_stride + p.offx[ph];
     a_off0[g] = (unsigned)(b * p.a_bs + p.a_co) + (unsigned)ay * (unsigned)p.a_rs + (unsigned)ax * (unsigned)p.a_ps;
     unsigned vm = 0;
@@ -390,15 +391,27 @@ igemm_bf16_kernel(const GParams p) {
     // bf16 tile through LDS: [BM][BN] with a 16-byte row pad, then 16-byte row stores
     constexpr int PITCH = BN * 2 + 16;
     char* tl = smem;
+    // Column pairs: lanes l and l^1 hold columns c and c^1 of the same 4 rows; one DPP lane swap of two
+    // values gives the even lane rows 0-1 and the odd lane rows 2-3 of the pair, each written as one
+    // bf16x2 dword (half the LDS stores of per-element 16-bit writes)
+    const bool even = (cl & 1) == 0;
+    const int pcol = cl & ~1;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + 16 * i + rq + r, col = wn * TN + 16 * j + cl;
-          *reinterpret_cast<unsigned short*>(tl + row * PITCH + col * 2) = f2bf(acc[i][j][r]);
-        }
+      for (int j = 0; j < FN; ++j) {
+        const float s0 = even ? acc[i][j][2] : acc[i][j][0];
+        const float s1 = even ? acc[i][j][3] : acc[i][j][1];
+        // quad_perm [1,0,3,2]: every lane receives its neighbour's value
+        const float x0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xF, 0xF, false));
+        const float x1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s1), 0xB1, 0xF, 0xF, false));
+        const float lo0 = even ? acc[i][j][0] : x0, hi0 = even ? x0 : acc[i][j][2];
+        const float lo1 = even ? acc[i][j][1] : x1, hi1 = even ? x1 : acc[i][j][3];
+        const int row = wm * TM + 16 * i + rq + (even ? 0 : 2), col = wn * TN + 16 * j + pcol;
+        char* dst = tl + row * PITCH + col * 2;
+        *reinterpret_cast<unsigned*>(dst) = (unsigned)f2bf(lo0) | ((unsigned)f2bf(hi0) << 16);
+        *reinterpret_cast<unsigned*>(dst + PITCH) = (unsigned)f2bf(lo1) | ((unsigned)f2bf(hi1) << 16);
+      }
     __syncthreads();
     constexpr int CPR = BN / 8;  // 16-byte chunks per row (64*NW is a multiple of CPR: fixed cc per thread)
     constexpr int ITER = BM * CPR / (64 * NW);
@@ -411,8 +424,8 @@ igemm_bf16_kernel(const GParams p) {
         const int row = (tid + it * 64 * NW) / CPR;
         const int m = m0 + row;
         if (m >= p.M || n >= p.N) continue;
-        const int b = m / GHW, rem = m - b * GHW;
-        const int y = rem / p.GW, x = rem - y * p.GW;
+        const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+        const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
         const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
         const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
@@ -439,8 +452,8 @@ igemm_bf16_kernel(const GParams p) {
         const int m = m0 + row;
         const bool in = m < p.M && n < p.N;
         const int mm = in ? m : m0;
-        const int b = mm / GHW, rem = mm - b * GHW;
-        const int y = rem / p.GW, x = rem - y * p.GW;
+        const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
+        const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
         const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
         tv[u] = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
         if (in) {
@@ -503,8 +516,8 @@ igemm_bf16_kernel(const GParams p) {
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + wm * TM + 16 * i + rq + r;
       if (m >= p.M) continue;
-      const int b = m / GHW, rem = m - b * GHW;
-      const int y = rem / p.GW, x = rem - y * p.GW;
+      const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+      const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
       const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
       const long long ro = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps;
 #pragma unroll
@@ -584,8 +597,8 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
       float v[8];
       rowval(row, v);
       const int ph = (int)(row / p.M), m = (int)(row - (long long)ph * p.M);
-      const int b = m / GHW, rem = m - b * GHW;
-      const int y = rem / p.GW, x = rem - y * p.GW;
+      const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+      const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
       const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
       const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
       uint4 o;
@@ -922,6 +935,9 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
   if (kind == STC_CONVT_S2) { p.GH = x.H; p.GW = x.W; }
   else { p.GH = y.H; p.GW = y.W; }
   p.M = B * p.GH * p.GW; p.N = Cout; p.K = taps * Cin;
+  STC_REQUIRE(p.M < (1 << 24), "bf16 conv: M = %d pixels per phase (>= 2^24)", p.M);
+  p.inv_ghw = 1.0f / (float)(p.GH * p.GW);
+  p.inv_gw = 1.0f / (float)p.GW;
   p.b = (const char*)w_packed;
   p.b_phase_stride = Cout * p.K;
   p.b_bytes = (unsigned)((long long)g.nphase * p.b_phase_stride * 2);
