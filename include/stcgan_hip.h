@@ -275,6 +275,29 @@ int stc_istd_errors(const unsigned char* img1, const unsigned char* img2, const 
 int stc_istd_ssim(const unsigned char* img1, const unsigned char* img2, int B, int H, int W, double* out, void* ws,
                   int64_t ws_bytes, void* stream);
 
+/* ISTD evaluation with the reference's resize branches (src/eval.py:64-81), one image pair per call.
+ * Images are typed planes [H][W][C]:
+ *   STC_IMG_U8F32 (0): uint8 read as util.img_as_float32 (float32(u) * float32(1/255))
+ *   STC_IMG_U8F64 (1): uint8 read as util.img_as_float   (u * (1/255) in float64)
+ *   STC_IMG_F64   (2): float64
+ * stc_image_resize_f64: skimage 0.17 transform.resize(src, (OH, OW), mode="edge", order 1) -> float64,
+ *   with anti_alias: the gaussian prefilter of resize's anti_aliasing (sigma = max(0, (in/out-1)/2)
+ *   per axis, scipy mode 'nearest', truncate 4); ws >= stc_image_resize_workspace(H, W, C) bytes.
+ * stc_istd_errors_ex: out[7] as stc_istd_errors for img1 (U8F32 or F64) vs img2 (U8F32 or F64), the
+ *   sRGB gamma in each image's dtype and float64 from the xyz product on (skimage.color.rgb2lab);
+ *   mask: float64 [H][W] (shadow = value > 0.5, util.img_as_bool) or NULL.
+ * stc_istd_ssim_ex: out[1] = SSIM of the pair (as stc_istd_ssim, typed inputs).
+ *   ws for both: >= stc_istd_typed_workspace(H, W) bytes.                                        */
+enum { STC_IMG_U8F32 = 0, STC_IMG_U8F64 = 1, STC_IMG_F64 = 2 };
+int64_t stc_image_resize_workspace(int H, int W, int C);
+int stc_image_resize_f64(const void* src, int kind, int H, int W, int C, int OH, int OW, int anti_alias, double* dst,
+                         void* ws, int64_t ws_bytes, void* stream);
+int64_t stc_istd_typed_workspace(int H, int W);
+int stc_istd_errors_ex(const void* img1, int kind1, const void* img2, int kind2, const double* mask, int H, int W,
+                       double* out, void* ws, int64_t ws_bytes, void* stream);
+int stc_istd_ssim_ex(const void* img1, int kind1, const void* img2, int kind2, int H, int W, double* out, void* ws,
+                     int64_t ws_bytes, void* stream);
+
 /* ---- training-batch preparation ---------------------------------------------------
  * src: uint8 [B][H][W][C] (decoded images, the loader's channel order); params: device int32
  * [B][3] = {flip, row_offset, col_offset} drawn on the host in the reference's order; pad_h /

@@ -84,6 +84,11 @@ _SIGS = {
     "stc_istd_errors_workspace": (_i64, [_i32, _i32, _i32]),
     "stc_istd_errors": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp]),
     "stc_istd_ssim": (_i32, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "stc_image_resize_workspace": (_i64, [_i32, _i32, _i32]),
+    "stc_image_resize_f64": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "stc_istd_typed_workspace": (_i64, [_i32, _i32]),
+    "stc_istd_errors_ex": (_i32, [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "stc_istd_ssim_ex": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp]),
     "stc_prepare_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
     "stc_prepare_batch_f32": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
     "stc_resize_area": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),

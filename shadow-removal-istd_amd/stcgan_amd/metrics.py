@@ -5,8 +5,11 @@ keys (rmse, mae, rmse_non, mae_non, rmse_all, mae_all, and psnr / ssim without a
 per-pixel work -- rgb2lab of both images, the masked LAB error sums, the squared error behind
 PSNR and SSIM -- runs in ``stc_istd_errors`` / ``stc_istd_ssim`` (csrc/istd_metrics.hip).  Files
 are read as RGB uint8 (skimage.io.imread's order) with PIL; the host only decodes PNGs and adds
-up the per-image sums.  Pairs must have the same size and ``size`` must be None (the reference's
-resize branch, skimage.transform.resize, is not restated).
+up the per-image sums.  Every resize branch of eval.py:64-81 runs on the GPU too
+(``stc_image_resize_f64``: skimage transform.resize, mode "edge", order 1, with the mask's default
+anti-aliasing): img2 follows img1's shape, the mask img1's size, and with ``size`` all three are
+resized to size x size; types follow the reference (img2 and the mask are float64 after their
+resize, img1 stays img_as_float32 unless ``size`` resizes it).
 """
 import math
 import os
@@ -18,7 +21,7 @@ from ._lib import check, lib, ptr, stream
 
 
 def _dev_u8(a, device):
-    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint8)).to(device)
+    return torch.from_numpy(np.array(a, dtype=np.uint8, copy=True)).to(device)
 
 
 def istd_errors(img1, img2, mask=None):
@@ -62,27 +65,98 @@ def psnr_from_sse(sse, H, W):
     return math.inf if mse == 0 else 10.0 * math.log10(1.0 / mse)
 
 
-def all_metrics(dir1, dir2, size=None, maskdir=None, device="cuda"):
-    """src/eval.py:41-115 over the files of dir1 (same names in dir2 / maskdir)."""
+IMG_U8F32, IMG_U8F64, IMG_F64 = 0, 1, 2
+
+
+def resize_f64(img, kind, out_hw, anti_alias=False):
+    """skimage transform.resize(img, out_hw, mode="edge") on the GPU -> float64 CUDA tensor
+    [OH, OW(, C)]; img: uint8 (kind IMG_U8F32 / IMG_U8F64) or float64 CUDA tensor [H, W(, C)]."""
+    two_d = img.dim() == 2
+    x = img.contiguous()
+    H, W = x.shape[:2]
+    C = 1 if two_d else x.shape[2]
+    OH, OW = out_hw
+    out = torch.empty((OH, OW) if two_d else (OH, OW, C), dtype=torch.float64, device=x.device)
+    nbytes = lib().stc_image_resize_workspace(H, W, C)
+    ws = torch.empty(int(nbytes), dtype=torch.uint8, device=x.device)
+    check(lib().stc_image_resize_f64(ptr(x), kind, H, W, C, OH, OW, int(anti_alias), ptr(out), ptr(ws), int(nbytes),
+                                     stream()), "stc_image_resize_f64")
+    return out
+
+
+def istd_errors_typed(img1, kind1, img2, kind2, mask=None):
+    """[7] float64 sums (as istd_errors) of one pair of typed images [H, W, 3]; mask float64 [H, W]
+    (shadow = value > 0.5) or None."""
+    H, W = img1.shape[:2]
+    out = torch.empty(7, dtype=torch.float64, device=img1.device)
+    nbytes = lib().stc_istd_typed_workspace(H, W)
+    ws = torch.empty(int(nbytes), dtype=torch.uint8, device=img1.device)
+    check(lib().stc_istd_errors_ex(ptr(img1.contiguous()), kind1, ptr(img2.contiguous()), kind2,
+                                   ptr(None if mask is None else mask.contiguous()), H, W, ptr(out), ptr(ws),
+                                   int(nbytes), stream()), "stc_istd_errors_ex")
+    return out
+
+
+def istd_ssim_typed(img1, kind1, img2, kind2):
+    H, W = img1.shape[:2]
+    out = torch.empty(1, dtype=torch.float64, device=img1.device)
+    nbytes = lib().stc_istd_typed_workspace(H, W)
+    ws = torch.empty(int(nbytes), dtype=torch.uint8, device=img1.device)
+    check(lib().stc_istd_ssim_ex(ptr(img1.contiguous()), kind1, ptr(img2.contiguous()), kind2, H, W, ptr(out),
+                                 ptr(ws), int(nbytes), stream()), "stc_istd_ssim_ex")
+    return out
+
+
+def _read_rgb(path):
     from PIL import Image
+    return np.asarray(Image.open(path).convert("RGB"))
+
+
+def _read_gray(path):
+    """io.imread(path, as_gray=True) of a single-channel PNG: the uint8 plane as stored."""
+    from PIL import Image
+    im = Image.open(path)
+    if im.mode not in ("L", "P", "1"):
+        raise NotImplementedError(f"stcgan_amd.metrics: {path}: masks are single-channel PNGs ({im.mode})")
+    return np.asarray(im.convert("L"))
+
+
+def pair_sums(a_u8, b_u8, m_u8=None, size=None, device="cuda"):
+    """One iteration of eval.py's loop (:62-107) on uint8 arrays: returns (sums [7] over the compared
+    images, sse of the PSNR pair, ssim or None)."""
+    A, Bt = _dev_u8(a_u8, device), _dev_u8(b_u8, device)
+    H, W = a_u8.shape[:2]
+    img2 = resize_f64(Bt, IMG_U8F32, (H, W))                      # float64, img1's shape
+    mask = resize_f64(_dev_u8(m_u8, device), IMG_U8F64, (H, W), anti_alias=True) if m_u8 is not None else None
     if size is not None:
-        raise NotImplementedError("stcgan_amd.metrics: the resize branch (size != None) is not restated")
+        i1 = resize_f64(A, IMG_U8F32, (size, size))
+        i2 = resize_f64(img2, IMG_F64, (size, size))
+        mk = resize_f64(mask, IMG_F64, (size, size), anti_alias=True) if mask is not None else None
+        s = istd_errors_typed(i1, IMG_F64, i2, IMG_F64, mk)
+    else:
+        s = istd_errors_typed(A, IMG_U8F32, img2, IMG_F64, mask)
+    s = s.cpu().numpy()
+    sse, ss = None, None
+    if m_u8 is None:
+        sse = float(istd_errors_typed(A, IMG_U8F32, img2, IMG_F64, None)[6]) if size is not None else float(s[6])
+        ss = float(istd_ssim_typed(A, IMG_U8F32, img2, IMG_F64)[0]) if H >= 7 and W >= 7 else float("nan")
+    return s, sse, ss
+
+
+def all_metrics(dir1, dir2, size=None, maskdir=None, device="cuda"):
+    """src/eval.py:41-115 over the files of dir1 (same names in dir2 / maskdir), every resize branch
+    included."""
     sums = np.zeros(7)
     psnrs, ssims = [], []
     for f in sorted(os.listdir(dir1)):
-        a = np.asarray(Image.open(os.path.join(dir1, f)).convert("RGB"))
-        b = np.asarray(Image.open(os.path.join(dir2, f)).convert("RGB"))
-        if a.shape != b.shape:
-            raise NotImplementedError(f"stcgan_amd.metrics: {f}: sizes differ ({a.shape} vs {b.shape})")
-        m = None
-        if maskdir is not None:
-            m = _dev_u8(np.asarray(Image.open(os.path.join(maskdir, f)).convert("L"))[None], device)
-        A, Bt = _dev_u8(a[None], device), _dev_u8(b[None], device)
-        s = istd_errors(A, Bt, m)[0].cpu().numpy()
+        a = _read_rgb(os.path.join(dir1, f))
+        b = _read_rgb(os.path.join(dir2, f))
+        m = _read_gray(os.path.join(maskdir, f)) if maskdir is not None else None
+        s, sse, ss = pair_sums(a, b, m, size, device)
         sums += s
         if maskdir is None:
-            psnrs.append(psnr_from_sse(float(s[6]), a.shape[0], a.shape[1]))
-            ssims.append(float(istd_ssim(A, Bt)[0]))
+            psnrs.append(psnr_from_sse(sse, a.shape[0], a.shape[1]))
+            ssims.append(ss)
     rs, ms, ns, rn, mn, nn = sums[:6]
     res = {"rmse": rs / ns if ns else float("nan"), "mae": ms / ns if ns else float("nan"),
            "rmse_non": rn / nn if nn else float("nan"), "mae_non": mn / nn if nn else float("nan"),
