@@ -312,6 +312,18 @@ int stc_prepare_batch_f32(const float* src, int B, int H, int W, int C, const in
  * the normalised image ((u / 255 - 0.5) * 2), uint8 [B][H][W][C] -> fp32 NHWC [B][OH][OW][C]. */
 int stc_resize_area(const unsigned char* src, int B, int H, int W, int C, int OH, int OW, float* dst, void* stream);
 
+/* Resize (transform.py:173-178) when the image does not shrink in both axes: cv.resize INTER_LINEAR of
+ * the float32 image (OpenCV's generic float path); src: uint8 [B][H][W][C] (src_u8 = 1, normalised
+ * (u / 255 - 0.5) * 2 on the fly) or fp32 NHWC; dst fp32 NHWC [B][OH][OW][C].                     */
+int stc_resize_linear(const void* src, int src_u8, int B, int H, int W, int C, int OH, int OW, float* dst,
+                      void* stream);
+/* RandomScale / RandomRotate (transform.py:59-100): cv.warpAffine(img, M_b, (W, H), INTER_LINEAR,
+ * BORDER_CONSTANT 0) of every image b with its forward matrix M_b (device, float64 [B][6], the
+ * getRotationMatrix2D result); OpenCV's inversion and fixed-point (1/32 pixel) sampling.  src as for
+ * stc_resize_linear, dst fp32 NHWC [B][H][W][C].                                                  */
+int stc_warp_affine(const void* src, int src_u8, int B, int H, int W, int C, const double* M, float* dst,
+                    void* stream);
+
 /* ---- optimizer --------------------------------------------------------------------
  * One launch over many tensors.  table: device array of ntensors records
  * {param*, grad*, exp_avg*, exp_avg_sq*, numel, first_block} (6 x int64), where

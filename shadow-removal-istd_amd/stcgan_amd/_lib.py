@@ -91,6 +91,8 @@ _SIGS = {
     "stc_istd_ssim_ex": (_i32, [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _i64, _vp]),
     "stc_prepare_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
     "stc_prepare_batch_f32": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "stc_resize_linear": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "stc_warp_affine": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "stc_resize_area": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "stc_time_next_main_kernel": (_i32, [_vp, _vp]),
     "stc_last_error": (ctypes.c_char_p, []),

@@ -13,8 +13,10 @@ Differences that do not change results:
     source lists (zero-copy: the first layer gathers the channels itself);
   * multi-GPU is one process per GPU with an RCCL gradient all-reduce
     (parallel.py) instead of nn.DataParallel.
-The data pipeline (ISTD folders + augmentation, STCGAN/dataset.py / transform.py)
-is outside this hot path: loaders are any iterable of (names, x, m, y) batches.
+Loaders: any iterable of (names, x, m, y) batches; with ``args.data_dir`` and no
+loader passed, the reference's two ISTD loaders (STCGAN/stcgan.py:73-104) are built
+on data.ISTDLoader (decode on the host, Resize / RandomScale / RandomRotate / flip /
+crop on the device), each rank taking its shard of the global ``args.batch_size``.
 """
 import datetime
 import logging
@@ -92,6 +94,9 @@ class STCGAN(object):
         self.sync_G.enable_overlap()
         self.sync_D.enable_overlap()
 
+        data_dir = getattr(args, "data_dir", None)
+        if data_dir is not None and train_loader is None and valid_loader is None:
+            train_loader, valid_loader = self.istd_loaders(args)
         self.train_loader = train_loader
         self.valid_loader = valid_loader
 
@@ -112,6 +117,19 @@ class STCGAN(object):
             self.valid_interval = getattr(args, "valid_every", 10)
         if "infer" in tasks:
             self.inferd_dir = getattr(args, "infered", None)
+
+    def istd_loaders(self, args):
+        """The reference's train/valid loaders (STCGAN/stcgan.py:73-104) on data.ISTDLoader."""
+        from .data import ISTDLoader
+        self.logger.info("Creating data loaders")
+        common = dict(batch_size=args.batch_size, datas=("img", "mask", "target"),
+                      workers=getattr(args, "workers", 0), rank=parallel.rank(), world=parallel.world(),
+                      device=self.device)
+        train = ISTDLoader(args.data_dir, "train", resize=(300, 400), scale=getattr(args, "aug_scale", 0.05),
+                           angle=getattr(args, "aug_angle", 15), flip_prob=0.5,
+                           crop_size=getattr(args, "image_size", 256), shuffle=True, drop_last=True, **common)
+        valid = ISTDLoader(args.data_dir, "test", resize=(256, 256), shuffle=False, drop_last=False, **common)
+        return train, valid
 
     # ------------------------------------------------------------------ training
     def train(self, epochs=5000):
