@@ -158,6 +158,24 @@ __device__ __forceinline__ double block_sum256(double v, double* sh) {
   return r;
 }
 
+// mean / rstd / affine table / running statistics of channel c from the merged N, mean, M2
+__device__ __forceinline__ void bn_finalize_store(int c, double N, double mu, double M2, const float* gamma,
+                                                  const float* beta, float* rmean, float* rvar, long long* nbt,
+                                                  float momentum, float eps, float* mean_o, float* rstd_o,
+                                                  float* scale, float* shift) {
+  const double var = N > 0 ? M2 / N : 0.0;
+  const float rs = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  if (mean_o) mean_o[c] = (float)mu;
+  if (rstd_o) rstd_o[c] = rs;
+  const float sc = g * rs;
+  scale[c] = sc;
+  shift[c] = bt - (float)mu * sc;
+  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
+  if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(N > 1 ? M2 / (N - 1) : var);
+  if (nbt && c == 0) nbt[0] += 1;
+}
+
 __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int nchunks, int C,
                                                           const float* gamma, const float* beta,
                                                           float* rmean, float* rvar, long long* nbt,
@@ -232,19 +250,64 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int
   }
   const double N = n, mu = sm;
   const double M2 = block_sum256(m2, sh);
-  if (threadIdx.x == 0) {
-    const double var = N > 0 ? M2 / N : 0.0;
-    const float rs = (float)(1.0 / sqrt(var + (double)eps));
-    const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    if (mean_o) mean_o[c] = (float)mu;
-    if (rstd_o) rstd_o[c] = rs;
-    const float sc = g * rs;
-    scale[c] = sc;
-    shift[c] = bt - (float)mu * sc;
-    if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
-    if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(N > 1 ? M2 / (N - 1) : var);
-    if (nbt && c == 0) nbt[0] += 1;
+  if (threadIdx.x == 0)
+    bn_finalize_store(c, N, mu, M2, gamma, beta, rmean, rvar, nbt, momentum, eps, mean_o, rstd_o, scale, shift);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// The same merge with one wave per channel (4 channels per block, no block barriers): the
+// finalize runs once per BatchNorm per pass, so its latency, not its bytes, is what it costs.
+__global__ void __launch_bounds__(256) bn_finalize_wave_kernel(const float* part, int nchunks, int C,
+                                                               const float* gamma, const float* beta,
+                                                               float* rmean, float* rvar, long long* nbt,
+                                                               float momentum, float eps,
+                                                               float* mean_o, float* rstd_o, float* scale, float* shift) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  auto load4 = [&](int k0, float4* pp) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * 64;
+      pp[u] = k < nchunks ? *reinterpret_cast<const float4*>(part + ((long long)k * C + c) * 4)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  double n = 0, sm = 0;
+  for (int k0 = lane; k0 < nchunks; k0 += 256) {
+    float4 pp[4];
+    load4(k0, pp);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (pp[u].x <= 0.f) continue;
+      n += pp[u].x;
+      sm += (double)pp[u].x * pp[u].w + (double)pp[u].y;
+    }
   }
+  const double N = wave_sum(n), S = wave_sum(sm);
+  const double mu = N > 0 ? S / N : 0.0;
+  double m2 = 0;
+  for (int k0 = lane; k0 < nchunks; k0 += 256) {
+    float4 pp[4];
+    load4(k0, pp);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (pp[u].x <= 0.f) continue;
+      const double nb = pp[u].x, s1 = pp[u].y, r = s1 / nb;
+      double q = (double)pp[u].z - s1 * r;
+      if (q < 0) q = 0;
+      const double d = (double)pp[u].w + r - mu;
+      m2 += q + nb * d * d;
+    }
+  }
+  const double M2 = wave_sum(m2);
+  if (lane == 0)
+    bn_finalize_store(c, N, mu, M2, gamma, beta, rmean, rvar, nbt, momentum, eps, mean_o, rstd_o, scale, shift);
 }
 
 // eval-mode table from running statistics
@@ -372,6 +435,34 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* part,
   }
 }
 
+// one wave per channel (4 per block): as bn_bwd_finalize_kernel without block barriers
+__global__ void __launch_bounds__(256) bn_bwd_finalize_wave_kernel(const float* part, int nchunks, int C, float* dgamma,
+                                                                   float* dbeta) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  double a = 0, b = 0;
+  for (int k0 = lane; k0 < nchunks; k0 += 256) {
+    float2 pp[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * 64;
+      pp[u] = k < nchunks ? *reinterpret_cast<const float2*>(part + ((long long)k * C + c) * 2) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a += pp[u].x;
+      b += pp[u].y;
+    }
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if (lane == 0) {
+    dbeta[c] = (float)a;
+    dgamma[c] = (float)b;
+  }
+}
+
 template <typename T, bool DENSE>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, PixDiv pd, long long P, int C, const float* scale,
                                                            const float* shift, const float* mean, const float* rstd,
@@ -456,6 +547,52 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(View x, PixDiv pd, lo
     }
     VW<T>::store(reinterpret_cast<T*>(dx.p) + o.dx, d);
   };
+  if constexpr (DENSE) {
+    // Streaming form (host: every view pixel-dense with 32-bit element offsets, 256 % CG == 0, so
+    // the grid stride is a whole number of pixels): this thread's channel group and its table are
+    // fixed, the pixel advances by a constant -- no per-element index division.
+    const unsigned nthr = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned pstep = nthr / (unsigned)CG, Pu = (unsigned)P;
+    unsigned pix = t0 / (unsigned)CG;
+    if (pix >= Pu) return;
+    const int c = N * (int)(t0 % (unsigned)CG);
+    table(c / N);
+    const T* xp = reinterpret_cast<const T*>(x.p) + x.co + c;
+    const T* g1p = reinterpret_cast<const T*>(gi.g1.p) + gi.g1.co + c;
+    const T* g2p = reinterpret_cast<const T*>(gi.g2.p) + gi.g2.co + c;
+    T* dp = reinterpret_cast<T*>(dx.p) + dx.co + c;
+    const unsigned xs = x.ps, g1s = gi.g1.ps, g2s = gi.g2.ps, ds = dx.ps;
+    auto ld = [&](unsigned q, In& in) {
+      VW<T>::load(xp + q * xs, in.v);
+      if (gi.has1) VW<T>::load(g1p + q * g1s, in.g1);
+      if (gi.has2) VW<T>::load(g2p + q * g2s, in.g2);
+    };
+    auto put = [&](unsigned q, const In& in) {
+      float d[N];
+#pragma unroll
+      for (int e = 0; e < N; ++e) {
+        const float n = fmaf(in.v[e], sc[e], sh[e]);
+        float dn = 0.f;
+        if (gi.has1) dn += in.g1[e] * dact(n, gi.s1);
+        if (gi.has2) dn += in.g2[e] * dact(n, gi.s2);
+        d[e] = fmaf(k1[e], dn, -fmaf(k2[e], in.v[e], k0[e]));
+      }
+      VW<T>::store(dp + q * ds, d);
+    };
+    for (; pix + pstep < Pu; pix += 2 * pstep) {  // both pixels' loads in flight before either is used
+      In a, b;
+      ld(pix, a);
+      ld(pix + pstep, b);
+      put(pix, a);
+      put(pix + pstep, b);
+    }
+    if (pix < Pu) {
+      In a;
+      ld(pix, a);
+      put(pix, a);
+    }
+    return;
+  }
   long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (; idx + stride < total; idx += 2 * stride) {  // both elements' loads in flight before either is used
     const Off oa = offs(idx), ob = offs(idx + stride);
@@ -526,6 +663,30 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(View x, PixDiv pd, long l
       VW<T>::store(reinterpret_cast<T*>(y2.p) + o2, o);
     }
   };
+  if constexpr (DENSE) {  // streaming form: as bn_bwd_apply_kernel's
+    const unsigned nthr = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned pstep = nthr / (unsigned)CG, Pu = (unsigned)P;
+    unsigned pix = t0 / (unsigned)CG;
+    if (pix >= Pu) return;
+    const int c = N * (int)(t0 % (unsigned)CG);
+    table(c / N);
+    const T* xp = reinterpret_cast<const T*>(x.p) + x.co + c;
+    const unsigned xs = x.ps, s1s = y1.ps, s2s = y2.ps;
+    const long long b1 = y1.co + c, b2 = y2.co + c;
+    for (; pix + pstep < Pu; pix += 2 * pstep) {
+      float va[N], vb[N];
+      VW<T>::load(xp + pix * xs, va);
+      VW<T>::load(xp + (pix + pstep) * xs, vb);
+      emit(va, b1 + pix * s1s, b2 + pix * s2s);
+      emit(vb, b1 + (pix + pstep) * s1s, b2 + (pix + pstep) * s2s);
+    }
+    if (pix < Pu) {
+      float va[N];
+      VW<T>::load(xp + pix * xs, va);
+      emit(va, b1 + pix * s1s, b2 + pix * s2s);
+    }
+    return;
+  }
   long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (; idx + stride < total; idx += 2 * stride) {  // two 16-byte loads in flight per thread
     long long ax, a1, a2, bx, b1, b2;
@@ -623,6 +784,17 @@ extern "C" int stc_chan_stats_chunks(int B, int H, int W) { return stat_chunks((
 // pixel-dense view: rows and images follow each other without gaps, so pixel p sits at p * ps
 static bool pix_dense(const stc_view& v) { return v.rs == (int64_t)v.W * v.ps && v.bs == (int64_t)v.H * v.rs; }
 
+// the streaming (DENSE) element-wise form: pixel-dense views whose element offsets fit 32 bits, and a
+// channel-group count dividing 256 (the grid stride is then a whole number of pixels)
+static bool stream_ok(int B, const stc_view& v, int C, int N) {
+  if (!v.p) return true;
+  const long long extent = (long long)B * v.H * v.W * v.ps + v.co + C;
+  return pix_dense(v) && extent < (1ll << 31) && 256 % (C / N) == 0;
+}
+static int grid_stream(long long work) {  // >= 4 pixel-vectors per thread, at most 8 blocks per CU
+  return (int)std::max<long long>(1, std::min<long long>((work + 1023) / 1024, 2048));
+}
+
 static bool vec_ok(int dtype, int C, const stc_view& v) {
   const int N = dtype == STC_F32 ? 4 : 8;
   return C % N == 0 && C / N <= 256 && v.cs == 1 && v.co % N == 0 && v.ps % N == 0 && v.rs % N == 0 && v.bs % N == 0;
@@ -650,8 +822,8 @@ extern "C" int stc_bn_apply(int dtype, int B, stc_view x, int C, const float* sc
   const PixDiv pd = mkpix(B, x.H, x.W);
   const long long P = (long long)B * x.H * x.W;
   const int N = dtype == STC_F32 ? 4 : 8;
-  const int blocks = grid_for(P * (C / N));
-  const bool dense = pix_dense(x) && pix_dense(y1) && (!y2.p || pix_dense(y2));
+  const bool dense = stream_ok(B, x, C, N) && stream_ok(B, y1, C, N) && stream_ok(B, y2, C, N);
+  const int blocks = dense ? grid_stream(P * (C / N)) : grid_for(P * (C / N));
   const int h2 = y2.p != nullptr ? 1 : 0;
 #define STC_BA(T_, D_) hipLaunchKernelGGL((bn_apply_kernel<T_, D_>), dim3(blocks), dim3(256), 0, st, v, pd, P, C, scale, shift, o1, slope1, o2, slope2, h2)
   if (dtype == STC_F32) { if (dense) STC_BA(float, true); else STC_BA(float, false); }
@@ -686,8 +858,13 @@ extern "C" int stc_bn_finalize(const float* part, int nchunks, int C, const floa
     hipLaunchKernelGGL(bn_eval_table_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, running_mean,
                        running_var, eps, scale, shift);
   } else {
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, part, nchunks, C, gamma, beta, running_mean,
-                       running_var, (long long*)num_batches_tracked, momentum, eps, mean, rstd, scale, shift);
+    if (nchunks <= 8192)
+      hipLaunchKernelGGL(bn_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nchunks, C, gamma, beta,
+                         running_mean, running_var, (long long*)num_batches_tracked, momentum, eps, mean, rstd, scale,
+                         shift);
+    else
+      hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, part, nchunks, C, gamma, beta, running_mean,
+                         running_var, (long long*)num_batches_tracked, momentum, eps, mean, rstd, scale, shift);
   }
   STC_CHECK_LAUNCH();
   return 0;
@@ -723,15 +900,20 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
   GradIn gi = mkgrad(g1, slope1, g2, slope2);
   if (mean) {
     STC_REQUIRE(part2 && dgamma && dbeta && gamma && rstd && scale && shift, "stc_bn_bwd_apply: missing BN tensors");
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part2, nchunks, C, dgamma, dbeta);
+    if (nchunks <= 8192)
+      hipLaunchKernelGGL(bn_bwd_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part2, nchunks, C, dgamma, dbeta);
+    else
+      hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part2, nchunks, C, dgamma, dbeta);
     STC_CHECK_LAUNCH();
   }
   View v = mkview(x), o = mkview(dx);
   const PixDiv pd = mkpix(B, x.H, x.W);
   const long long P = (long long)B * x.H * x.W;
-  const long long work = P * (C / (dtype == STC_F32 ? 4 : 8));
-  const bool dense = pix_dense(x) && pix_dense(dx) && (!g1.p || pix_dense(g1)) && (!g2.p || pix_dense(g2));
-#define STC_BB(T_, D_) hipLaunchKernelGGL((bn_bwd_apply_kernel<T_, D_>), dim3(grid_for(work)), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o)
+  const int N = dtype == STC_F32 ? 4 : 8;
+  const long long work = P * (C / N);
+  const bool dense = stream_ok(B, x, C, N) && stream_ok(B, dx, C, N) && stream_ok(B, g1, C, N) && stream_ok(B, g2, C, N);
+  const int blocks = dense ? grid_stream(work) : grid_for(work);
+#define STC_BB(T_, D_) hipLaunchKernelGGL((bn_bwd_apply_kernel<T_, D_>), dim3(blocks), dim3(256), 0, st, v, pd, P, C, scale, shift, mean, rstd, gamma, gi, dgamma, dbeta, o)
   if (dtype == STC_F32) { if (dense) STC_BB(float, true); else STC_BB(float, false); }
   else { if (dense) STC_BB(bf16, true); else STC_BB(bf16, false); }
 #undef STC_BB

@@ -47,6 +47,14 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return *reinterpret_cast<unsigned short*>(&b);
 }
 
+// {lo, hi} -> one dword of two bf16 (round-to-nearest-even), a single v_cvt_pk_bf16_f32
+typedef __bf16 stc_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float stc_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  const stc_f32x2 v = {lo, hi};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, stc_bf16x2));
+}
+
 // 4 consecutive elements <-> float4
 template <typename T> struct Vec4;
 template <> struct Vec4<float> {

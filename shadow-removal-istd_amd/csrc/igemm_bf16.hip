@@ -123,6 +123,19 @@ __device__ __forceinline__ void wait_ahead(int ahead) {
   }
 }
 
+// In-range taps t in [0, nt) of one axis, input coordinate a + step * t (step = +-1) inside [0, I):
+// an interval [lo, hi) in t, returned as a bit mask.
+__device__ __forceinline__ unsigned tap_mask(int a, int I, int step, int nt) {
+  const int a2 = step > 0 ? a : I - 1 - a;  // the step = -1 case mirrored onto step = +1
+  const int lo = min(max(-a2, 0), nt), hi = min(max(I - a2, 0), nt);
+  return ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+}
+// Row mask (bit ty) -> bit ty << lg, the first tap of row ty in a 2-D tap set (the column mask is
+// multiplied in: no carries, it has lg-bit width).
+__device__ __forceinline__ unsigned tap_spread(unsigned r, int lg) {
+  return (r & 1u) | (((r >> 1) & 1u) << (1 << lg)) | (((r >> 2) & 1u) << (2 << lg)) | (((r >> 3) & 1u) << (3 << lg));
+}
+
 template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB>
 __global__ void __launch_bounds__(64 * WM * WN)
 igemm_bf16_kernel(const GParams p) {
@@ -169,12 +182,12 @@ igemm_bf16_kernel(const GParams p) {
   // around the DMA instructions.
   const int prow = lane / CH;                   // row within the piece
   const int schunk = (lane % CH) ^ kswz<BK>(prow);  // source chunk of this lane's LDS slot
-  // Per DMA row: element offset of the tap-(0,0) source pixel, and a validity mask over the taps
-  // (bit ty: row in range for tap row ty; bit 4+tx: column in range for tap column tx) -- the
-  // K loop then needs one add and a bit test per row instead of re-deriving and bounds-checking
-  // the im2col address (this VALU work, not the MFMA, bounded the first version of the loop).
+  // Per DMA row: element offset of the tap-(0,0) source pixel, and the set of out-of-range taps
+  // (bit t = ty << lg_tw | tx, the K loop's tap index; all bits for rows past M) -- the K loop then
+  // needs one add and a bit extract per row instead of re-deriving and bounds-checking the im2col
+  // address.  The in-range taps of one axis are an interval (closed form, tap_mask).
   const int ntap1 = 1 << p.lg_tw;
-  unsigned a_off0[AG], a_vm[AG];
+  unsigned a_off0[AG], a_inv[AG];
 #pragma unroll
   for (int g = 0; g < AG; ++g) {
     const int m = m0 + (wave * AG + g) * RPP + prow;
@@ -183,12 +196,8 @@ igemm_bf16_kernel(const GParams p) {
     const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
     const int ay = y * p.in_stride + p.offy[ph], ax = x * p.in_stride + p.offx[ph];
     a_off0[g] = (unsigned)(b * p.a_bs + p.a_co) + (unsigned)ay * (unsigned)p.a_rs + (unsigned)ax * (unsigned)p.a_ps;
-    unsigned vm = 0;
-    for (int tt = 0; tt < ntap1; ++tt) {
-      if ((unsigned)(ay + p.stepy * tt) < (unsigned)p.IH) vm |= 1u << tt;
-      if ((unsigned)(ax + p.stepx * tt) < (unsigned)p.IW) vm |= 1u << (4 + tt);
-    }
-    a_vm[g] = m < p.M ? vm : 0u;
+    const unsigned rm = tap_mask(ay, p.IH, p.stepy, ntap1), cmk = tap_mask(ax, p.IW, p.stepx, ntap1);
+    a_inv[g] = m < p.M ? ~(cmk * tap_spread(rm, p.lg_tw)) : ~0u;
   }
   unsigned b_off[BG];
 #pragma unroll
@@ -212,9 +221,8 @@ igemm_bf16_kernel(const GParams p) {
                            (unsigned)ccur;
 #pragma unroll
     for (int g = 0; g < AG; ++g) {
-      const unsigned ok = (a_vm[g] >> ty) & (a_vm[g] >> (4 + tx)) & 1u;
-      const unsigned off = ((a_off0[g] + delta) * 2u) | (ok ? kpen : OOB);
-      dma16(ra, sA + (wave * AG + g) * 1024, off);
+      const unsigned pen = (((a_inv[g] >> (tcur & 31)) & 1u) << 31) | kpen;
+      dma16(ra, sA + (wave * AG + g) * 1024, ((a_off0[g] + delta) * 2u) | pen);
     }
 #pragma unroll
     for (int g = 0; g < BG; ++g) {
@@ -321,68 +329,74 @@ igemm_bf16_kernel(const GParams p) {
   }
 
   __syncthreads();  // every wave is done with the stage buffers
-  float* red = reinterpret_cast<float*>(smem);  // [WM][BN] partials, then [BN] column means
   if (p.stats) {
-    const int mrem = p.M - m0;
-    const int nvalid = mrem < BM ? mrem : BM;
-    float s1[FN];
+    // BatchNorm batch statistics of the tile, one shifted pass per wave over its accumulators
+    // (shift = the column's value in the wave's first row: S1 = sum(x - shift), S2 = sum((x - shift)^2)),
+    // then the WM row-waves merged through LDS into the tile's {count, 0, M2, mean} (Chan).
+    const int rows_w = min(TM, max(0, p.M - (m0 + wm * TM)));
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][3] {S1, S2, shift}
+    float sh[FN], s1[FN], s2[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      float s = 0.f;
+      sh[j] = __shfl(acc[0][j][0], cl, 64);
+      s1[j] = 0.f;
+      s2[j] = 0.f;
+    }
+    if (rows_w == TM) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + 16 * i + rq + r;
-          s += row < nvalid ? acc[i][j][r] : 0.f;
-        }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      s1[j] = s;
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = acc[i][j][r] - sh[j];
+            s1[j] += d;
+            s2[j] = fmaf(d, d, s2[j]);
+          }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = 16 * i + rq + r < rows_w ? acc[i][j][r] - sh[j] : 0.f;
+            s1[j] += d;
+            s2[j] = fmaf(d, d, s2[j]);
+          }
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16, 64);
+      s1[j] += __shfl_xor(s1[j], 32, 64);
+      s2[j] += __shfl_xor(s2[j], 16, 64);
+      s2[j] += __shfl_xor(s2[j], 32, 64);
     }
     if (lane < 16) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + 16 * j + lane] = s1[j];
-    }
-    __syncthreads();
-    float* cmean = red + WM * BN;
-    for (int c = tid; c < BN; c += 64 * NW) {
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) s += red[w * BN + c];
-      cmean[c] = s / (float)nvalid;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const float mu = cmean[wn * TN + 16 * j + cl];
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + 16 * i + rq + r;
-          const float d = acc[i][j][r] - mu;
-          s += row < nvalid ? d * d : 0.f;
-        }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      s1[j] = s;
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + 16 * j + lane] = s1[j];
+      for (int j = 0; j < FN; ++j) {
+        float* q = red + (wm * BN + wn * TN + 16 * j + lane) * 3;
+        q[0] = s1[j]; q[1] = s2[j]; q[2] = sh[j];
+      }
     }
     __syncthreads();
     const long long tile = (long long)ph * p.mtiles + mt;
     for (int c = tid; c < BN; c += 64 * NW) {
       const int n = n0 + c;
       if (n >= p.N) continue;
-      float s = 0.f;
+      float cnt = 0.f, mean = 0.f, m2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < WM; ++w) s += red[w * BN + c];
-      float4 o = make_float4((float)nvalid, 0.f, s, cmean[c]);
-      *reinterpret_cast<float4*>(p.stats + (tile * p.N + n) * 4) = o;
+      for (int w = 0; w < WM; ++w) {
+        const float nw = (float)min(TM, max(0, p.M - (m0 + w * TM)));
+        if (nw <= 0.f) continue;
+        const float* q = red + (w * BN + c) * 3;
+        const float mw = q[2] + q[0] / nw, m2w = fmaxf(q[1] - q[0] * (q[0] / nw), 0.f);
+        const float nt = cnt + nw, dl = mw - mean;
+        mean += dl * (nw / nt);
+        m2 += m2w + dl * dl * (cnt * nw / nt);
+        cnt = nt;
+      }
+      *reinterpret_cast<float4*>(p.stats + (tile * p.N + n) * 4) = make_float4(cnt, 0.f, m2, mean);
     }
     __syncthreads();
   }
@@ -394,23 +408,23 @@ igemm_bf16_kernel(const GParams p) {
     // Column pairs: lanes l and l^1 hold columns c and c^1 of the same 4 rows; one DPP lane swap of two
     // values gives the even lane rows 0-1 and the odd lane rows 2-3 of the pair, each written as one
     // bf16x2 dword (half the LDS stores of per-element 16-bit writes)
-    const bool even = (cl & 1) == 0;
+    const unsigned em = (cl & 1) == 0 ? 0xffffffffu : 0u;  // even lane: all ones
     const int pcol = cl & ~1;
+    // em ? u : v as one v_bfi_b32 (a ternary on the lane parity became a dynamically indexed
+    // accumulator read -- a chain of compares and selects)
+    auto sel = [em](float u, float v) { return __uint_as_float((em & __float_as_uint(u)) | (~em & __float_as_uint(v))); };
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const float s0 = even ? acc[i][j][2] : acc[i][j][0];
-        const float s1 = even ? acc[i][j][3] : acc[i][j][1];
+        const float a0 = acc[i][j][0], a1 = acc[i][j][1], a2 = acc[i][j][2], a3 = acc[i][j][3];
         // quad_perm [1,0,3,2]: every lane receives its neighbour's value
-        const float x0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xF, 0xF, false));
-        const float x1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s1), 0xB1, 0xF, 0xF, false));
-        const float lo0 = even ? acc[i][j][0] : x0, hi0 = even ? x0 : acc[i][j][2];
-        const float lo1 = even ? acc[i][j][1] : x1, hi1 = even ? x1 : acc[i][j][3];
-        const int row = wm * TM + 16 * i + rq + (even ? 0 : 2), col = wn * TN + 16 * j + pcol;
+        const float x0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sel(a2, a0)), 0xB1, 0xF, 0xF, false));
+        const float x1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sel(a3, a1)), 0xB1, 0xF, 0xF, false));
+        const int row = wm * TM + 16 * i + rq + (em ? 0 : 2), col = wn * TN + 16 * j + pcol;
         char* dst = tl + row * PITCH + col * 2;
-        *reinterpret_cast<unsigned*>(dst) = (unsigned)f2bf(lo0) | ((unsigned)f2bf(hi0) << 16);
-        *reinterpret_cast<unsigned*>(dst + PITCH) = (unsigned)f2bf(lo1) | ((unsigned)f2bf(hi1) << 16);
+        *reinterpret_cast<unsigned*>(dst) = pack_bf16x2(sel(a0, x0), sel(x0, a2));
+        *reinterpret_cast<unsigned*>(dst + PITCH) = pack_bf16x2(sel(a1, x1), sel(x1, a3));
       }
     __syncthreads();
     constexpr int CPR = BN / 8;  // 16-byte chunks per row (64*NW is a multiple of CPR: fixed cc per thread)
@@ -419,16 +433,28 @@ igemm_bf16_kernel(const GParams p) {
     const int cc = tid % CPR;
     const int n = n0 + cc * 8;
     if constexpr (!BNB) {
+      // rows r0 + RS*it of this thread: the pixel (b, y, x) is advanced incrementally (element
+      // offsets < 2^31: vec_out is only set when the whole output view fits)
+      constexpr int RS = 64 * NW / CPR;
+      const int r0 = tid / CPR;
+      int m = m0 + r0;
+      int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+      int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+      const unsigned cbase = (unsigned)(p.c_co + n);
 #pragma unroll 4
       for (int it = 0; it < ITER; ++it) {
-        const int row = (tid + it * 64 * NW) / CPR;
-        const int m = m0 + row;
-        if (m >= p.M || n >= p.N) continue;
-        const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
-        const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+        if (m >= p.M || n >= p.N) break;
         const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
-        const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
+        const unsigned off = (unsigned)b * (unsigned)p.c_bs + (unsigned)oy * (unsigned)p.c_rs + (unsigned)ox * (unsigned)p.c_ps +
+                             cbase;
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) =
+            *reinterpret_cast<const uint4*>(tl + (r0 + it * RS) * PITCH + cc * 16);
+        m += RS;
+        x += RS;
+        while (x >= p.GW) {
+          x -= p.GW;
+          if (++y == p.GH) { y = 0; ++b; }
+        }
       }
       return;
     }
@@ -706,7 +732,7 @@ static size_t bf16_lds_bytes(int cfg) {
   const TileCfg& t = kTiles[cfg];
   size_t stage = (size_t)t.NST * (t.BM + t.BN) * t.BK * 2;
   size_t epi = (size_t)t.BM * (t.BN * 2 + 16);
-  size_t red = (size_t)(t.WM + 1) * t.BN * 4;
+  size_t red = (size_t)t.WM * t.BN * 3 * 4;
   return std::max(stage, std::max(epi, red));
 }
 
@@ -890,9 +916,10 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
 }
 
 // ---- conv-level wrappers (geometry -> GParams), used by stc_conv_fwd_query / stc_conv_fwd_ex
-static bool vec_out_ok(const stc_view& y, int out_f32) {
+static bool vec_out_ok(int B, const stc_view& y, int Cout, int out_f32) {
+  const long long extent = (long long)(B - 1) * y.bs + (long long)(y.H - 1) * y.rs + (long long)(y.W - 1) * y.ps + y.co + Cout;
   return !out_f32 && y.cs == 1 && y.co % 8 == 0 && y.ps % 8 == 0 && y.rs % 8 == 0 && y.bs % 8 == 0 &&
-         ((uintptr_t)y.p & 15) == 0;
+         ((uintptr_t)y.p & 15) == 0 && extent < (1ll << 31);
 }
 
 bool bf16_conv_eligible(int kind, int B, const stc_view& x, int Cin, int Cout) {
@@ -945,7 +972,7 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
   p.os = g.os;
   for (int i = 0; i < 4; ++i) { p.oy0[i] = g.nphase == 4 ? (i >> 1) : 0; p.ox0[i] = g.nphase == 4 ? (i & 1) : 0; }
   p.bias = bias; p.tanh_ = epi_tanh; p.out_f32 = out_f32;
-  p.vec_out = vec_out_ok(y, out_f32) && Cout % 8 == 0 ? 1 : 0;
+  p.vec_out = vec_out_ok(B, y, Cout, out_f32) && Cout % 8 == 0 ? 1 : 0;
   p.nphase = g.nphase;
   if (p.M == 0 || Cout == 0) return 0;
   STC_REQUIRE(!epi_tanh, "bf16 conv: the MFMA tile kernel has no tanh epilogue");

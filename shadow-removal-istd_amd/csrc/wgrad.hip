@@ -312,6 +312,46 @@ int64_t wgrad_reduce_blocks(int R, int Cg_out) {
   return std::min<long long>((total + 127) / 128, 16384);
 }
 
+// The same sum for small outputs over many slabs (the 3-8 channel first/last layers: P = B*256*256
+// pixels split up to 256 ways, R*Cg_out*4 < 8192 output units): one wave per (r, ci, 4 taps) unit,
+// lane l summing slabs l, l + 64, ... in order, then a fixed xor-butterfly across the lanes
+// (deterministic; a thread per unit walking 256 slabs serially was latency-bound at 40-70 us).
+__global__ void __launch_bounds__(256) wgrad_reduce_wide_kernel(const float* __restrict__ ws, int nsplit, int R, int Cg,
+                                                                int Cg_out, float* __restrict__ dW) {
+  const int lane = threadIdx.x & 63;
+  const long long unit = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long long total = (long long)R * Cg_out * 4;
+  if (unit >= total) return;
+  const int g = (int)(unit & 3);
+  const long long rc = unit >> 2;
+  const int ci = (int)(rc % Cg_out);
+  const int r = (int)(rc / Cg_out);
+  const long long Ncol = 16LL * Cg;
+  const long long slab = (long long)R * Ncol;
+  const float* src = ws + (long long)r * Ncol + (long long)(4 * g) * Cg + ci;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int sp = lane; sp < nsplit; sp += 64) {
+    const float* a = src + (long long)sp * slab;
+    acc.x += a[0]; acc.y += a[Cg]; acc.z += a[2 * Cg]; acc.w += a[3 * Cg];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    acc.x += __shfl_xor(acc.x, o, 64); acc.y += __shfl_xor(acc.y, o, 64);
+    acc.z += __shfl_xor(acc.z, o, 64); acc.w += __shfl_xor(acc.w, o, 64);
+  }
+  if (lane == 0) *reinterpret_cast<float4*>(dW + ((long long)r * Cg_out + ci) * 16 + 4 * g) = acc;
+}
+
+void wgrad_reduce_launch(const float* ws, int nsplit, int R, int Cg, int Cg_out, float* dW, hipStream_t st) {
+  const long long units = (long long)R * Cg_out * 4;
+  if (units < 8192 && nsplit >= 16)
+    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, st, ws, nsplit, R, Cg,
+                       Cg_out, dW);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)wgrad_reduce_blocks(R, Cg_out)), dim3(128), 0, st, ws,
+                       nsplit, R, Cg, Cg_out, dW);
+}
+
 struct WgPlan {
   int mtiles, ntiles, nsplit, pchunk;
 };
@@ -423,8 +463,7 @@ extern "C" int stc_conv_wgrad_ex(int dtype, int B, int stride, stc_view D, int R
   else hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(256), 0, st, p);
   main_timer_end(st);
   STC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)wgrad_reduce_blocks(R, Cg_out)), dim3(128), 0, st,
-                     (const float*)p.ws, pl.nsplit, R, Cg, Cg_out, dW);
+  wgrad_reduce_launch((const float*)p.ws, pl.nsplit, R, Cg, Cg_out, dW, st);
   STC_CHECK_LAUNCH();
   return 0;
 }

@@ -13,7 +13,7 @@
 // 256x256 / 256x128 / 128x256 tiles for the large layers (half the DMA bytes per MFMA of the
 // 128x128 tile: the L2->LDS stream, not the MFMA, bounds the small tiles).  2-stage ring (DMA of
 // step s+1 under the MFMAs of step s).  The pixel range is split over blockIdx.z into fp32 slabs
-// that wgrad_reduce_kernel sums in a fixed order; a single split writes torch layout directly.
+// that wgrad_reduce_launch sums in a fixed order; a single split writes torch layout directly.
 #include <algorithm>
 
 #include "common.hpp"
@@ -409,7 +409,7 @@ constexpr int kNumWbCfg = sizeof(kWbCfg) / sizeof(kWbCfg[0]);
 
 struct WbPlan {
   int cfg, BM, BN, mtiles, ntiles, nsplit, pchunk;
-  bool slab;  // partial sums go to fp32 slabs + wgrad_reduce_kernel (always when nsplit > 1)
+  bool slab;  // partial sums go to fp32 slabs + the ordered reduce (always when nsplit > 1)
 };
 
 // force (optional, per call: stc_conv_wgrad_ex / stc_conv_wgrad_query): {tile config 0..5, pixel
@@ -467,9 +467,7 @@ int64_t wgrad_bf16_workspace(int B, int Hd, int Wd, int R, int Cg, const int32_t
   return (int64_t)pl.nsplit * R * 16LL * Cg * 4;
 }
 
-__global__ void __launch_bounds__(128) wgrad_reduce_kernel(const float* ws, int nsplit, int R, int Cg, int Cg_out,
-                                                           float* dW);
-int64_t wgrad_reduce_blocks(int R, int Cg_out);
+void wgrad_reduce_launch(const float* ws, int nsplit, int R, int Cg, int Cg_out, float* dW, hipStream_t st);
 
 // plan_out = {tile config, BM, BN, pixel splits, slab (1: slabs + reduce kernel)}
 void wgrad_bf16_plan(int B, int Hd, int Wd, int R, int Cg, const int32_t* force, int32_t* plan_out) {
@@ -529,8 +527,7 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
   main_timer_end(st);
   STC_CHECK_LAUNCH();
   if (!pl.slab) return 0;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)wgrad_reduce_blocks(R, Cg_out)), dim3(128), 0, st,
-                     (const float*)p.ws, pl.nsplit, R, Cg, Cg_out, dW);
+  wgrad_reduce_launch((const float*)p.ws, pl.nsplit, R, Cg, Cg_out, dW, st);
   STC_CHECK_LAUNCH();
   return 0;
 }
