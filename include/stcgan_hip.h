@@ -334,6 +334,16 @@ int stc_warp_affine(const void* src, int src_u8, int B, int H, int W, int C, con
 int stc_adam_step(const int64_t* table, int ntensors, int64_t total_blocks,
                   float lr, float beta1, float beta2, float eps, int step, void* stream);
 int stc_adam_elems_per_block(void);
+/* Adam fused with the weight repack (replaces stc_adam_step + stc_pack_weights after a step):
+ * table = ntensors records of 24 int64
+ *   {param*, grad*, exp_avg*, exp_avg_sq*, numel, first_block, kind, P, Q, q_tiles, npacks,
+ *    npacks x {mode, out*, N_pad, C_pad, dtype}, padding}
+ * kind 0: a flat tensor, ceil(numel / 1024) blocks.  kind 1: a [P][Q][4][4] weight, one block per
+ * 16 x 16 (p, q) tile (q_tiles = ceil(Q / 16)), whose updated values are also written to each of
+ * its npacks (<= 2) packed operands exactly as stc_pack_weight(dtype, mode, ..., N_pad, C_pad)
+ * would (padding entries are left as they are).  Same Adam arithmetic as stc_adam_step.           */
+int stc_adam_pack_step(const int64_t* table, int ntensors, int64_t total_blocks,
+                       float lr, float beta1, float beta2, float eps, int step, void* stream);
 
 /* ---- misc ------------------------------------------------------------------------
  * stc_time_next_main_kernel: instrumentation (bench.py).  The next call ON THIS THREAD that launches a

@@ -46,9 +46,167 @@ __global__ void __launch_bounds__(ADAM_BLOCK) adam_kernel(const long long* table
   }
 }
 
+// ---- Adam + GEMM-operand repack in one pass (stc_adam_pack_step) ------------------------------
+// A 4x4 conv / convT weight [P][Q][4][4] is updated a 16x16 (p, q) tile per block (16 contiguous
+// runs of 16*16 floats, read and written with coalesced float4 accesses), with Adam exactly as
+// adam_kernel, and the new values also land in an LDS tile;
+// the block then writes each of the weight's packed GEMM operands (stc_pack_weights layouts: the
+// bf16 / fp32 copies the convolutions read) from that tile with 16-lane-contiguous stores.  The
+// separate pack pass -- re-reading every fp32 weight once per packed layout -- goes away.
+// Other tensors (biases, BatchNorm affine) and weights without a packed copy: 1024 elements per
+// block as adam_kernel.
+constexpr int AP_W = 24;  // int64 per table record
+// record: 0 param, 1 grad, 2 exp_avg, 3 exp_avg_sq, 4 numel, 5 first_block, 6 kind (0 flat, 1 4x4 weight),
+// 7 P, 8 Q, 9 q-tiles, 10 packs, then per pack (11 + 5j): mode, out, N_pad, C_pad, dtype
+
+__device__ __forceinline__ float adam_elem(float pi, float gi, float& mi, float& vi, float lr_over_bc1, float bc2_sqrt,
+                                           float beta1, float beta2, float eps) {
+  const float w = 1.f - beta1;
+  mi = fabsf(w) < 0.5f ? mi + w * (gi - mi) : gi - (gi - mi) * (1.f - w);
+  vi = vi * beta2 + (1.f - beta2) * (gi * gi);
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  return pi + (-lr_over_bc1) * (mi / denom);
+}
+
+__global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, int ntensors, float lr_over_bc1,
+                                                        float bc2_sqrt, float beta1, float beta2, float eps) {
+  __shared__ __attribute__((aligned(16))) float tile[16][16][20];  // [p][tap][q] (rows of 20: 16-byte aligned q quads)
+  int lo = 0, hi = ntensors - 1;
+  const int blk = blockIdx.x;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (table[mid * AP_W + 5] <= blk) lo = mid;
+    else hi = mid - 1;
+  }
+  const long long* rec = table + lo * AP_W;
+  float* p = reinterpret_cast<float*>(rec[0]);
+  const float* g = reinterpret_cast<const float*>(rec[1]);
+  float* m = reinterpret_cast<float*>(rec[2]);
+  float* v = reinterpret_cast<float*>(rec[3]);
+  const int b = blk - (int)rec[5];
+  if (rec[6] == 0) {
+    const long long n = rec[4];
+    const long long base = (long long)b * 1024;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long long i = base + (long long)k * 256 + threadIdx.x;
+      if (i >= n) break;
+      float mi = m[i], vi = v[i];
+      p[i] = adam_elem(p[i], g[i], mi, vi, lr_over_bc1, bc2_sqrt, beta1, beta2, eps);
+      m[i] = mi;
+      v[i] = vi;
+    }
+    return;
+  }
+  const int P = (int)rec[7], Q = (int)rec[8], qt = (int)rec[9];
+  const int p0 = (b / qt) * 16, q0 = (b % qt) * 16;
+  const int np = min(16, P - p0), nq = min(16, Q - q0);
+  // the tile's rows p are contiguous runs of nq*16 floats: wave w updates rows w, w+4, w+8, w+12,
+  // lane l the 4 floats at 4l of the run (one 1 KiB coalesced access per wave-instruction)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ql = lane >> 2, t0 = (lane & 3) * 4;
+  // all four rows' loads are issued before any store (p / m / v may alias as far as the compiler
+  // knows: stores between them would serialise the rows' memory latencies)
+  float4 pp[4], gg[4], mm[4], vv[4];
+  bool ok[4];
+  long long e0[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int pl = wave + 4 * r;
+    ok[r] = pl < np && ql < nq;
+    e0[r] = ok[r] ? ((long long)(p0 + pl) * Q + q0) * 16 + 4 * lane : 0;
+    if (ok[r]) {
+      pp[r] = *reinterpret_cast<const float4*>(p + e0[r]);
+      gg[r] = *reinterpret_cast<const float4*>(g + e0[r]);
+      mm[r] = *reinterpret_cast<const float4*>(m + e0[r]);
+      vv[r] = *reinterpret_cast<const float4*>(v + e0[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (!ok[r]) continue;
+    const int pl = wave + 4 * r;
+    float4 a = pp[r], mq = mm[r], vq = vv[r];
+    const float4 gq = gg[r];
+    a.x = adam_elem(a.x, gq.x, mq.x, vq.x, lr_over_bc1, bc2_sqrt, beta1, beta2, eps);
+    a.y = adam_elem(a.y, gq.y, mq.y, vq.y, lr_over_bc1, bc2_sqrt, beta1, beta2, eps);
+    a.z = adam_elem(a.z, gq.z, mq.z, vq.z, lr_over_bc1, bc2_sqrt, beta1, beta2, eps);
+    a.w = adam_elem(a.w, gq.w, mq.w, vq.w, lr_over_bc1, bc2_sqrt, beta1, beta2, eps);
+    *reinterpret_cast<float4*>(p + e0[r]) = a;
+    *reinterpret_cast<float4*>(m + e0[r]) = mq;
+    *reinterpret_cast<float4*>(v + e0[r]) = vq;
+    tile[pl][t0][ql] = a.x; tile[pl][t0 + 1][ql] = a.y;
+    tile[pl][t0 + 2][ql] = a.z; tile[pl][t0 + 3][ql] = a.w;
+  }
+  __syncthreads();
+  const int npk = (int)rec[10];
+  for (int j = 0; j < npk; ++j) {
+    const long long* pk = rec + 11 + 5 * j;
+    const int mode = (int)pk[0];
+    char* out = reinterpret_cast<char*>(pk[1]);
+    const int npad = (int)pk[2], cpad = (int)pk[3], f32 = (int)pk[4] == STC_F32;
+    const bool phased = mode == STC_PACK_CONV_DGRAD || mode == STC_PACK_CONVT_FWD;
+    const bool n_is_p = mode == STC_PACK_CONV_FWD || mode == STC_PACK_CONVT_DGRAD;
+    const int nb = n_is_p ? p0 : q0, cb = n_is_p ? q0 : p0;
+    // 4 consecutive c per thread-iteration (one 8- / 16-byte store), 4 iterations per thread
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      const int c4 = (idx & 3) * 4, rest = idx >> 2, nl = rest >> 4;
+      long long o;
+      int tap;
+      if (!phased) {
+        tap = rest & 15;
+        o = ((long long)(nb + nl) * 16 + tap) * cpad + cb + c4;
+      } else {
+        const int t = rest & 3, z = (rest >> 2) & 3, ph = z >> 1, pw = z & 1;
+        tap = ((1 - ph) + 2 * (t >> 1)) * 4 + (1 - pw) + 2 * (t & 1);
+        o = (((long long)z * npad + nb + nl) * 4 + t) * cpad + cb + c4;
+      }
+      // (p, q) of the 4 values: n_is_p -> p = nl, q = c4..c4+3; else q = nl, p = c4..c4+3
+      const int lim_n = n_is_p ? np : nq, lim_c = n_is_p ? nq : np;
+      if (nl >= lim_n || c4 >= lim_c) continue;
+      float w[4];
+      if (n_is_p) {
+        const float4 q4 = *reinterpret_cast<const float4*>(&tile[nl][tap][c4]);
+        w[0] = q4.x; w[1] = q4.y; w[2] = q4.z; w[3] = q4.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = tile[c4 + e][tap][nl];
+      }
+      if (c4 + 4 <= lim_c) {
+        if (f32) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) = make_float4(w[0], w[1], w[2], w[3]);
+        } else {
+          uint2 u;
+          u.x = pack_bf16x2(w[0], w[1]);
+          u.y = pack_bf16x2(w[2], w[3]);
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + o) = u;
+        }
+      } else {
+        for (int e = 0; e < lim_c - c4; ++e) {
+          if (f32) reinterpret_cast<float*>(out)[o + e] = w[e];
+          else st1<bf16>(reinterpret_cast<bf16*>(out) + o + e, w[e]);
+        }
+      }
+    }
+  }
+}
+
 }  // namespace stc
 
 using namespace stc;
+
+extern "C" int stc_adam_pack_step(const int64_t* table, int ntensors, int64_t total_blocks, float lr, float beta1,
+                                  float beta2, float eps, int step, void* stream) {
+  STC_REQUIRE(ntensors > 0 && step >= 1, "stc_adam_pack_step: bad arguments");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const long long*)table, ntensors, (float)((double)lr / bc1), (float)sqrt(bc2), beta1, beta2, eps);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int stc_adam_step(const int64_t* table, int ntensors, int64_t total_blocks, float lr, float beta1,
                              float beta2, float eps, int step, void* stream) {

@@ -858,7 +858,7 @@ extern "C" int stc_bn_finalize(const float* part, int nchunks, int C, const floa
     hipLaunchKernelGGL(bn_eval_table_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, running_mean,
                        running_var, eps, scale, shift);
   } else {
-    if (nchunks <= 8192)
+    if (nchunks <= 256)  // one 4-load group per lane; more chunks: a block per channel keeps more loads in flight
       hipLaunchKernelGGL(bn_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nchunks, C, gamma, beta,
                          running_mean, running_var, (long long*)num_batches_tracked, momentum, eps, mean, rstd, scale,
                          shift);
@@ -900,7 +900,7 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
   GradIn gi = mkgrad(g1, slope1, g2, slope2);
   if (mean) {
     STC_REQUIRE(part2 && dgamma && dbeta && gamma && rstd && scale && shift, "stc_bn_bwd_apply: missing BN tensors");
-    if (nchunks <= 8192)
+    if (nchunks <= 256)
       hipLaunchKernelGGL(bn_bwd_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part2, nchunks, C, dgamma, dbeta);
     else
       hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part2, nchunks, C, dgamma, dbeta);

@@ -285,6 +285,25 @@ def pack(mode, W, n_pad, c_pad, dt):
 
 # generation counter bumped by our optimizer (it updates parameters in place behind autograd's back)
 _GEN = {}
+# id(weight) -> {cache key: cache} of every packed operand made from it (the optimizer rewrites
+# them in the same pass as the update: stc_adam_pack_step)
+_PACK_OWNERS = {}
+
+
+def pack_version(W):
+    return (W._version, _GEN.get(id(W), 0), W.data_ptr())
+
+
+def pack_targets(W):
+    """[(key, cache, mode, out, n_pad, c_pad, dtype)] of the packed operands of weight W."""
+    out = []
+    for key, cache in _PACK_OWNERS.get(id(W), {}).items():
+        hit = cache.get(key)
+        if hit is None:
+            continue
+        _, mode, n_pad, c_pad, dt = cache["__keys__"][key]
+        out.append((key, cache, mode, hit[1], n_pad, c_pad, dt))
+    return out
 
 
 def bump(params):
@@ -301,6 +320,7 @@ def packed(cache, W, mode, n_pad, c_pad, dt):
     if hit is not None and hit[0] == ver:
         return hit[1]
     cache.setdefault("__keys__", {})[key] = (W, mode, n_pad, c_pad, dt)
+    _PACK_OWNERS.setdefault(id(W), {})[key] = cache
     t = pack(mode, W, n_pad, c_pad, dt)
     cache[key] = (ver, t)
     return t

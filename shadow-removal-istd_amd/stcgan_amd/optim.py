@@ -3,9 +3,13 @@
 Same constructor and ``step()/zero_grad()/state_dict()`` surface as
 torch.optim.Adam for the options the reference uses (lr, betas, eps;
 weight_decay=0, amsgrad=False).  The pointer table lives on the device and is
-rebuilt only when a tensor moved; ``step()`` never synchronises.
+rebuilt only when a tensor moved; ``step()`` never synchronises.  The 4x4
+weights' packed GEMM operands (ops.packed) are rewritten in the same launch as
+the update (stc_adam_pack_step), so the next forward finds them fresh.
 """
 import torch
+
+from . import _lib as L
 
 from . import ops
 from ._lib import check, lib, ptr, stream
@@ -17,6 +21,7 @@ class Adam(torch.optim.Optimizer):
             raise NotImplementedError("stcgan_amd Adam: weight_decay/amsgrad are not on the ST-CGAN path")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False))
         self._epb = None
+        self.fuse_pack = True  # False: update only (the packed operands are then refreshed lazily)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -54,21 +59,43 @@ class Adam(torch.optim.Optimizer):
             if step_tensors:
                 torch._foreach_add_(step_tensors, 1.0)
             for step, plist in by_step.items():
-                key = tuple((p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
-                             self.state[p]["exp_avg_sq"].data_ptr(), p.numel()) for p in plist)
+                recs = [self._record(p) for p in plist]
+                key = tuple(r[0] for r in recs)
                 cached = self._tables.get(gi)
                 if cached is not None and cached[0] == key:
                     table, blocks = cached[1], cached[2]
                 else:
-                    # pointer table, rebuilt only when a tensor moved (the caching allocator hands the
-                    # gradients the same blocks step after step); the device copy is stream-ordered
+                    # pointer table, rebuilt only when a tensor or packed operand moved (the caching
+                    # allocator hands the gradients the same blocks step after step); stream-ordered copy
                     rows, blocks = [], 0
-                    for (pp, gp, mp, vp, n) in key:
-                        rows.append([pp, gp, mp, vp, n, blocks])
-                        blocks += (n + self._epb - 1) // self._epb
+                    for row, nblk, _ in recs:
+                        rows.append(list(row[:5]) + [blocks] + list(row[5:]))
+                        blocks += nblk
                     table = torch.tensor(rows, dtype=torch.int64).to(plist[0].device)
                     self._tables[gi] = (key, table, blocks)
-                check(lib().stc_adam_step(ptr(table), len(key), blocks, float(group["lr"]), float(b1), float(b2),
-                                          float(group["eps"]), int(step), stream()), "stc_adam_step")
+                check(lib().stc_adam_pack_step(ptr(table), len(key), blocks, float(group["lr"]), float(b1),
+                                               float(b2), float(group["eps"]), int(step), stream()),
+                      "stc_adam_pack_step")
                 ops.bump(plist)
+                for p, (_, _, targets) in zip(plist, recs):  # the packed operands written above are current
+                    ver = ops.pack_version(p)
+                    for (pkey, cache, out) in targets:
+                        cache[pkey] = (ver, out)
         return loss
+
+    def _record(self, p):
+        """(table row without first_block, blocks, packed targets) of one parameter."""
+        st = self.state[p]
+        head = (p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(), p.numel())
+        is_w = self.fuse_pack and p.dim() == 4 and tuple(p.shape[2:]) == (4, 4)
+        targets = ops.pack_targets(p)[:2] if is_w else []
+        if not targets:
+            return head + (0, 0, 0, 0, 0) + (0,) * 13, (p.numel() + 1023) // 1024, []
+        P, Q = p.shape[0], p.shape[1]
+        qt = (Q + 15) // 16
+        packs = ()
+        for (_, _, mode, out, n_pad, c_pad, dt) in targets:
+            packs += (mode, out.data_ptr(), n_pad, c_pad, L.dtype_code(dt))
+        packs += (0,) * (10 - len(packs))
+        return (head + (1, P, Q, qt, len(targets)) + packs + (0,) * 3, ((P + 15) // 16) * qt,
+                [(t[0], t[1], t[3]) for t in targets])
