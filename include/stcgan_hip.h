@@ -158,6 +158,13 @@ int stc_conv_wgrad_ex(int dtype, int B, int stride,
                       float* dW, const int32_t* force_plan, void* workspace, int64_t workspace_bytes, void* stream);
 int stc_conv_wgrad_query(int dtype, int B, int Hd, int Wd, int R, int Cg, const int32_t* force_plan,
                          int64_t* workspace_bytes, int32_t* plan_out);
+/* Narrow-R stride-1 weight gradient (the PatchGAN logits layer, 512 -> 1: STCGAN/networks.py:183-184):
+ * as stc_conv_wgrad for stride 1 when only the first R_out (1..2) of the R channels of D are nonzero
+ * (channel padding); rows R_out..R-1 of dW are written as zeros.  D: [B][G.H-1][G.W-1][>=R],
+ * G: NHWC, Cg % 64 == 0, D plane in LDS.  Workspace: stc_conv_wgrad_rows_workspace(B, G.H, R_out, Cg). */
+int stc_conv_wgrad_rows(int dtype, int B, stc_view D, int R, int R_out, stc_view G, int Cg, int Cg_out,
+                        float* dW, void* workspace, int64_t workspace_bytes, void* stream);
+int64_t stc_conv_wgrad_rows_workspace(int B, int IH, int R_out, int Cg);
 
 /* ---- weight packing ----------------------------------------------------------
  * W is a torch weight [P][Q][4][4] fp32.  out is [phases][N_pad][T][C_pad] of dtype.

@@ -269,12 +269,16 @@ igemm_bf16_kernel(const GParams p) {
   };
 
   if constexpr (NST == 2) {
-    // DMA of step s+1 lands under the MFMAs of step s; vmcnt(0) + barrier per step.
+    // DMA of step s+1 lands under the MFMAs of step s; one barrier per step.  Both buffers are free
+    // at the start, so steps 0 and 1 are issued together (one memory latency, not two, before the
+    // first MFMA -- the whole K loop of the K <= 128 layers) and step 0 waits with step 1 in flight.
+    constexpr int P = AG + BG;
     if (nsteps > 0) issue(0);
+    if (nsteps > 1) issue(1);
     for (int s = 0; s < nsteps; ++s) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (s + 1 < nsteps) issue((s + 1) & 1);
+      wait_ahead<P>(s == 0 && nsteps > 1 ? 1 : 0);  // counted vmcnt + lgkmcnt(0), then a raw barrier
+      __builtin_amdgcn_s_barrier();
+      if (s > 0 && s + 1 < nsteps) issue((s + 1) & 1);
       compute(s & 1);
     }
   } else {

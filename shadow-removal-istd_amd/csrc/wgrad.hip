@@ -378,7 +378,154 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
                int64_t workspace_bytes, hipStream_t st, const int32_t* force);
 }  // namespace stc
 
+namespace stc {
+
+// ---- narrow-R weight gradient of a stride-1 4x4 conv (the PatchGAN logits layer, 512 -> 1 channel:
+// STCGAN/networks.py:183-184).  With RO <= 2 real rows the GEMM form is all im2col traffic (16 taps
+// of the 512-channel input, padded R); here each input pixel q is read ONCE and scattered into its 16
+// taps: dW[r][ci][kh][kw] += G[q][ci] * D[qy-kh+1][qx-kw+1][r].
+// Block = (image, 64-channel chunk, pixel split ps of 4), 256 threads = 16 channel quads x 16 pixel
+// lanes: lane l takes the image's pixels 16 ps + l + 64 k; the image's D plane (RO channels, zero-padded by 2) sits in LDS and is
+// read as broadcasts.  The 16 lanes' partials are summed in a fixed order (xor butterfly, then LDS) into the
+// slab [image][RO][16 * Cg] (column tap * Cg + ci), which the ordered wide reduce sums over images.
+template <typename T, int RO>
+__global__ void __launch_bounds__(256) wgrad_rows_kernel(const char* __restrict__ dp, long long d_bs, long long d_rs,
+                                                         int d_ps, int d_co, int OH, int OW, const char* __restrict__ gp,
+                                                         long long g_bs, long long g_rs, int g_ps, int g_co, int IH,
+                                                         int IW, int Cg, float* __restrict__ ws) {
+  extern __shared__ float sm[];
+  constexpr int PS = 4;  // pixel splits per (image, chunk): 4 blocks, lane stride 64
+  const int nchunk = Cg / 64;
+  const int ps = blockIdx.x % PS, bc = blockIdx.x / PS;
+  const int b = bc / nchunk, cc = bc % nchunk;
+  const float inv_iw = 1.0f / (float)IW;
+  const int rows = OH + 4, cols = OW + 4;  // D plane with a 2-wide zero border
+  float* dl = sm;                          // [RO][rows][cols]
+  const T* D = reinterpret_cast<const T*>(dp);
+  for (int i = threadIdx.x; i < RO * rows * cols; i += 256) {
+    const int r = i / (rows * cols), rem = i - r * rows * cols, yy = rem / cols, xx = rem - yy * cols;
+    const int oy = yy - 2, ox = xx - 2;
+    float v = 0.f;
+    if (oy >= 0 && oy < OH && ox >= 0 && ox < OW)
+      v = ld1<T>(D + (long long)b * d_bs + (long long)oy * d_rs + (long long)ox * d_ps + d_co + r);
+    dl[i] = v;
+  }
+  __syncthreads();
+  const int quad = threadIdx.x & 15, plane = threadIdx.x >> 4;
+  const int c0 = cc * 64 + quad * 4;
+  float acc[RO][16][4];
+#pragma unroll
+  for (int r = 0; r < RO; ++r)
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[r][t][e] = 0.f;
+  const T* G = reinterpret_cast<const T*>(gp) + (long long)b * g_bs + g_co + c0;
+  const int npix = IH * IW;
+  auto body = [&](int q, const float4 gq) {
+    const int qy = fast_div(q, IW, inv_iw), qx = q - qy * IW;
+    const float gv[4] = {gq.x, gq.y, gq.z, gq.w};
+    // D[qy - kh + 1][qx - kw + 1] sits at LDS (qy - kh + 3, qx - kw + 3)
+#pragma unroll
+    for (int r = 0; r < RO; ++r)
+#pragma unroll
+      for (int kh = 0; kh < 4; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 4; ++kw) {
+          const float dv = dl[(r * rows + qy - kh + 3) * cols + qx - kw + 3];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[r][kh * 4 + kw][e] = fmaf(gv[e], dv, acc[r][kh * 4 + kw][e]);
+        }
+  };
+  int q = plane + 16 * ps;
+  for (; q + 64 * 3 < npix; q += 64 * 4) {  // four pixels' loads in flight
+    float4 g4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int qq = q + 64 * u, qy = fast_div(qq, IW, inv_iw), qx = qq - qy * IW;
+      g4[u] = Vec4<T>::load(G + (long long)qy * g_rs + (long long)qx * g_ps);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) body(q + 64 * u, g4[u]);
+  }
+  for (; q < npix; q += 64) {
+    const int qy = fast_div(q, IW, inv_iw), qx = q - qy * IW;
+    body(q, Vec4<T>::load(G + (long long)qy * g_rs + (long long)qx * g_ps));
+  }
+  // fixed-order sum over the 16 pixel lanes: the 4 planes of a wave by an xor butterfly, then the 4
+  // waves through LDS (red[wave][r][t][64 channels], reusing the D plane area)
+#pragma unroll
+  for (int r = 0; r < RO; ++r)
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[r][t][e];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        acc[r][t][e] = v;
+      }
+  __syncthreads();
+  float* red = sm;
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < 16) {
+#pragma unroll
+    for (int r = 0; r < RO; ++r)
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+        *reinterpret_cast<float4*>(red + (((wave * RO + r) * 16 + t) * 64 + quad * 4)) =
+            make_float4(acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]);
+  }
+  __syncthreads();
+  float* slab = ws + ((long long)b * PS + ps) * RO * 16 * Cg;
+  for (int o = threadIdx.x; o < RO * 16 * 64; o += 256) {  // o = (r * 16 + t) * 64 + c
+    const float v = (red[o] + red[RO * 16 * 64 + o]) + (red[2 * RO * 16 * 64 + o] + red[3 * RO * 16 * 64 + o]);
+    slab[(long long)(o >> 6) * Cg + cc * 64 + (o & 63)] = v;
+  }
+}
+
+}  // namespace stc
+
 using namespace stc;
+
+extern "C" int64_t stc_conv_wgrad_rows_workspace(int B, int IH, int R_out, int Cg) {
+  (void)IH;
+  return (int64_t)B * 4 * R_out * 16LL * Cg * 4;  // a slab per (image, pixel split)
+}
+
+extern "C" int stc_conv_wgrad_rows(int dtype, int B, stc_view D, int R, int R_out, stc_view G, int Cg, int Cg_out,
+                                   float* dW, void* workspace, int64_t workspace_bytes, void* stream) {
+  STC_REQUIRE(dtype == STC_F32 || dtype == STC_BF16, "stc_conv_wgrad_rows: bad dtype");
+  STC_REQUIRE(R_out >= 1 && R_out <= 2 && R_out <= R, "stc_conv_wgrad_rows: R_out=%d (1..2, <= R)", R_out);
+  STC_REQUIRE(Cg % 64 == 0 && Cg_out <= Cg && G.cs == 1 && G.co % 4 == 0 && G.ps % 4 == 0 && D.cs == 1,
+              "stc_conv_wgrad_rows: Cg=%d / views (NHWC, Cg a multiple of 64, 4-channel aligned)", Cg);
+  STC_REQUIRE(D.H == G.H - 1 && D.W == G.W - 1, "stc_conv_wgrad_rows: stride-1 4x4 geometry needs D = G - 1 (%dx%d vs %dx%d)",
+              D.H, D.W, G.H, G.W);
+  hipStream_t st = (hipStream_t)stream;
+  const int blocks = B * (Cg / 64) * 4;
+  const int64_t need = stc_conv_wgrad_rows_workspace(B, G.H, R_out, Cg);
+  STC_REQUIRE(workspace && workspace_bytes >= need, "stc_conv_wgrad_rows: workspace %lld < %lld",
+              (long long)workspace_bytes, (long long)need);
+  const size_t lds = std::max((size_t)R_out * (D.H + 4) * (D.W + 4), (size_t)4 * R_out * 16 * 64) * 4;
+  STC_REQUIRE(lds <= 160 * 1024, "stc_conv_wgrad_rows: D plane too large for LDS (%dx%d)", D.H, D.W);
+  float* ws = (float*)workspace;
+  main_timer_begin(st);
+#define STC_WR(T_, RO_)                                                                                          \
+  hipLaunchKernelGGL((wgrad_rows_kernel<T_, RO_>), dim3(blocks), dim3(256), lds, st, (const char*)D.p, D.bs,    \
+                     D.rs, D.ps, D.co, D.H, D.W, (const char*)G.p, G.bs, G.rs, G.ps, G.co, G.H, G.W, Cg, ws)
+  if (dtype == STC_BF16) { if (R_out == 1) STC_WR(bf16, 1); else STC_WR(bf16, 2); }
+  else { if (R_out == 1) STC_WR(float, 1); else STC_WR(float, 2); }
+#undef STC_WR
+  main_timer_end(st);
+  STC_CHECK_LAUNCH();
+  wgrad_reduce_launch(ws, B * 4, R_out, Cg, Cg_out, dW, st);
+  STC_CHECK_LAUNCH();
+  if (R > R_out) {  // the zero rows of the padded D channels
+    (void)hipMemsetAsync(dW + (size_t)R_out * Cg_out * 16, 0, (size_t)(R - R_out) * Cg_out * 16 * 4, st);
+    STC_CHECK_LAUNCH();
+  }
+  return 0;
+}
 
 extern "C" int stc_conv_wgrad_query(int dtype, int B, int Hd, int Wd, int R, int Cg, const int32_t* force_plan,
                                     int64_t* workspace_bytes, int32_t* plan_out) {

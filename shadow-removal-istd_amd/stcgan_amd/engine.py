@@ -346,7 +346,7 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
         gv = L.nhwc_view(g, 0, h, w)  # gradient wrt conv_i output (pre-activation / pre-BN), gch channels
         if need_w:
             dW = ops.wgrad(B, s, gv, gch, L.nhwc_view(act[i]), chans[i], saved["cin"] if i == 0 else chans[i], dt,
-                           device=dev)
+                           device=dev, rows=cout)
             grads[id(cv.weight)] = dW[:cout] if gch != cout else dW
             if cv.bias is not None:
                 grads[id(cv.bias)] = ops.chan_sum(B, gv, gch, cout, dt, dev)

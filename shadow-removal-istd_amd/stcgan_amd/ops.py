@@ -240,9 +240,27 @@ def _wgrad_kernel_name(plan, Hd, Wd):
 
 
 def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None,
-          force=None):
-    """Weight gradient [R][Cg_out][4][4] fp32 (stc_conv_wgrad_ex; force = optional {tile config, splits})."""
+          force=None, rows=None):
+    """Weight gradient [R][Cg_out][4][4] fp32 (stc_conv_wgrad_ex; force = optional {tile config, splits}).
+    rows: the number of nonzero (real) channels of D when the rest is padding -- a stride-1 layer with
+    1-2 of them goes to stc_conv_wgrad_rows."""
     l = lib()
+    if (rows is not None and rows <= 2 and stride == 1 and dpro is None and gpro is None and dslope is None
+            and gslope is None and force is None and Cg % 64 == 0 and (Dv.H + 4) * (Dv.W + 4) * rows <= 40000):
+        nbytes = l.stc_conv_wgrad_rows_workspace(B, Gv.H, rows, Cg)
+        ws, nb = _ws(nbytes, device)
+        dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)
+        timer = _timer
+        if timer is not None:
+            e0, e1 = _main_events()
+        rc = l.stc_conv_wgrad_rows(L.dtype_code(dt), B, Dv, R, rows, Gv, Cg, Cg_out, ptr(dW), ptr(ws), nb, stream())
+        if timer is not None:
+            _disarm()
+        check(rc, "stc_conv_wgrad_rows")
+        if timer is not None:
+            timer.append(("wgrad_rows_kernel", True, 2.0 * B * Dv.H * Dv.W * R * 16 * Cg, e0, e1,
+                          f"wgrad s1 P={B * Dv.H * Dv.W} R{R} (real {rows}) Cg{Cg}"))
+        return dW
     nbytes, plan = wgrad_query(B, Dv.H, Dv.W, R, Cg, dt, force)
     ws, nb = _ws(nbytes, device)
     dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)

@@ -310,3 +310,25 @@ WGRAD_FORCED = [  # (case, tile config, pixel splits): the 8-wave tiles on ragge
 def test_wgrad_bf16_forced_tiles(case, cfg, ns):
     """Every weight-gradient tile configuration (a per-call plan of stc_conv_wgrad_ex) against autograd."""
     test_wgrad_bf16_dma(case, force=(cfg, ns))
+
+
+@pytest.mark.parametrize("B,Cin,H,W,rows,dt", [(4, 512, 31, 31, 1, BF), (2, 64, 9, 13, 2, BF), (3, 128, 17, 5, 1, torch.float32),
+                                              (1, 64, 6, 7, 2, torch.float32), (32, 512, 31, 31, 1, BF)])
+def test_wgrad_rows_narrow_s1(B, Cin, H, W, rows, dt):
+    """stc_conv_wgrad_rows (the PatchGAN logits layer: conv s1, 1-2 real output channels padded to 8):
+    vs torch autograd; padded rows zero."""
+    x = q(rnd(B, Cin, H, W, seed=71)) if dt == BF else rnd(B, Cin, H, W, seed=71)
+    w = torch.zeros(8, Cin, 4, 4, requires_grad=True)
+    y = F.conv2d(x, w, None, 1, 1)
+    dy = rnd(*y.shape, seed=72)
+    dy[:, rows:] = 0
+    dy = q(dy) if dt == BF else dy
+    (gw,) = torch.autograd.grad(y, w, dy)
+    dW = ops.wgrad(B, 1, L.nhwc_view(nhwc(dy).to(DEV, dt)), 8, L.nhwc_view(nhwc(x).to(DEV, dt)), Cin, Cin, dt,
+                   device=DEV, rows=rows)
+    torch.cuda.synchronize()
+    got = dW.cpu()
+    err = float((got - gw).abs().max())
+    scale = float(gw.abs().max())
+    assert err <= 2e-5 * scale + 1e-6, f"wgrad rows: {err:.3e} vs {scale:.3e}"
+    assert float(got[rows:].abs().max()) == 0.0
