@@ -95,6 +95,10 @@ using lds_vptr = __attribute__((address_space(3))) void*;
 
 constexpr unsigned OOB = 0x80000000u;
 
+#ifndef STC_IGEMM_INTERLEAVE
+#define STC_IGEMM_INTERLEAVE 0
+#endif
+
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)lds_dst, 16, voff, 0, 0, 0);
 }
@@ -212,24 +216,30 @@ igemm_bf16_kernel(const GParams p) {
   const bool cdivk = (BK % p.cin) == 0;
   const int tadv = cdivk ? BK / p.cin : 0;
 
-  auto issue = [&](int stage) {
+  // one K-step's DMA = AG + BG pieces; the step's shared terms (the K-tail penalty and the tap
+  // delta of this lane's K position) are computed once (prep), the pieces one at a time (piece),
+  // so that they can be spread between the MFMAs of the previous step (compute_il)
+  unsigned st_kpen = 0, st_delta = 0;
+  int st_tcur = 0;
+  auto prep = [&]() {
+    st_kpen = kcur < kend ? 0u : OOB;
+    const int ty = tcur >> p.lg_tw, tx = tcur & tw_mask;
+    st_delta = (unsigned)(p.stepy * ty) * (unsigned)p.a_rs + (unsigned)(p.stepx * tx) * (unsigned)p.a_ps + (unsigned)ccur;
+    st_tcur = tcur;
+  };
+  auto piece = [&](int stage, int g) {
     char* sA = smem + stage * STAGE;
     char* sB = sA + BM * RB;
-    const unsigned kpen = kcur < kend ? 0u : OOB;
-    const int ty = tcur >> p.lg_tw, tx = tcur & tw_mask;
-    const unsigned delta = (unsigned)(p.stepy * ty) * (unsigned)p.a_rs + (unsigned)(p.stepx * tx) * (unsigned)p.a_ps +
-                           (unsigned)ccur;
-#pragma unroll
-    for (int g = 0; g < AG; ++g) {
-      const unsigned pen = (((a_inv[g] >> (tcur & 31)) & 1u) << 31) | kpen;
-      dma16(ra, sA + (wave * AG + g) * 1024, ((a_off0[g] + delta) * 2u) | pen);
+    if (g < AG) {
+      const unsigned pen = (((a_inv[g] >> (st_tcur & 31)) & 1u) << 31) | st_kpen;
+      dma16(ra, sA + (wave * AG + g) * 1024, ((a_off0[g] + st_delta) * 2u) | pen);
+    } else {
+      const int h = g - AG;
+      const unsigned off = ((b_off[h] + (unsigned)(kcur)) * 2u) | st_kpen | (b_off[h] & OOB);
+      dma16(rb, sB + (wave * BG + h) * 1024, off);
     }
-#pragma unroll
-    for (int g = 0; g < BG; ++g) {
-      const unsigned off = ((b_off[g] + (unsigned)kcur) * 2u) | kpen | (b_off[g] & OOB);
-      dma16(rb, sB + (wave * BG + g) * 1024, off);
-    }
-    // advance to the next K-step
+  };
+  auto advance = [&]() {  // to the next K-step
     kcur += BK;
     if (cdivk) {
       tcur += tadv;
@@ -237,6 +247,12 @@ igemm_bf16_kernel(const GParams p) {
       ccur += BK;
       while (ccur >= p.cin) { ccur -= p.cin; ++tcur; }
     }
+  };
+  auto issue = [&](int stage) {
+    prep();
+#pragma unroll
+    for (int g = 0; g < AG + BG; ++g) piece(stage, g);
+    advance();
   };
 
   floatx4 acc[FM][FN];
@@ -268,7 +284,46 @@ igemm_bf16_kernel(const GParams p) {
     }
   };
 
-  if constexpr (NST == 2) {
+  // compute with the next step's DMA pieces interleaved: one piece after each MFMA row (FN MFMAs),
+  // so the wave's LDS-DMA issue overlaps its own queued MFMAs instead of preceding all of them
+  auto compute_il = [&](int stage, int nstage, bool dma) {
+    const char* sA = smem + stage * STAGE + (wm * TM) * RB;
+    const char* sB = smem + stage * STAGE + BM * RB + (wn * TN) * RB;
+    if (dma) prep();
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8_t fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + i * 16 * RB + rd_off[kk]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sB + j * 16 * RB + rd_off[kk]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        const int slot = kk * FM + i;
+        if (dma && slot < AG + BG) {
+          piece(nstage, slot);
+          __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);  // the row's MFMAs, then the piece
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+      }
+    }
+    if (dma) {
+#pragma unroll
+      for (int g = KK * FM; g < AG + BG; ++g) piece(nstage, g);
+      advance();
+    }
+  };
+
+  if constexpr (NST == 2 && STC_IGEMM_INTERLEAVE) {
+    if (nsteps > 0) issue(0);
+    for (int s = 0; s < nsteps; ++s) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      compute_il(s & 1, (s + 1) & 1, s + 1 < nsteps);
+    }
+  } else if constexpr (NST == 2) {
     // DMA of step s+1 lands under the MFMAs of step s; one barrier per step.  Both buffers are free
     // at the start, so steps 0 and 1 are issued together (one memory latency, not two, before the
     // first MFMA -- the whole K loop of the K <= 128 layers) and step 0 waits with step 1 in flight.
