@@ -63,7 +63,7 @@ def warp_affine(images, mats):
     images: uint8 (normalised on the fly) or fp32 NHWC CUDA tensor; mats: [B, 2, 3] float64."""
     src = _nhwc(images).contiguous()
     B, H, W, C = src.shape
-    M = torch.as_tensor(np.ascontiguousarray(mats, np.float64).reshape(B, 6)).to(src.device)
+    M = torch.as_tensor(np.ascontiguousarray(mats, np.float64).reshape(B, 6)).pin_memory().to(src.device, non_blocking=True)
     out = torch.empty((B, H, W, C), dtype=torch.float32, device=src.device)
     check(lib().stc_warp_affine(ptr(src), int(src.dtype == torch.uint8), B, H, W, C, ptr(M), ptr(out), stream()),
           "stc_warp_affine")
@@ -116,7 +116,7 @@ def prepare(images, params, geom):
     src = images.contiguous()
     B, H, W, C = src.shape
     pad_h, pad_w, OH, OW = geom
-    p = torch.as_tensor(np.ascontiguousarray(params, np.int32)).to(src.device)
+    p = torch.as_tensor(np.ascontiguousarray(params, np.int32)).pin_memory().to(src.device, non_blocking=True)
     out = torch.empty((B, C, OH, OW), dtype=torch.float32, device=src.device)
     if src.dtype == torch.uint8:
         check(lib().stc_prepare_batch(ptr(src), B, H, W, C, ptr(p), pad_h, pad_w, OH, OW, ptr(out), stream()),

@@ -65,13 +65,15 @@ class Adam(torch.optim.Optimizer):
                 if cached is not None and cached[0] == key:
                     table, blocks = cached[1], cached[2]
                 else:
-                    # pointer table, rebuilt only when a tensor or packed operand moved (the caching
-                    # allocator hands the gradients the same blocks step after step); stream-ordered copy
+                    # pointer table, rebuilt when a tensor or packed operand moved (the gradients are new
+                    # tensors every step, so in practice every step: a few hundred rows)
                     rows, blocks = [], 0
                     for row, nblk, _ in recs:
                         rows.append(list(row[:5]) + [blocks] + list(row[5:]))
                         blocks += nblk
-                    table = torch.tensor(rows, dtype=torch.int64).to(plist[0].device)
+                    # pinned + non_blocking: a stream-ordered copy -- a pageable H2D copy would block the
+                    # host until the GPU has drained everything queued before it (one full step)
+                    table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(plist[0].device, non_blocking=True)
                     self._tables[gi] = (key, table, blocks)
                 check(lib().stc_adam_pack_step(ptr(table), len(key), blocks, float(group["lr"]), float(b1),
                                                float(b2), float(group["eps"]), int(step), stream()),
