@@ -225,7 +225,9 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
                 gx = _nhwc(B, 2 * S[1][0], 2 * S[1][1], saved["cin_pad"], dt, dev)
                 ops.conv(L.CONVT_S2, B, drv, co[0], wd, saved["cin_pad"], L.nhwc_view(gx), dt)
                 H, W = S[0]
-                src_grads = [torch.zeros((B, c, H, W), dtype=torch.float32, device=dev) for c in saved["src_c"]]
+                # only the sources that need a gradient; the scatter writes every element of those
+                src_grads = [torch.empty((B, c, H, W), dtype=torch.float32, device=dev) if nd else None
+                             for c, nd in zip(saved["src_c"], need_src)]
                 ops.scatter(gx, src_grads, saved["src_c"], dt, H, W)
             break
         cprev = co[k - 1]
@@ -356,7 +358,9 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
                 H, W = dims[0]
                 gx = _nhwc(B, 2 * h, 2 * w, saved["cin_pad"], dt, dev)
                 ops.conv(L.CONVT_S2, B, gv, gch, wd, saved["cin_pad"], L.nhwc_view(gx), dt)
-                src_grads = [torch.zeros((B, c, H, W), dtype=torch.float32, device=dev) for c in saved["src_c"]]
+                # only the sources that need a gradient; the scatter writes every element of those
+                src_grads = [torch.empty((B, c, H, W), dtype=torch.float32, device=dev) if nd else None
+                             for c, nd in zip(saved["src_c"], need_src)]
                 ops.scatter(gx, src_grads, saved["src_c"], dt, H, W)
             break
         # input gradient of conv_i (grad wrt act[i])
@@ -414,7 +418,7 @@ class NetFn(torch.autograd.Function):
         if saved is None:
             raise RuntimeError("stcgan_amd: backward through a network called in eval mode is not supported")
         need = ctx.needs_input_grad[1:]
-        need_src = any(need[:nsrc])
+        need_src = list(need[:nsrc]) if any(need[:nsrc]) else None  # per source, or None
         need_w = any(need[nsrc:])
         bwd = gen_backward if kind == "G" else disc_backward
         src_grads, grads = bwd(plan, saved, gout, dt, cache, need_src, need_w)
