@@ -676,7 +676,8 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
 bool bf16_narrow_eligible(int kind, int Cin, int Cout);
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout);
 int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
-                    const float* bias, int epi_tanh, int out_f32, void* ws, int64_t ws_bytes, hipStream_t st);
+                    const float* bias, int epi_tanh, int out_f32, void* ws, int64_t ws_bytes, hipStream_t st,
+                    const int32_t* force = nullptr);
 }  // namespace stc
 
 // bf16 operands on the LDS-DMA kernel (igemm_bf16.hip) whenever the shape allows (no prologue,
@@ -755,6 +756,10 @@ extern "C" int stc_conv_fwd_ex(int dtype, int kind, int B, stc_view x, int Cin, 
   if (bf16_path(dtype, kind, Cin, Cout) && !epi_tanh && bf16_conv_eligible(kind, B, x, Cin, Cout))
     return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, epi_tanh, out_f32, stats_part, stats_chunks,
                          force_plan, workspace, workspace_bytes, st);
+  if (force_plan && stats_part == nullptr && dtype == STC_BF16 && use_smalln(dtype, Cout, 16 * Cin) &&
+      bf16_narrow_eligible(kind, Cin, Cout))  // tuning hook: force_plan = {tile rows, 16-column blocks}
+    return bf16_narrow_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, epi_tanh, out_f32, workspace, workspace_bytes, st,
+                           force_plan);
   const int rc = stc_conv_fwd(dtype, kind, B, x, Cin, nullptr, nullptr, 0, 0.f, w_packed, Cout, y, bias, epi_tanh,
                               out_f32, workspace, workspace_bytes, stream);
   if (rc != 0 || stats_part == nullptr) return rc;

@@ -51,9 +51,13 @@ __device__ __forceinline__ void store_out(const HParams& p, long long off, float
 
 // GEOM 0: ConvT k4 s2 (4 phases, 3x3 neighbourhood, NB column blocks of 16: N' = 4N <= 16*NB)
 // GEOM 1: Conv k4 s1 (16 taps, 4x4 neighbourhood, N' = N <= 16)
-template <int GEOM, int NB, int TY>
+// Tile: TY grid rows x 16*TXB grid columns; wave w owns rows [w*TY/4, (w+1)*TY/4) and all TXB
+// 16-wide column blocks, so each B fragment (held in registers) feeds ROWS*TXB MFMAs.  The DMA of
+// chunk c+1 is issued before chunk c's wait (counted vmcnt: the B fragments of chunk c are issued
+// first, so they retire before it).
+template <int GEOM, int NB, int TY, int TXB>
 __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
-  constexpr int TX = 16;
+  constexpr int TX = 16 * TXB;
   constexpr int HALO = GEOM == 0 ? 2 : 3;
   constexpr int RY = TY + HALO, RX = TX + HALO;
   constexpr int NPIX = RY * RX;
@@ -61,6 +65,7 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
   constexpr int STAGE = PIECES * 1024;
   constexpr int NBR = GEOM == 0 ? 9 : 16;  // neighbour offsets
   constexpr int ROWS = TY / 4;             // grid rows per wave
+  constexpr int WP = (PIECES + 3) / 4;     // DMA pieces per wave (upper bound)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -79,7 +84,10 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
   auto issue = [&](int chunk, int stage) {
     char* dst = smem + stage * STAGE;
     const int ci = chunk * 64 + schunk * 8;
-    for (int pc = wave; pc < PIECES; pc += 4) {
+#pragma unroll
+    for (int k = 0; k < WP; ++k) {
+      const int pc = wave + 4 * k;
+      if (pc >= PIECES) break;
       const int pix = pc * 8 + (lane >> 3);
       const int py = pix / RX, px = pix - py * RX;
       const int iy = y0 - 1 + py, ix = x0 - 1 + px;
@@ -89,6 +97,8 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
       hdma16(ra, dst + pc * 1024, off);
     }
   };
+  // this wave's DMA pieces per chunk (the count vmcnt leaves in flight while chunk c is consumed)
+  const int my_pieces = (PIECES - wave + 3) / 4;
 
   // B fragment of (neighbour nb, column block j, half kk) for this lane: column n' = 16j + (lane & 15),
   // k = 8*(lane>>4) .. +8 within the 32-channel half.
@@ -115,19 +125,18 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
     return v;
   };
 
-  floatx4 acc[ROWS][NB];
+  floatx4 acc[ROWS][TXB][NB];
 #pragma unroll
   for (int r = 0; r < ROWS; ++r)
 #pragma unroll
-    for (int j = 0; j < NB; ++j) acc[r][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int cx = 0; cx < TXB; ++cx)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) acc[r][cx][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int gx = lane & 15;
   if (cbeg < cend) issue(cbeg, 0);
   int stage = 0;
   for (int ch = cbeg; ch < cend; ++ch) {
-    // this chunk's B fragments go to registers BEFORE the next chunk's DMA is issued: vmcnt
-    // retires in issue order, so a weight load issued behind that DMA would make the MFMAs of
-    // this chunk wait for the next chunk's pixels (no DMA / compute overlap at all)
     bf16x8_h bfr[2][NBR][NB];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -135,9 +144,24 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
       for (int nb = 0; nb < NBR; ++nb)
 #pragma unroll
         for (int j = 0; j < NB; ++j) bfr[kk][nb][j] = load_b(ch, nb, j, kk);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (ch + 1 < cend) issue(ch + 1, stage ^ 1);
+    // all waves finished reading stage^1 (chunk ch-1) before it is refilled with chunk ch+1
+    if (ch > cbeg) __builtin_amdgcn_s_barrier();
+    const bool pre = ch + 1 < cend;
+    if (pre) issue(ch + 1, stage ^ 1);
+    // chunk ch's pixels and B fragments landed; chunk ch+1's pieces may stay in flight
+    if (pre) {
+      switch (my_pieces) {  // vmcnt takes an immediate
+#define STC_VM(n) case n: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory"); break;
+        STC_VM(1) STC_VM(2) STC_VM(3) STC_VM(4) STC_VM(5) STC_VM(6) STC_VM(7) STC_VM(8) STC_VM(9) STC_VM(10)
+        STC_VM(11) STC_VM(12) STC_VM(13) STC_VM(14) STC_VM(15) STC_VM(16) STC_VM(17) STC_VM(18) STC_VM(19) STC_VM(20)
+        STC_VM(21) STC_VM(22) STC_VM(23) STC_VM(24) STC_VM(25) STC_VM(26) STC_VM(27) STC_VM(28) STC_VM(29) STC_VM(30)
+#undef STC_VM
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
     const char* sT = smem + stage * STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -147,49 +171,53 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
         const int dy = GEOM == 0 ? nb / 3 - 1 : nb / 4 - 1;
         const int dx = GEOM == 0 ? nb % 3 - 1 : nb % 4 - 1;
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) {
-          const int py = wave * ROWS + r + dy + 1, px = gx + dx + 1;
-          const int pix = py * RX + px;
-          const bf16x8_h af = *reinterpret_cast<const bf16x8_h*>(sT + pix * 128 + ((cslot ^ (pix & 7)) * 16));
+        for (int r = 0; r < ROWS; ++r)
 #pragma unroll
-          for (int j = 0; j < NB; ++j)
-            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[kk][nb][j], acc[r][j], 0, 0, 0);
-        }
+          for (int cx = 0; cx < TXB; ++cx) {
+            const int py = wave * ROWS + r + dy + 1, px = 16 * cx + gx + dx + 1;
+            const int pix = py * RX + px;
+            const bf16x8_h af = *reinterpret_cast<const bf16x8_h*>(sT + pix * 128 + ((cslot ^ (pix & 7)) * 16));
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+              acc[r][cx][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[kk][nb][j], acc[r][cx][j], 0, 0, 0);
+          }
       }
     }
     stage ^= 1;
   }
 
-  // ---- epilogue: acc[r][j][e] = grid point (y0 + wave*ROWS + r, x0 + 4*(lane>>4) + e), column 16j + (lane&15)
+  // ---- epilogue: acc[r][cx][j][e] = grid point (y0 + wave*ROWS + r, x0 + 16 cx + 4*(lane>>4) + e), column 16j + (lane&15)
   const int np_l = lane & 15;
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) {
     const int gy = y0 + wave * ROWS + r;
     if (gy >= p.GH) continue;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int gxx = x0 + 4 * (lane >> 4) + e;
-      if (gxx >= p.GW) continue;
+    for (int cx = 0; cx < TXB; ++cx)
 #pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const int np = 16 * j + np_l;
-        if (np >= p.NP) continue;
-        float v = acc[r][j][e];
-        if (p.nsplit > 1) {
-          const long long m = ((long long)img * p.GH + gy) * p.GW + gxx;
-          p.ws[((long long)split * p.Mtot + m) * p.NP + np] = v;
-          continue;
+      for (int e = 0; e < 4; ++e) {
+        const int gxx = x0 + 16 * cx + 4 * (lane >> 4) + e;
+        if (gxx >= p.GW) continue;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const int np = 16 * j + np_l;
+          if (np >= p.NP) continue;
+          float v = acc[r][cx][j][e];
+          if (p.nsplit > 1) {
+            const long long m = ((long long)img * p.GH + gy) * p.GW + gxx;
+            p.ws[((long long)split * p.Mtot + m) * p.NP + np] = v;
+            continue;
+          }
+          int ph = 0, n = np;
+          if (GEOM == 0) { ph = np / p.N; n = np - ph * p.N; }
+          if (p.bias) v += p.bias[n];
+          if (p.tanh_) v = tanhf(v);
+          const int oy = GEOM == 0 ? 2 * gy + (ph >> 1) : gy;
+          const int ox = GEOM == 0 ? 2 * gxx + (ph & 1) : gxx;
+          store_out(p, (long long)img * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps +
+                           (long long)(p.c_co + n) * p.c_cs, v);
         }
-        int ph = 0, n = np;
-        if (GEOM == 0) { ph = np / p.N; n = np - ph * p.N; }
-        if (p.bias) v += p.bias[n];
-        if (p.tanh_) v = tanhf(v);
-        const int oy = GEOM == 0 ? 2 * gy + (ph >> 1) : gy;
-        const int ox = GEOM == 0 ? 2 * gxx + (ph & 1) : gxx;
-        store_out(p, (long long)img * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps +
-                         (long long)(p.c_co + n) * p.c_cs, v);
       }
-    }
   }
 }
 
@@ -218,17 +246,24 @@ __global__ void narrow_reduce_kernel(const HParams p, int B) {
 }
 
 // ------------------------------------------------------------------------- host
-static size_t halo_lds(int geom, int ty) {
+static size_t halo_lds(int geom, int ty, int txb, int nstage) {
   const int halo = geom == 0 ? 2 : 3;
-  const int npix = (ty + halo) * (16 + halo);
-  return 2 * (size_t)((npix + 7) / 8) * 1024;
+  const int npix = (ty + halo) * (16 * txb + halo);
+  return (size_t)nstage * (size_t)((npix + 7) / 8) * 1024;
 }
 
-// Narrow plan: {ty, nsplit}.  Enough blocks to cover the chip ~2x.
-static void narrow_plan(int geom, int B, int GH, int GW, int cin, int* ty, int* nsplit) {
-  *ty = 8;  // (TY = 16: fewer, larger halo tiles -- measured slower, occupancy-bound)
+// Narrow plan: {ty, txb, nsplit}.  Taller / wider tiles reuse each register-held B fragment over more
+// MFMAs; the split over channel chunks keeps >= 1024 blocks on the long reductions.
+static void narrow_plan(int geom, int B, int GH, int GW, int cin, const int32_t* force, int* ty, int* txb,
+                        int* nsplit) {
+  *ty = 8;
+  *txb = 1;
+  if (force && force[0] > 0) {
+    *ty = force[0];
+    *txb = force[1] > 0 ? force[1] : 1;
+  }
   const int nchunks = cin / 64;
-  const long long blocks = (long long)B * cdiv(GH, *ty) * cdiv(GW, 16);
+  const long long blocks = (long long)B * cdiv(GH, *ty) * cdiv(GW, 16 * *txb);
   int ns = 1;
   while (blocks * ns < 1024 && ns * 2 <= nchunks) ns *= 2;
   *nsplit = ns;
@@ -242,15 +277,16 @@ bool bf16_narrow_eligible(int kind, int Cin, int Cout) {
 
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout) {
   const int geom = kind == STC_CONVT_S2 ? 0 : 1;
-  int ty, ns;
-  narrow_plan(geom, B, GH, GW, Cin, &ty, &ns);
+  int ty, txb, ns;
+  narrow_plan(geom, B, GH, GW, Cin, nullptr, &ty, &txb, &ns);
   if (ns <= 1) return 0;
   const int np = geom == 0 ? 4 * Cout : Cout;
   return (int64_t)ns * B * GH * GW * np * 4;
 }
 
 int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
-                    const float* bias, int epi_tanh, int out_f32, void* ws, int64_t ws_bytes, hipStream_t st) {
+                    const float* bias, int epi_tanh, int out_f32, void* ws, int64_t ws_bytes, hipStream_t st,
+                    const int32_t* force) {
   const int geom = kind == STC_CONVT_S2 ? 0 : 1;
   HParams p{};
   p.a = (const char*)x.p;
@@ -269,9 +305,9 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
   p.c = (char*)y.p; p.c_bs = y.bs; p.c_rs = y.rs; p.c_ps = y.ps; p.c_co = y.co; p.c_cs = y.cs;
   p.bias = bias; p.tanh_ = epi_tanh; p.out_f32 = out_f32;
   p.Mtot = (long long)B * p.GH * p.GW;
-  int ty, ns;
-  narrow_plan(geom, B, p.GH, p.GW, Cin, &ty, &ns);
-  p.tiles_x = cdiv(p.GW, 16);
+  int ty, txb, ns;
+  narrow_plan(geom, B, p.GH, p.GW, Cin, force, &ty, &txb, &ns);
+  p.tiles_x = cdiv(p.GW, 16 * txb);
   p.tiles_per_img = p.tiles_x * cdiv(p.GH, ty);
   const int nchunks = Cin / 64;
   p.chunks_per_split = cdiv(nchunks, ns);
@@ -283,14 +319,25 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
   }
   if ((long long)B * p.GH * p.GW == 0) return 0;
   dim3 grid((unsigned)(B * p.tiles_per_img), (unsigned)p.nsplit);
-  const size_t lds = halo_lds(geom, ty);
+  const size_t lds = halo_lds(geom, ty, txb, p.chunks_per_split > 1 ? 2 : 1);
+  STC_REQUIRE(lds <= 160 * 1024, "narrow bf16: tile %dx%d needs %zu B of LDS", ty, 16 * txb, lds);
   main_timer_begin(st);
+#define STC_NH(G_, NB_, TY_, TXB_) hipLaunchKernelGGL((narrow_halo_kernel<G_, NB_, TY_, TXB_>), grid, dim3(256), lds, st, p)
+#define STC_NH_T(G_, NB_)                                                                  \
+  if (ty == 8 && txb == 1) STC_NH(G_, NB_, 8, 1);                                          \
+  else if (ty == 8 && txb == 2) STC_NH(G_, NB_, 8, 2);                                     \
+  else if (ty == 16 && txb == 1) STC_NH(G_, NB_, 16, 1);                                   \
+  else if (ty == 16 && txb == 2) STC_NH(G_, NB_, 16, 2);                                   \
+  else if (ty == 32 && txb == 1) STC_NH(G_, NB_, 32, 1);                                   \
+  else return fail(-1, "narrow bf16: no kernel for a %dx%d tile", ty, 16 * txb);
   if (geom == 0) {
-    if (p.NP <= 16) hipLaunchKernelGGL((narrow_halo_kernel<0, 1, 8>), grid, dim3(256), lds, st, p);
-    else hipLaunchKernelGGL((narrow_halo_kernel<0, 2, 8>), grid, dim3(256), lds, st, p);
+    if (p.NP <= 16) { STC_NH_T(0, 1) }
+    else { STC_NH_T(0, 2) }
   } else {
-    hipLaunchKernelGGL((narrow_halo_kernel<1, 1, 8>), grid, dim3(256), lds, st, p);
+    STC_NH_T(1, 1)
   }
+#undef STC_NH_T
+#undef STC_NH
   main_timer_end(st);
   STC_CHECK_LAUNCH();
   if (p.nsplit > 1) {
