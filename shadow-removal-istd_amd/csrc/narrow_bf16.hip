@@ -35,6 +35,7 @@ struct HParams {
   int chunks_per_split, nsplit;
   float* ws;  // [split][Mtot][NP] when nsplit > 1
   long long Mtot;  // B * GH * GW
+  const char* frag;  // B fragment table (narrow_bfrag_kernel), in the workspace
 };
 
 typedef __bf16 bf16x8_h __attribute__((ext_vector_type(8)));
@@ -47,6 +48,34 @@ __device__ __forceinline__ void hdma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, 
 __device__ __forceinline__ void store_out(const HParams& p, long long off, float v) {
   if (p.out_f32) reinterpret_cast<float*>(p.c)[off] = v;
   else st1<bf16>(reinterpret_cast<bf16*>(p.c) + off, v);
+}
+
+// B fragments in MFMA order: frag[((chunk * 2 + kk) * NBR + nb) * NB + j][lane] (16 B each), so that the
+// main kernel loads them as whole 1 KiB wave rows with no address arithmetic.  Fragment (nb, j, kk)
+// of lane l: column n' = 16j + (l & 15) -> (phase, channel) = (n' / N, n' % N), channels
+// 8(l >> 4) .. +8 of the 32-channel half kk; zero where the (phase, neighbour) pair reads no tap.
+template <int GEOM, int NB>
+__global__ void __launch_bounds__(64) narrow_bfrag_kernel(const HParams p, uint4* __restrict__ frag) {
+  constexpr int NBR = GEOM == 0 ? 9 : 16;
+  const int f = blockIdx.x, lane = threadIdx.x;  // f = ((chunk * 2 + kk) * NBR + nb) * NB + j
+  const int j = f % NB, nb = (f / NB) % NBR, kk = (f / (NB * NBR)) % 2, chunk = f / (NB * NBR * 2);
+  const int np = 16 * j + (lane & 15);
+  const int c = chunk * 64 + kk * 32 + 8 * (lane >> 4);
+  int tap = -1, ph = 0, n = np;
+  if (GEOM == 0) {
+    const int dy = nb / 3 - 1, dx = nb % 3 - 1;
+    ph = np / p.N;
+    n = np - ph * p.N;
+    const int ty = (ph >> 1) - dy, tx = (ph & 1) - dx;
+    if (np < p.NP && ty >= 0 && ty <= 1 && tx >= 0 && tx <= 1) tap = ty * 2 + tx;
+  } else {
+    if (np < p.NP) tap = nb;  // tap index = (dy+1)*4 + (dx+1)
+  }
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (tap >= 0)
+    v = *reinterpret_cast<const uint4*>(p.w + (long long)ph * p.w_phase_stride +
+                                        ((long long)n * (GEOM == 0 ? 4 : 16) + tap) * p.cin + c);
+  frag[(long long)f * 64 + lane] = v;
 }
 
 // GEOM 0: ConvT k4 s2 (4 phases, 3x3 neighbourhood, NB column blocks of 16: N' = 4N <= 16*NB)
@@ -100,29 +129,11 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
   // this wave's DMA pieces per chunk (the count vmcnt leaves in flight while chunk c is consumed)
   const int my_pieces = (PIECES - wave + 3) / 4;
 
-  // B fragment of (neighbour nb, column block j, half kk) for this lane: column n' = 16j + (lane & 15),
-  // k = 8*(lane>>4) .. +8 within the 32-channel half.
+  // B fragment of (neighbour nb, column block j, half kk): one coalesced 16-byte load per lane from the
+  // fragment table (narrow_bfrag_kernel)
+  const uint4* frag = reinterpret_cast<const uint4*>(p.frag);
   auto load_b = [&](int chunk, int nb, int j, int kk) -> bf16x8_h {
-    const int np = 16 * j + (lane & 15);
-    const int c = chunk * 64 + kk * 32 + 8 * (lane >> 4);
-    int tap = -1, ph = 0, n = np;
-    if (GEOM == 0) {
-      const int dy = nb / 3 - 1, dx = nb % 3 - 1;
-      ph = np / p.N;
-      n = np - ph * p.N;
-      const int ty = (ph >> 1) - dy, tx = (ph & 1) - dx;
-      if (np < p.NP && ty >= 0 && ty <= 1 && tx >= 0 && tx <= 1) tap = ty * 2 + tx;
-    } else {
-      if (np < p.NP) tap = nb;  // tap index = (dy+1)*4 + (dx+1)
-    }
-    bf16x8_h v;
-    if (tap >= 0) {
-      v = *reinterpret_cast<const bf16x8_h*>(p.w + (long long)ph * p.w_phase_stride +
-                                             ((long long)n * (GEOM == 0 ? 4 : 16) + tap) * p.cin + c);
-    } else {
-      v = bf16x8_h{};
-    }
-    return v;
+    return __builtin_bit_cast(bf16x8_h, frag[((long long)((chunk * 2 + kk) * NBR + nb) * NB + j) * 64 + lane]);
   };
 
   floatx4 acc[ROWS][TXB][NB];
@@ -254,10 +265,10 @@ static size_t halo_lds(int geom, int ty, int txb, int nstage) {
 
 // Narrow plan: {ty, txb, nsplit}.  Taller / wider tiles reuse each register-held B fragment over more
 // MFMAs; the split over channel chunks keeps >= 1024 blocks on the long reductions.
-static void narrow_plan(int geom, int B, int GH, int GW, int cin, const int32_t* force, int* ty, int* txb,
-                        int* nsplit) {
+static void narrow_plan(int geom, int B, int GH, int GW, int cin, int np_cols, const int32_t* force, int* ty,
+                        int* txb, int* nsplit) {
   *ty = 8;
-  *txb = 1;
+  *txb = geom == 0 && np_cols > 16 ? 2 : 1;  // two column blocks per B fragment: -11 % on the N = 8 ConvT
   if (force && force[0] > 0) {
     *ty = force[0];
     *txb = force[1] > 0 ? force[1] : 1;
@@ -269,6 +280,14 @@ static void narrow_plan(int geom, int B, int GH, int GW, int cin, const int32_t*
   *nsplit = ns;
 }
 
+// bytes of the B fragment table: chunks x 2 halves x neighbours x column blocks x 1 KiB (256-aligned)
+static int64_t narrow_frag_bytes(int geom, int Cin, int Cout) {
+  const int nbr = geom == 0 ? 9 : 16;
+  const int np = geom == 0 ? 4 * Cout : Cout;
+  const int nb = np <= 16 ? 1 : 2;
+  return (int64_t)(Cin / 64) * 2 * nbr * nb * 1024;
+}
+
 bool bf16_narrow_eligible(int kind, int Cin, int Cout) {
   if (kind != STC_CONVT_S2 && kind != STC_CONV_S1) return false;
   if (Cin % 64 != 0) return false;
@@ -278,10 +297,9 @@ bool bf16_narrow_eligible(int kind, int Cin, int Cout) {
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout) {
   const int geom = kind == STC_CONVT_S2 ? 0 : 1;
   int ty, txb, ns;
-  narrow_plan(geom, B, GH, GW, Cin, nullptr, &ty, &txb, &ns);
-  if (ns <= 1) return 0;
   const int np = geom == 0 ? 4 * Cout : Cout;
-  return (int64_t)ns * B * GH * GW * np * 4;
+  narrow_plan(geom, B, GH, GW, Cin, np, nullptr, &ty, &txb, &ns);
+  return (ns <= 1 ? 0 : (int64_t)ns * B * GH * GW * np * 4) + narrow_frag_bytes(geom, Cin, Cout);
 }
 
 int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
@@ -306,18 +324,30 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
   p.bias = bias; p.tanh_ = epi_tanh; p.out_f32 = out_f32;
   p.Mtot = (long long)B * p.GH * p.GW;
   int ty, txb, ns;
-  narrow_plan(geom, B, p.GH, p.GW, Cin, force, &ty, &txb, &ns);
+  narrow_plan(geom, B, p.GH, p.GW, Cin, p.NP, force, &ty, &txb, &ns);
   p.tiles_x = cdiv(p.GW, 16 * txb);
   p.tiles_per_img = p.tiles_x * cdiv(p.GH, ty);
   const int nchunks = Cin / 64;
   p.chunks_per_split = cdiv(nchunks, ns);
   p.nsplit = cdiv(nchunks, p.chunks_per_split);
-  if (p.nsplit > 1) {
-    const int64_t need = (int64_t)p.nsplit * B * p.GH * p.GW * p.NP * 4;
-    STC_REQUIRE(ws && ws_bytes >= need, "narrow bf16: workspace %lld < %lld", (long long)ws_bytes, (long long)need);
-    p.ws = (float*)ws;
-  }
+  const int64_t slab_bytes = p.nsplit > 1 ? (int64_t)p.nsplit * B * p.GH * p.GW * p.NP * 4 : 0;
+  const int64_t frag_bytes = narrow_frag_bytes(geom, Cin, Cout);
+  STC_REQUIRE(ws && ws_bytes >= slab_bytes + frag_bytes, "narrow bf16: workspace %lld < %lld", (long long)ws_bytes,
+              (long long)(slab_bytes + frag_bytes));
+  if (p.nsplit > 1) p.ws = (float*)ws;
+  p.frag = (const char*)ws + slab_bytes;
   if ((long long)B * p.GH * p.GW == 0) return 0;
+  {
+    const int nbr = geom == 0 ? 9 : 16, nb = p.NP <= 16 ? 1 : 2;
+    const unsigned nfrag = (unsigned)((Cin / 64) * 2 * nbr * nb);
+    if (geom == 0) {
+      if (nb == 1) hipLaunchKernelGGL((narrow_bfrag_kernel<0, 1>), dim3(nfrag), dim3(64), 0, st, p, (uint4*)p.frag);
+      else hipLaunchKernelGGL((narrow_bfrag_kernel<0, 2>), dim3(nfrag), dim3(64), 0, st, p, (uint4*)p.frag);
+    } else {
+      hipLaunchKernelGGL((narrow_bfrag_kernel<1, 1>), dim3(nfrag), dim3(64), 0, st, p, (uint4*)p.frag);
+    }
+    STC_CHECK_LAUNCH();
+  }
   dim3 grid((unsigned)(B * p.tiles_per_img), (unsigned)p.nsplit);
   const size_t lds = halo_lds(geom, ty, txb, p.chunks_per_split > 1 ? 2 : 1);
   STC_REQUIRE(lds <= 160 * 1024, "narrow bf16: tile %dx%d needs %zu B of LDS", ty, 16 * txb, lds);
