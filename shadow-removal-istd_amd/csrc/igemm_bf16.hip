@@ -750,6 +750,71 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
   }
 }
 
+// The same reduction for few rows over many splits (the deep 1x1 - 4x4 layers): one wave per (row,
+// 8-channel group), lane l summing splits l, l + 64, ... in order, then a fixed xor butterfly.  Every
+// row is its own statistics chunk ({1, 0, 0, value}: Chan-mergeable) and, with the fused BN backward,
+// its own {dn, dn * xhat} chunk -- so no block-level row reduction is needed.
+__global__ void __launch_bounds__(256) splitk_reduce_wide_kernel(const GParams p) {
+  const int CG = p.N / 8;
+  const long long R = (long long)p.nphase * p.M;
+  const long long unit = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit >= R * CG) return;
+  const int lane = threadIdx.x & 63;
+  const long long row = unit / CG;
+  const int cg = (int)(unit - row * CG), n = cg * 8;
+  const int ph = (int)(row / p.M), m = (int)(row - (long long)ph * p.M);
+  const long long MN = (long long)p.M * p.N;
+  const float* src = p.ws + ((long long)ph * p.ksplit * p.M + m) * p.N + n;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = 0.f;
+  for (int s = lane; s < p.ksplit; s += 64) {
+    const float4 a = *reinterpret_cast<const float4*>(src + s * MN);
+    const float4 b = *reinterpret_cast<const float4*>(src + s * MN + 4);
+    v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+    v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += __shfl_xor(v[e], o, 64);
+  if (lane != 0) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    if (p.bias) v[e] += p.bias[n + e];
+    if (p.tanh_) v[e] = tanhf(v[e]);
+  }
+  const int GHW = p.GH * p.GW;
+  const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+  const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+  const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+  const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
+  uint4 o;
+  o.x = pack_bf16x2(v[0], v[1]); o.y = pack_bf16x2(v[2], v[3]);
+  o.z = pack_bf16x2(v[4], v[5]); o.w = pack_bf16x2(v[6], v[7]);
+  *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = o;
+  if (p.stats) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      *reinterpret_cast<float4*>(p.stats + (row * p.N + n + e) * 4) = make_float4(1.f, 0.f, 0.f, v[e]);
+  }
+  if (p.part2) {
+    const int bnch = n - p.bch_off;
+    if (bnch >= 0 && bnch < p.bC) {
+      float ba[8], bb[8], vr[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { ba[e] = 0.f; bb[e] = 0.f; }
+      const unsigned w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { vr[2 * e] = __uint_as_float(w[e] << 16); vr[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u); }
+      if (oy < p.bxH && ox < p.bxW) bnb_accum(p, b, oy, ox, bnch, vr, ba, bb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        *reinterpret_cast<float2*>(p.part2 + (row * p.bC + bnch + e) * 2) = make_float2(ba[e], bb[e]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- host
 struct BPlan {
   int cfg;  // index into the tile table
@@ -834,7 +899,11 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
     if (cfg < 0) {
       cfg = order[no - 1];
       ks = 1;
-      while (allow_split && tiles(cfg) * ks < 400 && ks < 8 && ksteps / (ks * 2) >= 8) ks *= 2;
+      // the 1x1 / 2x2 grids (<= 256 GEMM rows): up to 32 splits of >= 4 K-steps, reduced by
+      // splitk_reduce_wide_kernel (deep-layer sweep, scripts/deep_sweep.py: 12.9 -> 9.2 us at 1x1)
+      const bool tiny = (long long)M * nphase <= 256;
+      const int kmax = tiny ? 32 : 8, smin = tiny ? 4 : 8;
+      while (allow_split && tiles(cfg) * ks < 400 && ks < kmax && ksteps / (ks * 2) >= smin) ks *= 2;
     }
   }
   if (!allow_split) ks = 1;
@@ -868,6 +937,7 @@ struct Bf16Problem {
   int64_t ws_bytes;
   int stats_chunks;
   int reduce_rows;
+  bool wide;  // split-K reduction by splitk_reduce_wide_kernel (a chunk per row)
 };
 
 // Shared planning for query and launch.
@@ -879,8 +949,9 @@ static Bf16Problem bf16_problem(int M, int N, int K, int nphase, const int32_t* 
   if (pr.pl.ksplit > 1) {
     pr.ws_bytes = (int64_t)nphase * pr.pl.ksplit * (int64_t)M * N * 4;
     const long long rows = (long long)nphase * M;
+    pr.wide = pr.pl.ksplit >= 16 && rows * (N / 8) <= 16384;  // a wave per unit pays off with >= 16 splits
     pr.reduce_rows = reduce_rows_per_block(rows, N);
-    pr.stats_chunks = (int)((rows + pr.reduce_rows - 1) / pr.reduce_rows);
+    pr.stats_chunks = pr.wide ? (int)rows : (int)((rows + pr.reduce_rows - 1) / pr.reduce_rows);
   } else {
     pr.ws_bytes = 0;
     pr.stats_chunks = nphase * pr.pl.mtiles;
@@ -967,8 +1038,13 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     p.stats = stats;
     p.part2 = part2;
     const long long rows = (long long)p.nphase * p.M;
-    const int blocks = (int)((rows + pr.reduce_rows - 1) / pr.reduce_rows);
-    hipLaunchKernelGGL(splitk_reduce_stats_kernel, dim3(blocks), dim3(256), 0, st, p, pr.reduce_rows);
+    if (pr.wide) {
+      const long long units = rows * (p.N / 8);
+      hipLaunchKernelGGL(splitk_reduce_wide_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, st, p);
+    } else {
+      const int blocks = (int)((rows + pr.reduce_rows - 1) / pr.reduce_rows);
+      hipLaunchKernelGGL(splitk_reduce_stats_kernel, dim3(blocks), dim3(256), 0, st, p, pr.reduce_rows);
+    }
     STC_CHECK_LAUNCH();
   }
   return 0;
