@@ -885,8 +885,8 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
       order[0] = 23; order[1] = 2; order[2] = 5; no = 3;
     } else if (K <= 512) {  // (Cin = 128 ConvT-geometry dgrads: the 3-stage BK = 32 128x64 tile, -9 %)
       order[0] = 23; order[1] = 2; order[2] = 5; no = 3;
-    } else {
-      order[0] = 5; order[1] = 2; no = 2;
+    } else {  // (N = 64 ConvT d1: the 3-stage 128x64 tile, -4 % vs 64x64 in scripts/sweep_cfg.sh)
+      order[0] = 11; order[1] = 5; order[2] = 2; no = 3;
     }
     for (int k = 1; k <= 8 && cfg < 0; k *= 2) {
       if (k > 1 && (ksteps / k < 8 || !allow_split)) break;

@@ -62,7 +62,10 @@ def _worker(rank, world, port, out):
     sync()
     assert sync.works == [None, None] and sync.count == [0, 0]
     if rank == 0:
-        out.put([p.grad.clone() for p in plist])
+        import io
+        buf = io.BytesIO()
+        torch.save([p.grad.clone() for p in plist], buf)  # bytes: the worker may exit before the parent reads
+        out.put(buf.getvalue())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -91,6 +94,8 @@ def test_grad_allreduce_matches_global_batch():
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
+    import io
+    got = torch.load(io.BytesIO(got), weights_only=True)
     # single-process reference: per-shard BN (two forwards), loss = mean over the global batch
     st = fixture_state(ref.discriminator_state_template(4, 8), 13, "one")
     params = {k: v.clone().requires_grad_(not ref._is_buffer(k)) for k, v in st.items()}
