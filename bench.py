@@ -176,9 +176,10 @@ def roofline_of_step(tr, x, m, y, args, B, s):
     import torch
     from stcgan_amd import ops
     ops._timer = []
+    lanes, tr.streams = tr.streams, False  # one stream: each launch's events bracket it alone
     tr.train_step(x, m, y)
     torch.cuda.synchronize()
-    launches, ops._timer = ops._timer, None
+    launches, ops._timer, tr.streams = ops._timer, None, lanes
     per, shapes = {}, {}
     for name, _single, fl, e0, e1, desc in launches:
         ms = e0.elapsed_time(e1)

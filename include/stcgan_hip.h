@@ -351,6 +351,12 @@ int stc_adam_elems_per_block(void);
  * would (padding entries are left as they are).  Same Adam arithmetic as stc_adam_step.           */
 int stc_adam_pack_step(const int64_t* table, int ntensors, int64_t total_blocks,
                        float lr, float beta1, float beta2, float eps, int step, void* stream);
+/* dst[e] += src[e] (fp32, numel[e] elements) for ntensors <= 16 tensors in one launch (host arrays of
+ * device pointers).  Sums the weight gradients of two calls of one network inside one differentiated
+ * graph -- the discriminators' real and fake calls, STCGAN/stcgan.py:215-227 -- which autograd would
+ * otherwise add with one ATen kernel per parameter.                                               */
+int stc_grad_accumulate(int ntensors, float* const* dst, const float* const* src, const int64_t* numel,
+                        void* stream);
 
 /* ---- misc ------------------------------------------------------------------------
  * stc_time_next_main_kernel: instrumentation (bench.py).  The next call ON THIS THREAD that launches a

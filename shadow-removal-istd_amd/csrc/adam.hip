@@ -193,6 +193,49 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, 
   }
 }
 
+// ---- multi-tensor gradient accumulation: dst[e] += src[e] for up to GA_MAX tensors in one launch.
+// Replaces the per-parameter ATen adds autograd issues when a network is called twice in one
+// differentiated graph (the discriminators' real + fake calls, STCGAN/stcgan.py:215-227).
+constexpr int GA_MAX = 16;
+constexpr int GA_ELEMS = 4096;  // per block: 256 threads x 4 float4
+struct GradAccArgs {
+  float* dst[GA_MAX];
+  const float* src[GA_MAX];
+  long long n[GA_MAX];
+  int first_block[GA_MAX + 1];
+  int vec[GA_MAX];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void grad_acc_kernel(GradAccArgs a) {
+  const int b = blockIdx.x;
+  int e = 0;
+  while (e + 1 < a.count && b >= a.first_block[e + 1]) ++e;
+  const long long n = a.n[e];
+  float* __restrict__ d = a.dst[e];
+  const float* __restrict__ s = a.src[e];
+  const long long base = (long long)(b - a.first_block[e]) * GA_ELEMS;
+  if (a.vec[e]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long long i = base + (long long)(k * 256 + threadIdx.x) * 4;
+      if (i + 3 < n) {
+        float4 x = *reinterpret_cast<const float4*>(d + i);
+        const float4 y = *reinterpret_cast<const float4*>(s + i);
+        x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
+        *reinterpret_cast<float4*>(d + i) = x;
+      } else {
+        for (long long j = i; j < n && j < i + 4; ++j) d[j] += s[j];
+      }
+    }
+  } else {
+    for (int k = threadIdx.x; k < GA_ELEMS; k += 256) {
+      const long long i = base + k;
+      if (i < n) d[i] += s[i];
+    }
+  }
+}
+
 }  // namespace stc
 
 using namespace stc;
@@ -223,3 +266,28 @@ extern "C" int stc_adam_step(const int64_t* table, int ntensors, int64_t total_b
 }
 
 extern "C" int stc_adam_elems_per_block(void) { return ADAM_BLOCK * ADAM_ELEMS; }
+
+extern "C" int stc_grad_accumulate(int ntensors, float* const* dst, const float* const* src, const int64_t* numel,
+                                   void* stream) {
+  STC_REQUIRE(ntensors >= 0 && ntensors <= GA_MAX, "stc_grad_accumulate: 0..16 tensors per call");
+  if (ntensors == 0) return 0;
+  GradAccArgs a{};
+  int blocks = 0;
+  for (int e = 0; e < ntensors; ++e) {
+    STC_REQUIRE(dst[e] != nullptr && src[e] != nullptr && numel[e] >= 0, "stc_grad_accumulate: bad tensor");
+    a.dst[e] = dst[e];
+    a.src[e] = src[e];
+    a.n[e] = numel[e];
+    a.vec[e] = ((((uintptr_t)dst[e]) | ((uintptr_t)src[e])) & 15) == 0;
+    a.first_block[e] = blocks;
+    const long long nb = (numel[e] + GA_ELEMS - 1) / GA_ELEMS;
+    STC_REQUIRE(blocks + nb < (1ll << 30), "stc_grad_accumulate: too large");
+    blocks += (int)nb;
+  }
+  a.first_block[ntensors] = blocks;
+  a.count = ntensors;
+  if (blocks == 0) return 0;
+  hipLaunchKernelGGL(grad_acc_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  STC_CHECK_LAUNCH();
+  return 0;
+}

@@ -396,12 +396,44 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
 # ----------------------------------------------------------------------------- autograd
 
 
+class WeightGradGroup:
+    """Calls of one network inside one differentiated graph (the discriminator's real and fake calls,
+    STCGAN/stcgan.py:215-227) whose weight gradients the engine sums itself -- one
+    stc_grad_accumulate launch -- instead of autograd's one ATen add per parameter: every member's
+    backward but the last returns no weight gradient, the last returns the sum.  Every member's
+    backward must run (one loss over all of them, as train_step builds); use a fresh group per graph."""
+
+    def __init__(self):
+        self.members = 0
+        self.done = 0
+        self.stash = None
+
+    def join(self):
+        if self.done:
+            raise RuntimeError("WeightGradGroup: a call joined after its backward started; use a fresh group")
+        self.members += 1
+
+    def add(self, grads):
+        """Fold one member's {id(param): grad}; returns the sum after the last member, else None."""
+        self.done += 1
+        if self.stash is None:
+            self.stash = grads
+        else:
+            ops.grad_accumulate([(self.stash[k], g) for k, g in grads.items() if k in self.stash])
+            for k, g in grads.items():
+                self.stash.setdefault(k, g)
+        if self.done < self.members:
+            return None
+        out, self.stash = self.stash, None
+        return out
+
+
 class NetFn(torch.autograd.Function):
     """One autograd node per network call.  inputs: (ctrl, *sources, *params)."""
 
     @staticmethod
     def forward(ctx, ctrl, *tensors):
-        plan, kind, train, dt, cache, nsrc = ctrl
+        plan, kind, train, dt, cache, nsrc, group = ctrl
         sources = [t.contiguous().float() for t in tensors[:nsrc]]
         save = train and any(ctx.needs_input_grad[1:])
         ops.refresh_packs(cache)  # all operands packed since the last optimiser step, one launch
@@ -409,11 +441,14 @@ class NetFn(torch.autograd.Function):
         out, saved = fwd(plan, sources, train, dt, cache, save)
         ctx.ctrl = ctrl
         ctx.saved_net = saved
+        ctx.group = group if (save and any(ctx.needs_input_grad[1 + nsrc:])) else None
+        if ctx.group is not None:
+            ctx.group.join()
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        plan, kind, train, dt, cache, nsrc = ctx.ctrl
+        plan, kind, train, dt, cache, nsrc, _ = ctx.ctrl
         saved = ctx.saved_net
         if saved is None:
             raise RuntimeError("stcgan_amd: backward through a network called in eval mode is not supported")
@@ -423,6 +458,8 @@ class NetFn(torch.autograd.Function):
         bwd = gen_backward if kind == "G" else disc_backward
         src_grads, grads = bwd(plan, saved, gout, dt, cache, need_src, need_w)
         ctx.saved_net = None
+        if ctx.group is not None:
+            grads = ctx.group.add(grads) or {}
         out = [None]
         for i in range(nsrc):
             out.append(src_grads[i] if (src_grads is not None and need[i]) else None)

@@ -53,6 +53,9 @@ class _HipNet(nn.Module):
         self.compute_dtype = torch.float32
         self._pack_cache = {}
         self._plan = None
+        # engine.WeightGradGroup that this network's calls join (set by the trainer around the calls
+        # of one graph whose weight gradients the engine sums), or None
+        self.weight_grad_group = None
 
     def set_compute_dtype(self, dtype):
         """'fp32' (default, parity path) or 'bf16' (bf16 operands, fp32 accumulation/BN/master weights)."""
@@ -69,7 +72,8 @@ class _HipNet(nn.Module):
         if self._plan is None:
             self._plan = self._make_plan()
         params = self._plan.params
-        ctrl = (self._plan, self.kind, self.training, self.compute_dtype, self._pack_cache, len(sources))
+        ctrl = (self._plan, self.kind, self.training, self.compute_dtype, self._pack_cache, len(sources),
+                self.weight_grad_group)
         return engine.NetFn.apply(ctrl, *sources, *params)
 
     def _apply(self, fn, *args, **kwargs):

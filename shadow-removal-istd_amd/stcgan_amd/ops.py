@@ -487,3 +487,17 @@ def infer_output(net_out, oh=192, ow=256):
     out = torch.empty((B, oh, ow, C), dtype=torch.uint8, device=x.device)
     check(lib().stc_infer_output(ptr(x), B, C, H, W, oh, ow, ptr(out), stream()), "stc_infer_output")
     return out
+
+
+def grad_accumulate(pairs):
+    """dst += src (fp32, contiguous, same numel) for every (dst, src) in pairs: one launch per 16."""
+    for k in range(0, len(pairs), 16):
+        chunk = pairs[k:k + 16]
+        for d, s in chunk:
+            assert d.dtype == torch.float32 and s.dtype == torch.float32 and d.is_contiguous() \
+                and s.is_contiguous() and d.numel() == s.numel(), "grad_accumulate: fp32 contiguous pairs"
+        n = len(chunk)
+        dst = (ctypes.c_void_p * n)(*[d.data_ptr() for d, _ in chunk])
+        src = (ctypes.c_void_p * n)(*[s.data_ptr() for _, s in chunk])
+        num = (ctypes.c_int64 * n)(*[d.numel() for d, _ in chunk])
+        check(lib().stc_grad_accumulate(n, dst, src, num, stream()), "stc_grad_accumulate")

@@ -27,6 +27,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import engine
 from . import networks
 from . import parallel
 from .loss import AdversarialLoss, DataLoss
@@ -93,6 +94,9 @@ class STCGAN(object):
         self.sync_D = parallel.GradAllReduce([list(self.D2.parameters()), list(self.D1.parameters())])
         self.sync_G.enable_overlap()
         self.sync_D.enable_overlap()
+        # discriminators on side HIP streams (train_step / _lanes); off for a strictly serial step
+        self.streams = bool(getattr(args, "streams", True))
+        self._side = None
 
         data_dir = getattr(args, "data_dir", None)
         if data_dir is not None and train_loader is None and valid_loader is None:
@@ -185,21 +189,62 @@ class STCGAN(object):
                    + adv(C1_real - mean0(C1_fake), is_real=False)) * 0.5
         return G1_loss, G2_loss
 
+    def _lanes(self):
+        """(main, D1 lane, D2 lane): the discriminators run on their own HIP streams so their
+        kernels overlap the generators' (and each other's) -- many of the step's launches are
+        latency-bound small grids that leave most of the 256 CUs idle.  Autograd runs each
+        network's backward on the stream its forward ran on and inserts the cross-stream
+        waits for the gradients that flow between them."""
+        main = torch.cuda.current_stream(self.device)
+        if not self.streams:
+            return main, None, None
+        if getattr(self, "_side", None) is None:
+            self._side = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
+        return (main,) + self._side
+
+    def _on(self, lane, net, srcs, after=None):
+        """net(srcs) on ``lane`` (None = the current stream), after the main-stream event ``after``."""
+        if lane is None:
+            return net(srcs)
+        with torch.cuda.stream(lane):
+            if after is not None:
+                lane.wait_event(after)
+            for s in srcs:
+                s.record_stream(lane)
+            out = net(srcs)
+        out.record_stream(torch.cuda.current_stream(self.device))
+        return out
+
     def train_step(self, x, m, y, training=True, acc=None):
         """One iteration of STCGAN.run_epoch (STCGAN/stcgan.py:208-312): D step then G step.
-        Returns the on-device loss scalars (no host sync)."""
+        Returns the on-device loss scalars (no host sync).  The call order of every network
+        (and so every BN running-statistics update) is the reference's; with ``streams`` the
+        discriminator calls run on side streams (see _lanes) -- same kernels, same results."""
         self.optim_D.zero_grad()
         self.optim_G.zero_grad()
+        main, l1, l2 = self._lanes()
+        if l1 is not None:  # side lanes start after everything queued so far (last optimizer step)
+            l1.wait_stream(main)
+            l2.wait_stream(main)
         with torch.set_grad_enabled(training):
             self.optim_D.zero_grad()
             self.D1.requires_grad_(True)
             self.D2.requires_grad_(True)
-            C1_real = self.D1([x, m])
+            # each discriminator's real + fake weight gradients summed by the engine (one launch)
+            self.D1.weight_grad_group = engine.WeightGradGroup()
+            self.D2.weight_grad_group = engine.WeightGradGroup()
+            C1_real = self._on(l1, self.D1, [x, m])
+            C2_real = self._on(l2, self.D2, [x, m, y])
             m_pred = self.G1(x)
-            C1_fake = self.D1([x, m_pred.detach()])
-            C2_real = self.D2([x, m, y])
+            ev_m = main.record_event() if l1 is not None else None
+            C1_fake = self._on(l1, self.D1, [x, m_pred.detach()], after=ev_m)
             y_pred = self.G2([x, m_pred])
-            C2_fake = self.D2([x, m_pred.detach(), y_pred.detach()])
+            ev_y = main.record_event() if l1 is not None else None
+            C2_fake = self._on(l2, self.D2, [x, m_pred.detach(), y_pred.detach()], after=ev_y)
+            self.D1.weight_grad_group = self.D2.weight_grad_group = None
+            if l1 is not None:
+                main.wait_stream(l1)
+                main.wait_stream(l2)
             D1_loss, D2_loss = self._d_losses(C1_real, C1_fake, C2_real, C2_fake)
             D_loss = self.lambda2 * D1_loss + self.lambda3 * D2_loss
             if training:
@@ -212,10 +257,16 @@ class STCGAN(object):
             self.D1.requires_grad_(False)
             self.D2.requires_grad_(False)
             if training:  # D is not updated when validating
-                C1_real = self.D1([x, m])
-                C1_fake = self.D1([x, m_pred])
-                C2_real = self.D2([x, m, y])
-                C2_fake = self.D2([x, m_pred, y_pred])
+                if l1 is not None:  # after optim_D.step
+                    l1.wait_stream(main)
+                    l2.wait_stream(main)
+                C1_real = self._on(l1, self.D1, [x, m])
+                C1_fake = self._on(l1, self.D1, [x, m_pred])
+                C2_real = self._on(l2, self.D2, [x, m, y])
+                C2_fake = self._on(l2, self.D2, [x, m_pred, y_pred])
+                if l1 is not None:
+                    main.wait_stream(l1)
+                    main.wait_stream(l2)
             G1_loss, G2_loss = self._g_losses(C1_real, C1_fake, C2_real, C2_fake)
             data1_loss = self.data_loss(m_pred, m)
             data2_loss = self.data_loss(y_pred, y)
@@ -224,6 +275,9 @@ class STCGAN(object):
                 G_loss.backward()
                 self.sync_G()
                 self.optim_G.step()
+        if l1 is not None:  # nothing on the side lanes outlives the step
+            main.wait_stream(l1)
+            main.wait_stream(l2)
         vals = dict(D1=D1_loss.detach(), D2=D2_loss.detach(), D=D_loss.detach(), G1=G1_loss.detach(),
                     G2=G2_loss.detach(), data1=data1_loss.detach(), data2=data2_loss.detach(), G=G_loss.detach())
         if acc is not None:

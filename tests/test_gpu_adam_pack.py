@@ -51,3 +51,24 @@ def test_adam_pack_matches_adam_then_pack(P, Q, modes, dt):
                                want.view(torch.int16 if dt == torch.bfloat16 else torch.int32)), (step, m)
             if modes.index(m) < 2:
                 assert fresh.data_ptr() == out.data_ptr()  # written in place by stc_adam_pack_step
+
+
+def test_grad_accumulate_matches_add():
+    """stc_grad_accumulate (the engine's sum of a network's real + fake weight gradients) == dst + src,
+    bit-exact, for ragged sizes, misaligned (scalar-path) views and more than 16 tensors."""
+    from stcgan_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(5)
+    sizes = [1, 3, 4, 17, 4095, 4096, 4097, 65536 + 5, 1 << 20] + [257] * 12
+    pairs, want = [], []
+    for i, n in enumerate(sizes):
+        d = torch.randn(n + 1, generator=g, device="cuda")
+        s = torch.randn(n + 1, generator=g, device="cuda")
+        if i % 3 == 1:  # 4-byte offset: the scalar path
+            d, s = d[1:], s[1:]
+        else:
+            d, s = d[:n], s[:n]
+        want.append(d + s)
+        pairs.append((d, s))
+    ops.grad_accumulate(pairs)
+    for (d, _), w in zip(pairs, want):
+        assert torch.equal(d, w)

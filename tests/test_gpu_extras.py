@@ -79,3 +79,30 @@ def test_checkpoint_resume_is_bit_identical(tmp_path):
         s1, s2 = getattr(t1, n).state_dict(), getattr(t2, n).state_dict()
         for k in s1:
             assert torch.equal(s1[k], s2[k]), (n, k)
+
+
+@pytest.mark.parametrize("dtype,loss_type", [("bf16", "normal"), ("fp32", "rel_avg")])
+def test_side_stream_step_is_bit_identical(dtype, loss_type):
+    """Discriminators on side HIP streams (STCGAN.streams) vs the one-stream step: same kernels in
+    the same per-network order, so three steps leave bit-identical states and losses."""
+    from stcgan_amd.stcgan import STCGAN
+    g = torch.Generator().manual_seed(3)
+    batches = [tuple(torch.rand((4, c, 256, 256), generator=g).cuda() * 2 - 1 for c in (3, 1, 3)) for _ in range(3)]
+    out = []
+    for lanes in (False, True):
+        torch.manual_seed(11)
+        a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5, beta2=0.999,
+                                  D_loss_fn="standard", D_loss_type=loss_type, ngf=64, dtype=dtype, streams=lanes,
+                                  load_weights_g1=None, load_weights_g2=None, load_weights_d1=None,
+                                  load_weights_d2=None)
+        tr = STCGAN(a)
+        losses = [tr.train_step(*b) for b in batches]
+        torch.cuda.synchronize()
+        out.append((losses, {n: getattr(tr, n).state_dict() for n in ("G1", "G2", "D1", "D2")}))
+    (l0, s0), (l1, s1) = out
+    for a_, b_ in zip(l0, l1):
+        for k in a_:
+            assert float(a_[k]) == float(b_[k]), k
+    for n in s0:
+        for k in s0[n]:
+            assert torch.equal(s0[n][k], s1[n][k]), (n, k)
