@@ -386,7 +386,7 @@ namespace stc {
 // taps: dW[r][ci][kh][kw] += G[q][ci] * D[qy-kh+1][qx-kw+1][r].
 // Block = (image, 64-channel chunk, pixel split ps of 4), 256 threads = 16 channel quads x 16 pixel
 // lanes: lane l takes the image's pixels 16 ps + l + 64 k; the image's D plane (RO channels, zero-padded by 2) sits in LDS and is
-// read as broadcasts.  The 16 lanes' partials are summed in a fixed order (xor butterfly, then LDS) into the
+// read as broadcasts.  The 16 lanes' partials are summed in a fixed order (through LDS) into the
 // slab [image][RO][16 * Cg] (column tap * Cg + ci), which the ordered wide reduce sums over images.
 template <typename T, int RO>
 __global__ void __launch_bounds__(256) wgrad_rows_kernel(const char* __restrict__ dp, long long d_bs, long long d_rs,
@@ -452,35 +452,30 @@ __global__ void __launch_bounds__(256) wgrad_rows_kernel(const char* __restrict_
     const int qy = fast_div(q, IW, inv_iw), qx = q - qy * IW;
     body(q, Vec4<T>::load(G + (long long)qy * g_rs + (long long)qx * g_ps));
   }
-  // fixed-order sum over the 16 pixel lanes: the 4 planes of a wave by an xor butterfly, then the 4
-  // waves through LDS (red[wave][r][t][64 channels], reusing the D plane area)
+  // fixed-order sum over the 16 pixel planes (4 per wave), all through LDS: every plane stores its
+  // partials (part[plane][r][t][64 channels], after the D plane), then each output is
+  // ((p0 + p1) + (p2 + p3)) per wave and (w0 + w1) + (w2 + w3) across waves -- the order the former
+  // xor-butterfly (ds_bpermute) version used.  That version gave sporadically different sums for one
+  // (tap, channel-in-quad) register of a whole wave when other streams' kernels shared the GPU
+  // (tests/test_gpu_dist.py), so the cross-lane step is plain LDS traffic now.
+  float* part = sm + ((RO * rows * cols + 3) & ~3);
+  constexpr int PL = RO * 16 * 64;  // floats per plane
 #pragma unroll
   for (int r = 0; r < RO; ++r)
 #pragma unroll
     for (int t = 0; t < 16; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = acc[r][t][e];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        acc[r][t][e] = v;
-      }
-  __syncthreads();
-  float* red = sm;
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) < 16) {
-#pragma unroll
-    for (int r = 0; r < RO; ++r)
-#pragma unroll
-      for (int t = 0; t < 16; ++t)
-        *reinterpret_cast<float4*>(red + (((wave * RO + r) * 16 + t) * 64 + quad * 4)) =
-            make_float4(acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]);
-  }
+      *reinterpret_cast<float4*>(part + plane * PL + (r * 16 + t) * 64 + quad * 4) =
+          make_float4(acc[r][t][0], acc[r][t][1], acc[r][t][2], acc[r][t][3]);
   __syncthreads();
   float* slab = ws + ((long long)b * PS + ps) * RO * 16 * Cg;
-  for (int o = threadIdx.x; o < RO * 16 * 64; o += 256) {  // o = (r * 16 + t) * 64 + c
-    const float v = (red[o] + red[RO * 16 * 64 + o]) + (red[2 * RO * 16 * 64 + o] + red[3 * RO * 16 * 64 + o]);
-    slab[(long long)(o >> 6) * Cg + cc * 64 + (o & 63)] = v;
+  for (int o = threadIdx.x; o < PL; o += 256) {  // o = (r * 16 + t) * 64 + c
+    float w4[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float* pw = part + 4 * w * PL + o;
+      w4[w] = (pw[0] + pw[PL]) + (pw[2 * PL] + pw[3 * PL]);
+    }
+    slab[(long long)(o >> 6) * Cg + cc * 64 + (o & 63)] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
   }
 }
 
@@ -506,7 +501,7 @@ extern "C" int stc_conv_wgrad_rows(int dtype, int B, stc_view D, int R, int R_ou
   const int64_t need = stc_conv_wgrad_rows_workspace(B, G.H, R_out, Cg);
   STC_REQUIRE(workspace && workspace_bytes >= need, "stc_conv_wgrad_rows: workspace %lld < %lld",
               (long long)workspace_bytes, (long long)need);
-  const size_t lds = std::max((size_t)R_out * (D.H + 4) * (D.W + 4), (size_t)4 * R_out * 16 * 64) * 4;
+  const size_t lds = ((((size_t)R_out * (D.H + 4) * (D.W + 4) + 3) & ~(size_t)3) + (size_t)16 * R_out * 16 * 64) * 4;
   STC_REQUIRE(lds <= 160 * 1024, "stc_conv_wgrad_rows: D plane too large for LDS (%dx%d)", D.H, D.W);
   float* ws = (float*)workspace;
   main_timer_begin(st);

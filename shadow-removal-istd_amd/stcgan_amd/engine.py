@@ -278,15 +278,25 @@ def _conv_out(h, s):
     return (h + 2 - 4) // s + 1
 
 
-def disc_forward(plan, sources, train, dt, cache, save):
-    """raw[i] = conv_{i-1} raw output (raw[0] = padded input); act[i] = input of conv_i."""
+def disc_forward(plan, sources, train, dt, cache, save, inputs=None):
+    """raw[i] = conv_{i-1} raw output (raw[0] = padded input); act[i] = input of conv_i.
+    inputs: optional dict reusing the gathered NHWC input across calls on the same source tensors
+    (the trainer's real/fake pairs are fed to each discriminator twice per step, STCGAN/stcgan.py:215-280;
+    valid while those tensors are alive and unmodified -- one train step)."""
     dev = sources[0].device
     B, _, H, W = sources[0].shape
     cin = sum(s.shape[1] for s in sources)
     assert cin == plan.in_c, f"discriminator expects {plan.in_c} input channels, got {cin}"
     cin_pad = ops.pad_channels(cin, dt)
-    xin = _nhwc(B, H, W, cin_pad, dt, dev)
-    ops.gather(sources, xin, dt)
+    key = None
+    if inputs is not None:
+        key = tuple((s.data_ptr(), s._version, tuple(s.shape)) for s in sources) + (dt, cin_pad)
+    xin = inputs.get(key) if key is not None else None
+    if xin is None:
+        xin = _nhwc(B, H, W, cin_pad, dt, dev)
+        ops.gather(sources, xin, dt)
+        if key is not None:
+            inputs[key] = xin
     n = plan.n
     raw, act, dims, chans, tabs, stats = [xin], [xin], [(H, W)], [cin_pad], [None], [None]
     out = None
@@ -433,12 +443,12 @@ class NetFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, ctrl, *tensors):
-        plan, kind, train, dt, cache, nsrc, group = ctrl
+        plan, kind, train, dt, cache, nsrc, group, inputs = ctrl
         sources = [t.contiguous().float() for t in tensors[:nsrc]]
         save = train and any(ctx.needs_input_grad[1:])
         ops.refresh_packs(cache)  # all operands packed since the last optimiser step, one launch
-        fwd = gen_forward if kind == "G" else disc_forward
-        out, saved = fwd(plan, sources, train, dt, cache, save)
+        out, saved = (gen_forward(plan, sources, train, dt, cache, save) if kind == "G" else
+                      disc_forward(plan, sources, train, dt, cache, save, inputs))
         ctx.ctrl = ctrl
         ctx.saved_net = saved
         ctx.group = group if (save and any(ctx.needs_input_grad[1 + nsrc:])) else None
@@ -448,13 +458,19 @@ class NetFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        plan, kind, train, dt, cache, nsrc, _ = ctx.ctrl
+        plan, kind, train, dt, cache, nsrc, _, _ = ctx.ctrl
         saved = ctx.saved_net
         if saved is None:
             raise RuntimeError("stcgan_amd: backward through a network called in eval mode is not supported")
         need = ctx.needs_input_grad[1:]
         need_src = list(need[:nsrc]) if any(need[:nsrc]) else None  # per source, or None
         need_w = any(need[nsrc:])
+        if gout.is_cuda:
+            # a side-stream network's incoming gradient is allocated on the main stream (the loss
+            # backward): autograd orders this stream after it, but does not keep the caching allocator
+            # from handing the block back to the main stream once this Python call returns, while the
+            # kernels enqueued here may still read it
+            gout.record_stream(torch.cuda.current_stream(gout.device))
         bwd = gen_backward if kind == "G" else disc_backward
         src_grads, grads = bwd(plan, saved, gout, dt, cache, need_src, need_w)
         ctx.saved_net = None

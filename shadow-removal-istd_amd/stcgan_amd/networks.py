@@ -56,6 +56,9 @@ class _HipNet(nn.Module):
         # engine.WeightGradGroup that this network's calls join (set by the trainer around the calls
         # of one graph whose weight gradients the engine sums), or None
         self.weight_grad_group = None
+        # dict reusing gathered inputs across this network's calls on the same tensors (set by the trainer
+        # for one train step), or None
+        self.input_cache = None
 
     def set_compute_dtype(self, dtype):
         """'fp32' (default, parity path) or 'bf16' (bf16 operands, fp32 accumulation/BN/master weights)."""
@@ -73,7 +76,7 @@ class _HipNet(nn.Module):
             self._plan = self._make_plan()
         params = self._plan.params
         ctrl = (self._plan, self.kind, self.training, self.compute_dtype, self._pack_cache, len(sources),
-                self.weight_grad_group)
+                self.weight_grad_group, self.input_cache)
         return engine.NetFn.apply(ctrl, *sources, *params)
 
     def _apply(self, fn, *args, **kwargs):

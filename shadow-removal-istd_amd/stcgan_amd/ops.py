@@ -4,6 +4,7 @@ Every function here enqueues HIP kernels of libstcgan_hip.so on torch's current
 stream; torch is used only for device memory (caching allocator) and streams.
 """
 import ctypes
+import os
 
 import torch
 
@@ -239,14 +240,23 @@ def _wgrad_kernel_name(plan, Hd, Wd):
     return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}>"
 
 
+# The narrow-R VALU weight gradient (stc_conv_wgrad_rows) for the PatchGAN logits layer is opt-in
+# (STC_WGRAD_ROWS=1, or rows_kernel=True per call): with two processes sharing one GPU
+# (tests/test_gpu_dist.py) it returned, in about one run of three, sums that differ by ~1e-6 relative
+# in one (tap, channel-in-quad) accumulator of a whole wave on bit-identical inputs -- also with its
+# lane butterfly replaced by LDS sums, its LDS regions separated and a persistent workspace -- while
+# the padded-GEMM path was clean in every run.  Off by default until that is understood (~0.1 ms/step).
+_ROWS_DEFAULT = os.environ.get("STC_WGRAD_ROWS", "0") == "1"
+
+
 def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None,
-          force=None, rows=None):
+          force=None, rows=None, rows_kernel=None):
     """Weight gradient [R][Cg_out][4][4] fp32 (stc_conv_wgrad_ex; force = optional {tile config, splits}).
     rows: the number of nonzero (real) channels of D when the rest is padding -- a stride-1 layer with
     1-2 of them goes to stc_conv_wgrad_rows."""
     l = lib()
-    if (rows is not None and rows <= 2 and stride == 1 and dpro is None and gpro is None and dslope is None
-            and gslope is None and force is None and Cg % 64 == 0 and (Dv.H + 4) * (Dv.W + 4) * rows <= 40000):
+    if (rows is not None and rows <= 2 and stride == 1 and (_ROWS_DEFAULT if rows_kernel is None else rows_kernel) and dpro is None and gpro is None and dslope is None
+            and gslope is None and force is None and Cg % 64 == 0 and ((Dv.H + 4) * (Dv.W + 4) + 16384) * rows <= 40000):
         nbytes = l.stc_conv_wgrad_rows_workspace(B, Gv.H, rows, Cg)
         ws, nb = _ws(nbytes, device)
         dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)

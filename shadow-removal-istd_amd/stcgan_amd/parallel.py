@@ -134,6 +134,11 @@ class GradAllReduce:
         self.ready = [False] * len(self.groups)
         self.hooks = []
         self.overlap = False
+        # streams the gradients of each group were accumulated on (autograd runs a leaf's
+        # AccumulateGrad, and so the hook, on the stream of the backward that produced it; the
+        # discriminators' backwards run on side streams): the exchange waits for all of them
+        self.arrival_streams = [dict() for _ in self.groups]
+        self.cuda = bool(self.groups) and bool(self.groups[0]) and self.groups[0][0].is_cuda
 
     # ---- hooks --------------------------------------------------------------------
     def enable_overlap(self):
@@ -148,6 +153,9 @@ class GradAllReduce:
 
     def _arrived(self, gi):
         self.count[gi] += 1
+        if self.cuda:
+            st = torch.cuda.current_stream()
+            self.arrival_streams[gi].setdefault(st.cuda_stream, st)
         need = self.expected[gi] * sum(1 for p in self.groups[gi] if p.requires_grad)
         if self.count[gi] == need:
             self.ready[gi] = True
@@ -168,6 +176,15 @@ class GradAllReduce:
 
     def _launch(self, gi):
         self._ensure_flat()
+        # the launching hook may run on another group's stream (a group completing early waits
+        # for the groups before it): order the gather after every stream this group's gradients
+        # were written on
+        if self.arrival_streams[gi]:
+            cur = torch.cuda.current_stream()
+            for key, st in self.arrival_streams[gi].items():
+                if key != cur.cuda_stream:
+                    cur.wait_stream(st)
+            self.arrival_streams[gi].clear()
         works = []
         for b, flat in zip(self.buckets[gi], self.flat[gi]):
             grads = [p.grad.reshape(-1) if p.grad is not None else None for p in b]

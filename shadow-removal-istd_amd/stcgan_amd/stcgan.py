@@ -226,6 +226,14 @@ class STCGAN(object):
         if l1 is not None:  # side lanes start after everything queued so far (last optimizer step)
             l1.wait_stream(main)
             l2.wait_stream(main)
+        # each discriminator sees the same real and fake inputs in the D and the G step: gather them once
+        self.D1.input_cache, self.D2.input_cache = {}, {}
+        try:
+            return self._step(x, m, y, training, acc, main, l1, l2)
+        finally:
+            self.D1.input_cache = self.D2.input_cache = None
+
+    def _step(self, x, m, y, training, acc, main, l1, l2):
         with torch.set_grad_enabled(training):
             self.optim_D.zero_grad()
             self.D1.requires_grad_(True)

@@ -325,7 +325,7 @@ def test_wgrad_rows_narrow_s1(B, Cin, H, W, rows, dt):
     dy = q(dy) if dt == BF else dy
     (gw,) = torch.autograd.grad(y, w, dy)
     dW = ops.wgrad(B, 1, L.nhwc_view(nhwc(dy).to(DEV, dt)), 8, L.nhwc_view(nhwc(x).to(DEV, dt)), Cin, Cin, dt,
-                   device=DEV, rows=rows)
+                   device=DEV, rows=rows, rows_kernel=True)
     torch.cuda.synchronize()
     got = dW.cpu()
     err = float((got - gw).abs().max())
