@@ -254,6 +254,27 @@ int stc_scatter_nchw(int dtype, int B, int H, int W, stc_view src, int nsrc, flo
  * bwd: grad = gout[0] * dloss/dp (gout is a device scalar).                  */
 enum { STC_LOSS_L1 = 0, STC_LOSS_MSE_CONST = 1, STC_LOSS_BCE_CONST = 2 };
 int stc_loss_parts(int64_t n);
+/* One objective of several loss terms (replaces the per-term AdversarialLoss / DataLoss calls and the
+ * torch scalar arithmetic combining them, STCGAN/stcgan.py:240-251 (D, loss type "normal") and
+ * :291-299 (G)).  Term k: kind (STC_LOSS_*), constant target consts[k] or targets[k], numels[k] elements.
+ * fwd: vals[k] = mean loss of term k (bit-identical to stc_loss_fwd), then
+ *   STC_LOSS_COMBINE_D (terms fake1, real1, fake2, real2; w = {lambda2, lambda3, -}):
+ *     out[0] = D, vals[4] = D1, vals[5] = D2 with D1 = (fake1 + real1) * 0.5, D2 = (fake2 + real2) * 0.5,
+ *     D = l2*D1 + l3*D2 (vals: 6 floats);
+ *   STC_LOSS_COMBINE_G (terms data1, data2, G1, G2; w = {lambda1, lambda2, lambda3}):
+ *     out[0] = G = ((data1 + l1*data2) + l2*G1) + l3*G2;
+ *   fp32, one rounding per operation in that order (the torch evaluation).  part: stc_loss_multi_parts floats.
+ * bwd: grads[k] (nullable) = ((gout * wa[k]) * wb[k]) / n_k * dloss_k/dp. */
+#define STC_LOSS_MAX_TERMS 8
+#define STC_LOSS_COMBINE_D 0
+#define STC_LOSS_COMBINE_G 1
+int stc_loss_multi_parts(int nterm, const int64_t* numels);
+int stc_loss_multi_fwd(int nterm, const int32_t* kinds, const float* consts, const float* const* preds,
+                       const float* const* targets, const int64_t* numels, int mode, const float* w,
+                       float* part, float* vals, float* out, void* stream);
+int stc_loss_multi_bwd(int nterm, const int32_t* kinds, const float* consts, const float* const* preds,
+                       const float* const* targets, const int64_t* numels, const float* wa, const float* wb,
+                       const float* gout, float* const* grads, void* stream);
 int stc_loss_fwd(int kind, const float* p, const float* t, float c, int64_t n,
                  float* part, float* out, void* stream);
 int stc_loss_bwd(int kind, const float* p, const float* t, float c, int64_t n,

@@ -17,11 +17,13 @@ ap.add_argument("--steps", type=int, default=4)
 ap.add_argument("--warmup", type=int, default=2)
 ap.add_argument("--dtype", default="bf16")
 ap.add_argument("--streams", type=int, default=1)
+ap.add_argument("--fused", type=int, default=1)
+ap.add_argument("--repeat", type=int, default=1)
 args = ap.parse_args()
 a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5, beta2=0.999,
                           D_loss_fn="standard", D_loss_type="normal", ngf=64, dtype=args.dtype, load_weights_g1=None,
                           load_weights_g2=None, load_weights_d1=None, load_weights_d2=None,
-                          streams=bool(args.streams))
+                          streams=bool(args.streams), fused_objectives=bool(args.fused))
 torch.manual_seed(1234)
 tr = STCGAN(a)
 dev = torch.device("cuda", 0)
@@ -32,9 +34,10 @@ y = torch.rand((B, 3, 256, 256), device=dev) * 2 - 1
 for _ in range(args.warmup):
     tr.train_step(x, m, y)
 torch.cuda.synchronize()
-t0 = time.perf_counter()
-for _ in range(args.steps):
-    tr.train_step(x, m, y)
-torch.cuda.synchronize()
-print(f"{(time.perf_counter() - t0) / args.steps * 1e3:.3f} ms/step ({args.steps} steps, streams={args.streams})",
-      flush=True)
+for _ in range(args.repeat):
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_step(x, m, y)
+    torch.cuda.synchronize()
+    print(f"{(time.perf_counter() - t0) / args.steps * 1e3:.3f} ms/step ({args.steps} steps, streams={args.streams}, "
+          f"fused={args.fused})", flush=True)

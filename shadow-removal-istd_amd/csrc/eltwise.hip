@@ -337,6 +337,101 @@ extern "C" int stc_loss_bwd(int kind, const float* p, const float* t, float c, i
   return 0;
 }
 
+// ---- several loss terms of one objective in two launches (forward) / one launch (backward) --------
+// Each term is exactly stc_loss_fwd's two-level sum (same blocks, same per-block order, the same fp64
+// final reduction), so its value is bit-identical to the single-term call; the objective's combination
+// of the terms (STCGAN/stcgan.py:240-251, 291-299) is then evaluated with one fp32 rounding per torch op,
+// in torch's order, and the backward scales each term by the same fp32 product chain autograd forms.
+struct LossTerms {
+  const float* p[STC_LOSS_MAX_TERMS];
+  const float* t[STC_LOSS_MAX_TERMS];
+  float* g[STC_LOSS_MAX_TERMS];
+  long long n[STC_LOSS_MAX_TERMS];
+  float c[STC_LOSS_MAX_TERMS];
+  float wa[STC_LOSS_MAX_TERMS], wb[STC_LOSS_MAX_TERMS];
+  int kind[STC_LOSS_MAX_TERMS];
+  int first[STC_LOSS_MAX_TERMS + 1];  // first block of each term
+  int count;
+};
+
+__device__ __forceinline__ int loss_term_of(const LossTerms& a, int blk) {
+  int k = 0;
+  while (k + 1 < a.count && blk >= a.first[k + 1]) ++k;
+  return k;
+}
+
+__global__ void loss_multi_partial_kernel(LossTerms a, float* part) {
+  const int k = loss_term_of(a, blockIdx.x);
+  const long long b0 = (long long)(blockIdx.x - a.first[k]) * LOSS_PER_BLOCK;
+  const float* p = a.p[k];
+  const float* t = a.t[k];
+  const long long n = a.n[k];
+  const int kind = a.kind[k];
+  const float c = a.c[k];
+  float acc = 0.f;
+  for (int q = 0; q < 16; ++q) {
+    const long long i = b0 + q * LOSS_BLOCK + threadIdx.x;
+    if (i < n) acc += loss_elem(kind, p[i], t ? t[i] : c);
+  }
+  __shared__ float red[LOSS_BLOCK];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = LOSS_BLOCK / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+#pragma clang fp contract(off)
+// vals[k] = term k (then D1, D2 for STC_LOSS_COMBINE_D); out[0] = the objective
+__global__ void loss_multi_final_kernel(LossTerms a, const float* part, int mode, float w0, float w1, float w2,
+                                        float* vals, float* out) {
+  __shared__ double red[256];
+  __shared__ float v[STC_LOSS_MAX_TERMS];
+  for (int k = 0; k < a.count; ++k) {
+    double s = 0;
+    for (int q = a.first[k] + threadIdx.x; q < a.first[k + 1]; q += 256) s += part[q];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) v[k] = (float)(red[0] / (double)a.n[k]);
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  for (int k = 0; k < a.count; ++k) vals[k] = v[k];
+  if (mode == STC_LOSS_COMBINE_D) {
+    // D1 = (fake1 + real1) * 0.5, D2 = (fake2 + real2) * 0.5, D = l2 * D1 + l3 * D2
+    const float d1 = (v[0] + v[1]) * 0.5f, d2 = (v[2] + v[3]) * 0.5f;
+    out[0] = d1 * w0 + d2 * w1;
+    vals[a.count] = d1;
+    vals[a.count + 1] = d2;
+  } else {
+    // G = ((data1 + l1 * data2) + l2 * G1) + l3 * G2
+    out[0] = ((v[0] + v[1] * w0) + v[2] * w1) + v[3] * w2;
+  }
+}
+
+// grad_k = ((gout * wa_k) * wb_k) / n_k * dloss_k/dp, the chain autograd applies to a term of the objective
+__global__ void loss_multi_bwd_kernel(LossTerms a, const float* gout) {
+  const int k = loss_term_of(a, blockIdx.x);
+  float* grad = a.g[k];
+  if (!grad) return;
+  const float g = ((gout[0] * a.wa[k]) * a.wb[k]) / (float)a.n[k];
+  const float* p = a.p[k];
+  const float* t = a.t[k];
+  const long long n = a.n[k];
+  const int kind = a.kind[k];
+  const float c = a.c[k];
+  const long long nb = a.first[k + 1] - a.first[k];
+  for (long long i = (long long)(blockIdx.x - a.first[k]) * 256 + threadIdx.x; i < n; i += nb * 256)
+    grad[i] = g * loss_grad(kind, p[i], t ? t[i] : c);
+}
+#pragma clang fp contract(on)
+
 // Multi-tensor form: one launch packs up to STC_PACK_MAX weights; block ranges per descriptor.
 struct PackSet {
   stc_pack_desc d[STC_PACK_MAX];
@@ -422,6 +517,65 @@ extern "C" int stc_pack_weight(int dtype, int mode, const float* W, int P, int Q
     hipLaunchKernelGGL(pack_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, mode, W, P, Q, (float*)out, N_pad, C_pad, nph, taps);
   else
     hipLaunchKernelGGL(pack_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, mode, W, P, Q, (bf16*)out, N_pad, C_pad, nph, taps);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+static int loss_terms(int nterm, const int32_t* kinds, const float* consts, const float* const* preds,
+                      const float* const* targets, const int64_t* numels, LossTerms& a, bool bwd_blocks) {
+  STC_REQUIRE(nterm >= 1 && nterm <= STC_LOSS_MAX_TERMS, "stc_loss_multi: 1..%d terms", STC_LOSS_MAX_TERMS);
+  int blocks = 0;
+  a.count = nterm;
+  for (int k = 0; k < nterm; ++k) {
+    STC_REQUIRE(kinds[k] >= 0 && kinds[k] <= 2 && numels[k] > 0 && preds[k], "stc_loss_multi: bad term %d", k);
+    STC_REQUIRE(kinds[k] != STC_LOSS_L1 || targets[k], "stc_loss_multi: L1 term %d needs a target", k);
+    a.p[k] = preds[k];
+    a.t[k] = targets[k];
+    a.n[k] = numels[k];
+    a.c[k] = consts[k];
+    a.kind[k] = kinds[k];
+    a.first[k] = blocks;
+    blocks += bwd_blocks ? (int)std::min<int64_t>((numels[k] + 255) / 256, 2048) : stc_loss_parts(numels[k]);
+  }
+  a.first[nterm] = blocks;
+  return blocks;
+}
+
+extern "C" int stc_loss_multi_parts(int nterm, const int64_t* numels) {
+  int np = 0;
+  for (int k = 0; k < nterm; ++k) np += stc_loss_parts(numels[k]);
+  return np;
+}
+
+extern "C" int stc_loss_multi_fwd(int nterm, const int32_t* kinds, const float* consts, const float* const* preds,
+                                  const float* const* targets, const int64_t* numels, int mode, const float* w,
+                                  float* part, float* vals, float* out, void* stream) {
+  STC_REQUIRE(mode == STC_LOSS_COMBINE_D || mode == STC_LOSS_COMBINE_G, "stc_loss_multi_fwd: bad mode");
+  STC_REQUIRE(nterm == 4, "stc_loss_multi_fwd: the combinations take 4 terms");
+  LossTerms a{};
+  const int blocks = loss_terms(nterm, kinds, consts, preds, targets, numels, a, false);
+  if (blocks < 0) return blocks;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(loss_multi_partial_kernel, dim3(blocks), dim3(LOSS_BLOCK), 0, st, a, part);
+  STC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(loss_multi_final_kernel, dim3(1), dim3(256), 0, st, a, (const float*)part, mode, w[0], w[1],
+                     w[2], vals, out);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_loss_multi_bwd(int nterm, const int32_t* kinds, const float* consts, const float* const* preds,
+                                  const float* const* targets, const int64_t* numels, const float* wa,
+                                  const float* wb, const float* gout, float* const* grads, void* stream) {
+  LossTerms a{};
+  const int blocks = loss_terms(nterm, kinds, consts, preds, targets, numels, a, true);
+  if (blocks < 0) return blocks;
+  for (int k = 0; k < nterm; ++k) {
+    a.g[k] = grads[k];
+    a.wa[k] = wa[k];
+    a.wb[k] = wb[k];
+  }
+  hipLaunchKernelGGL(loss_multi_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, gout);
   STC_CHECK_LAUNCH();
   return 0;
 }

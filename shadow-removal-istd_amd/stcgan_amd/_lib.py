@@ -16,6 +16,7 @@ F32, BF16 = 0, 1
 CONV_S2, CONV_S1, CONVT_S2, CONV_S1_DGRAD = 0, 1, 2, 3
 PACK_CONV_FWD, PACK_CONV_DGRAD, PACK_CONV_S1_DGRAD, PACK_CONVT_FWD, PACK_CONVT_DGRAD = 0, 1, 2, 3, 4
 LOSS_L1, LOSS_MSE_CONST, LOSS_BCE_CONST = 0, 1, 2
+LOSS_COMBINE_D, LOSS_COMBINE_G = 0, 1
 
 
 class View(ctypes.Structure):
@@ -78,6 +79,9 @@ _SIGS = {
     "stc_loss_parts": (_i32, [_i64]),
     "stc_loss_fwd": (_i32, [_i32, _vp, _vp, _f32, _i64, _vp, _vp, _vp]),
     "stc_loss_bwd": (_i32, [_i32, _vp, _vp, _f32, _i64, _vp, _vp, _vp]),
+    "stc_loss_multi_parts": (_i32, [_i32, _vp]),
+    "stc_loss_multi_fwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "stc_loss_multi_bwd": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "stc_adam_step": (_i32, [_vp, _i32, _i64, _f32, _f32, _f32, _f32, _i32, _vp]),
     "stc_adam_elems_per_block": (_i32, []),
     "stc_conv_wgrad_rows": (_i32, [_i32, _i32, View, _i32, _i32, View, _i32, _i32, _vp, _vp, _i64, _vp]),
@@ -129,8 +133,14 @@ def check(rc, what):
         raise RuntimeError(f"{what} failed (rc={rc}): {msg}")
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_device = torch._C._cuda_getDevice
+
+
 def stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """The current HIP stream of the current device (the raw accessor: torch.cuda.current_stream() costs
+    ~8 us of Python per call, and the step makes a few hundred launches)."""
+    return ctypes.c_void_p(_raw_stream(_cur_device()))
 
 
 def ptr(t):

@@ -4,6 +4,8 @@ DataLoss (STCGAN/loss.py:14-26) and AdversarialLoss (STCGAN/loss.py:59-86) run a
 HIP reduction kernels (deterministic two-level sums) with hand-written gradients.
 VisualLoss and SoftAdapt are not on the path.
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -42,6 +44,79 @@ class _LossFn(torch.autograd.Function):
         check(lib().stc_loss_bwd(ctx.kind, ptr(pred), ptr(t), float(ctx.c), pred.numel(), ptr(gout), ptr(grad),
                                  stream()), "stc_loss_bwd")
         return None, None, grad, None
+
+
+def _arr(ctype, vals):
+    return (ctype * len(vals))(*vals)
+
+
+class _ObjectiveFn(torch.autograd.Function):
+    """Four loss terms and the scalar arithmetic combining them as one node: two launches forward, one
+    backward (stc_loss_multi_*), instead of 4 loss nodes and ~6 torch scalar ops with their own launches
+    and autograd nodes.  Values bit-identical to the per-term path (same reductions, same fp32 rounding
+    order).  forward -> (objective, parts): parts = the named sub-losses, not differentiable."""
+
+    @staticmethod
+    def forward(ctx, mode, kinds, consts, w, wab, *tensors):
+        preds = [t.contiguous() for t in tensors[:4]]
+        targets = [t.contiguous() if t is not None else None for t in tensors[4:]]
+        for p_, t_ in zip(preds, targets):
+            if p_.dtype != torch.float32 or not p_.is_cuda:
+                raise TypeError("stcgan_amd losses take fp32 CUDA inputs")
+            if t_ is not None and t_.shape != p_.shape:
+                raise ValueError(f"loss: target shape {tuple(t_.shape)} != prediction {tuple(p_.shape)}")
+        dev = preds[0].device
+        numels = [p_.numel() for p_ in preds]
+        l = lib()
+        n_arr = _arr(ctypes.c_int64, numels)
+        part = torch.empty(l.stc_loss_multi_parts(4, n_arr), dtype=torch.float32, device=dev)
+        vals = torch.empty(6, dtype=torch.float32, device=dev)  # the 4 terms, then D1, D2 (mode D)
+        total = torch.empty((), dtype=torch.float32, device=dev)
+        args = (4, _arr(ctypes.c_int32, kinds), _arr(ctypes.c_float, consts),
+                _arr(ctypes.c_void_p, [p_.data_ptr() for p_ in preds]),
+                _arr(ctypes.c_void_p, [t_.data_ptr() if t_ is not None else None for t_ in targets]), n_arr)
+        check(l.stc_loss_multi_fwd(*args, mode, _arr(ctypes.c_float, list(w) + [0.0] * (3 - len(w))), ptr(part),
+                                   ptr(vals), ptr(total), stream()), "stc_loss_multi_fwd")
+        ctx.args, ctx.wab = args, wab
+        ctx.save_for_backward(*preds, *[t_ if t_ is not None else preds[0] for t_ in targets])
+        ctx.mark_non_differentiable(vals)
+        return total, vals
+
+    @staticmethod
+    def backward(ctx, gout, _gparts):
+        preds = ctx.saved_tensors[:4]
+        need = ctx.needs_input_grad[5:9]
+        grads = [torch.empty_like(p_) if nd else None for p_, nd in zip(preds, need)]
+        wa, wb = ctx.wab
+        gout = gout.contiguous().float()
+        check(lib().stc_loss_multi_bwd(*ctx.args, _arr(ctypes.c_float, wa), _arr(ctypes.c_float, wb), ptr(gout),
+                                       _arr(ctypes.c_void_p, [g.data_ptr() if g is not None else None
+                                                              for g in grads]), stream()), "stc_loss_multi_bwd")
+        return (None,) * 5 + tuple(grads) + (None,) * 4
+
+
+def d_objective(adv, C1_fake, C1_real, C2_fake, C2_real, lambda2, lambda3):
+    """The D objective of STCGAN/stcgan.py:240-251 (loss type "normal"):
+    D1 = (adv(C1_fake, fake) + adv(C1_real, real)) * 0.5, D2 likewise, D = lambda2*D1 + lambda3*D2.
+    Returns (D, D1, D2)."""
+    real, fake = adv._labels
+    k = L.LOSS_BCE_CONST if adv.ls else L.LOSS_MSE_CONST
+    total, parts = _ObjectiveFn.apply(L.LOSS_COMBINE_D, [k] * 4, [fake, real, fake, real], [lambda2, lambda3],
+                                      ([lambda2, lambda2, lambda3, lambda3], [0.5] * 4),
+                                      C1_fake, C1_real, C2_fake, C2_real, None, None, None, None)
+    return total, parts[4], parts[5]
+
+
+def g_objective(adv, m_pred, m, y_pred, y, C1_fake, C2_fake, lambda1, lambda2, lambda3):
+    """The G objective of STCGAN/stcgan.py:291-299 (loss type "normal"): G1 = adv(C1_fake, real),
+    G2 = adv(C2_fake, real), data1 = L1(m_pred, m), data2 = L1(y_pred, y),
+    G = data1 + lambda1*data2 + lambda2*G1 + lambda3*G2.  Returns (G, G1, G2, data1, data2)."""
+    real = adv._labels[0]
+    k = L.LOSS_BCE_CONST if adv.ls else L.LOSS_MSE_CONST
+    total, v = _ObjectiveFn.apply(L.LOSS_COMBINE_G, [L.LOSS_L1, L.LOSS_L1, k, k], [0.0, 0.0, real, real],
+                                  [lambda1, lambda2, lambda3], ([1.0, lambda1, lambda2, lambda3], [1.0] * 4),
+                                  m_pred, y_pred, C1_fake, C2_fake, m, y, None, None)
+    return total, v[2], v[3], v[0], v[1]
 
 
 def l1_loss(pred, target):

@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from . import engine
+from . import ops
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
 
@@ -64,6 +65,7 @@ class _HipNet(nn.Module):
         """'fp32' (default, parity path) or 'bf16' (bf16 operands, fp32 accumulation/BN/master weights)."""
         self.compute_dtype = _DTYPES[dtype] if isinstance(dtype, str) else dtype
         self._pack_cache.clear()
+        ops.invalidate_packs()
         return self
 
     def _run(self, inp):
@@ -81,6 +83,7 @@ class _HipNet(nn.Module):
 
     def _apply(self, fn, *args, **kwargs):
         self._pack_cache.clear()
+        ops.invalidate_packs()
         self._plan = None
         return super()._apply(fn, *args, **kwargs)
 

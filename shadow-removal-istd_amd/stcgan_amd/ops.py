@@ -298,8 +298,19 @@ def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=Non
 _PHASED = {L.PACK_CONV_DGRAD, L.PACK_CONVT_FWD}
 
 
+# bumped whenever a packed-operand buffer is created or dropped: the optimiser's cached pointer tables
+# (optim.Adam._fast_step) hold the addresses of these buffers
+PACK_EPOCH = 0
+
+
+def invalidate_packs():
+    global PACK_EPOCH
+    PACK_EPOCH += 1
+
+
 def pack(mode, W, n_pad, c_pad, dt):
     """Pack a torch weight [P][Q][4][4] into the GEMM operand layout [phases][n_pad][taps][c_pad]."""
+    invalidate_packs()
     P, Q = W.shape[0], W.shape[1]
     nph, taps = (4, 4) if mode in _PHASED else (1, 16)
     out = torch.empty((nph, n_pad, taps, c_pad), dtype=dt, device=W.device)
@@ -369,6 +380,7 @@ def refresh_packs(cache):
         if hit is None:
             nph, taps = (4, 4) if mode in _PHASED else (1, 16)
             out = torch.empty((nph, n_pad, taps, c_pad), dtype=dt, device=W.device)
+            invalidate_packs()
         else:
             out = hit[1]
         Wc = W.detach()

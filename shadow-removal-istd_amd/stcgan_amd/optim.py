@@ -33,7 +33,10 @@ class Adam(torch.optim.Optimizer):
             self._epb = lib().stc_adam_elems_per_block()
             self._steps = {}    # id(param) -> (state step tensor, its value as a Python int)
             self._tables = {}   # (group, step) -> (pointer key, device table, blocks)
+            self._fast = {}     # group -> the last step's table and per-parameter records (see _fast_step)
         for gi, group in enumerate(self.param_groups):
+            if self._fast_step(gi, group):
+                continue
             b1, b2 = group["betas"]
             # group params by step count (all equal in practice).  The step count is mirrored in a
             # Python int (no per-parameter tensor op / .item() on the host path), and the state's
@@ -83,7 +86,82 @@ class Adam(torch.optim.Optimizer):
                     ver = ops.pack_version(p)
                     for (pkey, cache, out) in targets:
                         cache[pkey] = (ver, out)
+            self._fast.pop(gi, None)
+            if len(by_step) == 1:
+                (step, plist), = by_step.items()
+                recs = [self._record(p) for p in plist]
+                self._fast[gi] = dict(
+                    key=tuple((id(p), p.data_ptr(), p.grad.data_ptr()) for p in plist), plist=plist,
+                    rows=[list(r[0]) for r in recs], table=self._tables[gi][1], blocks=self._tables[gi][2],
+                    targets=[r[2] for r in recs], step=step, epoch=ops.PACK_EPOCH,
+                    step_tensors=[self.state[p]["step"] for p in plist])
+                f = self._fast[gi]
+                f["tables"] = {f["key"]: (f["table"], f["blocks"])}
         return loss
+
+    def _fast_step(self, gi, group):
+        """The steady-state step of a group without per-parameter record building: valid while the
+        parameters with a gradient, their storage, the optimiser state and every packed operand
+        buffer (ops.PACK_EPOCH) are those of the previous step; only the gradients' addresses are
+        read (usually unchanged: the table is then reused as is).  Returns False to take the full path."""
+        f = self._fast.get(gi)
+        if f is None or f["epoch"] != ops.PACK_EPOCH:
+            return False
+        plist = f["plist"]
+        key = []
+        for p in group["params"]:
+            g = p.grad
+            if g is None:
+                continue
+            if g.dtype is not torch.float32 or not g.is_contiguous():
+                return False
+            key.append((id(p), p.data_ptr(), g.data_ptr()))
+        key = tuple(key)
+        if key != f["key"]:
+            if len(key) != len(f["key"]) or any(a[:2] != b[:2] for a, b in zip(key, f["key"])):
+                return False
+            # same parameters, other gradient buffers (the caching allocator cycles through a few address
+            # patterns): a table per pattern, built once -- patch the grad column and upload
+            hit = f["tables"].get(key)
+            if hit is None:
+                rows, blocks = [], 0
+                for r, k in zip(f["rows"], key):
+                    r[1] = k[2]
+                for r, p in zip(f["rows"], plist):
+                    rows.append(r[:5] + [blocks] + r[5:])
+                    blocks += self._nblocks(p, r)
+                table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(plist[0].device, non_blocking=True)
+                if len(f["tables"]) >= 8:
+                    f["tables"].pop(next(iter(f["tables"])))
+                hit = f["tables"][key] = (table, blocks)
+            f["table"], f["blocks"] = hit
+            f["key"] = key
+            self._tables[gi] = (None, f["table"], f["blocks"])
+        step = f["step"] + 1
+        b1, b2 = group["betas"]
+        torch._foreach_add_(f["step_tensors"], 1.0)
+        check(lib().stc_adam_pack_step(ptr(f["table"]), len(plist), f["blocks"], float(group["lr"]), float(b1),
+                                       float(b2), float(group["eps"]), step, stream()), "stc_adam_pack_step")
+        ops.bump(plist)
+        for p, targets, st in zip(plist, f["targets"], f["step_tensors"]):
+            self._steps[id(p)] = (st, step)
+            if targets:
+                ver = ops.pack_version(p)
+                for (pkey, cache, out) in targets:
+                    cache[pkey] = (ver, out)
+        f["step"] = step
+        return True
+
+    @staticmethod
+    def _nblocks(p, row):
+        if row[5]:  # packed 4x4 weight: 16x16 (p, q) tiles
+            return ((p.shape[0] + 15) // 16) * row[8]
+        return (p.numel() + 1023) // 1024
+
+    def load_state_dict(self, state_dict):
+        self._fast = {}
+        self._steps = {}
+        return super().load_state_dict(state_dict)
 
     def _record(self, p):
         """(table row without first_block, blocks, packed targets) of one parameter."""

@@ -53,6 +53,12 @@ def broadcast_state(modules, src=0):
         for m in modules:
             for t in list(m.parameters()) + list(m.buffers()):
                 dist.broadcast(t.data, src)
+            # the in-place write through .data does not bump the parameters' versions: drop any packed
+            # operands made from the pre-broadcast values
+            if getattr(m, "_pack_cache", None):
+                from . import ops
+                m._pack_cache.clear()
+                ops.invalidate_packs()
 
 
 def broadcast_buffers(modules, src=0):

@@ -30,7 +30,7 @@ import torch.nn as nn
 from . import engine
 from . import networks
 from . import parallel
-from .loss import AdversarialLoss, DataLoss
+from .loss import AdversarialLoss, DataLoss, d_objective, g_objective
 from .optim import Adam
 
 
@@ -96,6 +96,8 @@ class STCGAN(object):
         self.sync_D.enable_overlap()
         # discriminators on side HIP streams (train_step / _lanes); off for a strictly serial step
         self.streams = bool(getattr(args, "streams", True))
+        # loss type "normal": the D and G objectives as one fused node each (loss.d_objective / g_objective)
+        self.fused_objectives = bool(getattr(args, "fused_objectives", True))
         self._side = None
 
         data_dir = getattr(args, "data_dir", None)
@@ -253,8 +255,12 @@ class STCGAN(object):
             if l1 is not None:
                 main.wait_stream(l1)
                 main.wait_stream(l2)
-            D1_loss, D2_loss = self._d_losses(C1_real, C1_fake, C2_real, C2_fake)
-            D_loss = self.lambda2 * D1_loss + self.lambda3 * D2_loss
+            if self.d_loss_type == "normal" and self.fused_objectives:  # one node (loss.d_objective)
+                D_loss, D1_loss, D2_loss = d_objective(self.adv_loss, C1_fake, C1_real, C2_fake, C2_real,
+                                                       self.lambda2, self.lambda3)
+            else:
+                D1_loss, D2_loss = self._d_losses(C1_real, C1_fake, C2_real, C2_fake)
+                D_loss = self.lambda2 * D1_loss + self.lambda3 * D2_loss
             if training:
                 D_loss.backward()
                 self.sync_D()
@@ -275,10 +281,14 @@ class STCGAN(object):
                 if l1 is not None:
                     main.wait_stream(l1)
                     main.wait_stream(l2)
-            G1_loss, G2_loss = self._g_losses(C1_real, C1_fake, C2_real, C2_fake)
-            data1_loss = self.data_loss(m_pred, m)
-            data2_loss = self.data_loss(y_pred, y)
-            G_loss = data1_loss + self.lambda1 * data2_loss + self.lambda2 * G1_loss + self.lambda3 * G2_loss
+            if self.d_loss_type == "normal" and self.fused_objectives:
+                G_loss, G1_loss, G2_loss, data1_loss, data2_loss = g_objective(
+                    self.adv_loss, m_pred, m, y_pred, y, C1_fake, C2_fake, self.lambda1, self.lambda2, self.lambda3)
+            else:
+                G1_loss, G2_loss = self._g_losses(C1_real, C1_fake, C2_real, C2_fake)
+                data1_loss = self.data_loss(m_pred, m)
+                data2_loss = self.data_loss(y_pred, y)
+                G_loss = data1_loss + self.lambda1 * data2_loss + self.lambda2 * G1_loss + self.lambda3 * G2_loss
             if training:
                 G_loss.backward()
                 self.sync_G()
