@@ -388,6 +388,14 @@ namespace stc {
 // lanes: lane l takes the image's pixels 16 ps + l + 64 k; the image's D plane (RO channels, zero-padded by 2) sits in LDS and is
 // read as broadcasts.  The 16 lanes' partials are summed in a fixed order (through LDS) into the
 // slab [image][RO][16 * Cg] (column tap * Cg + ci), which the ordered wide reduce sums over images.
+// One non-packed v_fma_f32.  The compiler otherwise pairs these accumulations into v_pk_fma_f32 with
+// op_sel; in that form the kernel returned sporadically different low-half sums (one (tap, even
+// channel) accumulator of a whole wave) when two processes shared the GPU (tests/test_gpu_dist.py).
+__device__ __forceinline__ float fma_scalar(float a, float b, float c) {
+  asm("v_fma_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
+
 template <typename T, int RO>
 __global__ void __launch_bounds__(256) wgrad_rows_kernel(const char* __restrict__ dp, long long d_bs, long long d_rs,
                                                          int d_ps, int d_co, int OH, int OW, const char* __restrict__ gp,
@@ -434,7 +442,7 @@ __global__ void __launch_bounds__(256) wgrad_rows_kernel(const char* __restrict_
         for (int kw = 0; kw < 4; ++kw) {
           const float dv = dl[(r * rows + qy - kh + 3) * cols + qx - kw + 3];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[r][kh * 4 + kw][e] = fmaf(gv[e], dv, acc[r][kh * 4 + kw][e]);
+          for (int e = 0; e < 4; ++e) acc[r][kh * 4 + kw][e] = fma_scalar(gv[e], dv, acc[r][kh * 4 + kw][e]);
         }
   };
   int q = plane + 16 * ps;
@@ -454,10 +462,8 @@ __global__ void __launch_bounds__(256) wgrad_rows_kernel(const char* __restrict_
   }
   // fixed-order sum over the 16 pixel planes (4 per wave), all through LDS: every plane stores its
   // partials (part[plane][r][t][64 channels], after the D plane), then each output is
-  // ((p0 + p1) + (p2 + p3)) per wave and (w0 + w1) + (w2 + w3) across waves -- the order the former
-  // xor-butterfly (ds_bpermute) version used.  That version gave sporadically different sums for one
-  // (tap, channel-in-quad) register of a whole wave when other streams' kernels shared the GPU
-  // (tests/test_gpu_dist.py), so the cross-lane step is plain LDS traffic now.
+  // ((p0 + p1) + (p2 + p3)) per wave and (w0 + w1) + (w2 + w3) across waves (the order of an xor
+  // butterfly over the planes followed by a cross-wave sum).
   float* part = sm + ((RO * rows * cols + 3) & ~3);
   constexpr int PL = RO * 16 * 64;  // floats per plane
 #pragma unroll

@@ -240,13 +240,11 @@ def _wgrad_kernel_name(plan, Hd, Wd):
     return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}>"
 
 
-# The narrow-R VALU weight gradient (stc_conv_wgrad_rows) for the PatchGAN logits layer is opt-in
-# (STC_WGRAD_ROWS=1, or rows_kernel=True per call): with two processes sharing one GPU
-# (tests/test_gpu_dist.py) it returned, in about one run of three, sums that differ by ~1e-6 relative
-# in one (tap, channel-in-quad) accumulator of a whole wave on bit-identical inputs -- also with its
-# lane butterfly replaced by LDS sums, its LDS regions separated and a persistent workspace -- while
-# the padded-GEMM path was clean in every run.  Off by default until that is understood (~0.1 ms/step).
-_ROWS_DEFAULT = os.environ.get("STC_WGRAD_ROWS", "0") == "1"
+# The narrow-R VALU weight gradient (stc_conv_wgrad_rows) for the PatchGAN logits layer (~25 us vs ~75 us
+# for the padded GEMM).  STC_WGRAD_ROWS=0 (or rows_kernel=False per call) takes the GEMM path.  Its
+# accumulations are forced to non-packed v_fma_f32 (csrc/wgrad.hip): compiled to v_pk_fma_f32 with op_sel,
+# it returned sporadically different low-half sums with two processes on one GPU (tests/test_gpu_dist.py).
+_ROWS_DEFAULT = os.environ.get("STC_WGRAD_ROWS", "1") == "1"
 
 
 def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None,
