@@ -174,12 +174,15 @@ def make_trainer(ngf, dtype, local):
 def roofline_of_step(tr, x, m, y, args, B, s):
     """Dominant kernel of one (untimed) train step by summed device time, and the north-star set."""
     import torch
-    from stcgan_amd import ops
+    from stcgan_amd import engine, ops
     ops._timer = []
-    lanes, tr.streams = tr.streams, False  # one stream: each launch's events bracket it alone
+    # one stream (no side-stream networks or weight gradients): each launch's events bracket it alone
+    lanes, tr.streams = tr.streams, False
+    overlap, engine.WGRAD_OVERLAP = engine.WGRAD_OVERLAP, False
     tr.train_step(x, m, y)
     torch.cuda.synchronize()
     launches, ops._timer, tr.streams = ops._timer, None, lanes
+    engine.WGRAD_OVERLAP = overlap
     per, shapes = {}, {}
     for name, _single, fl, e0, e1, desc in launches:
         ms = e0.elapsed_time(e1)

@@ -10,6 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "shadow-removal-istd_amd"))
 import torch  # noqa: E402
 
+from stcgan_amd import engine  # noqa: E402
 from stcgan_amd.stcgan import STCGAN  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -19,7 +20,12 @@ ap.add_argument("--dtype", default="bf16")
 ap.add_argument("--streams", type=int, default=1)
 ap.add_argument("--fused", type=int, default=1)
 ap.add_argument("--repeat", type=int, default=1)
+ap.add_argument("--wgrad-overlap", type=int, default=1)
+ap.add_argument("--ab", default="", help="comma list of wgrad-overlap settings cycled per repeat (same process)")
 args = ap.parse_args()
+engine.WGRAD_OVERLAP = args.wgrad_overlap > 0
+if args.wgrad_overlap > 1:
+    engine.WGRAD_OVERLAP_MAX_PIX = args.wgrad_overlap
 a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5, beta2=0.999,
                           D_loss_fn="standard", D_loss_type="normal", ngf=64, dtype=args.dtype, load_weights_g1=None,
                           load_weights_g2=None, load_weights_d1=None, load_weights_d2=None,
@@ -34,10 +40,24 @@ y = torch.rand((B, 3, 256, 256), device=dev) * 2 - 1
 for _ in range(args.warmup):
     tr.train_step(x, m, y)
 torch.cuda.synchronize()
-for _ in range(args.repeat):
+ab = [int(v) for v in args.ab.split(",")] if args.ab else None
+res = {}
+for rep in range(args.repeat):
+    if ab:
+        o = ab[rep % len(ab)]
+        engine.WGRAD_OVERLAP = o > 0
+        engine.WGRAD_OVERLAP_MAX_PIX = o if o > 1 else 1 << 30
+        args.wgrad_overlap = o
+        for _ in range(2):
+            tr.train_step(x, m, y)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.train_step(x, m, y)
     torch.cuda.synchronize()
     print(f"{(time.perf_counter() - t0) / args.steps * 1e3:.3f} ms/step ({args.steps} steps, streams={args.streams}, "
-          f"fused={args.fused})", flush=True)
+          f"fused={args.fused}, wgrad_overlap={args.wgrad_overlap})", flush=True)
+    res.setdefault(args.wgrad_overlap, []).append((time.perf_counter() - t0) / args.steps * 1e3)
+if ab:
+    for k, v in res.items():
+        print(f"wgrad_overlap={k}: median {sorted(v)[len(v) // 2]:.3f} ms/step over {len(v)}", flush=True)

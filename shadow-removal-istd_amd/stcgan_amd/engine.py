@@ -30,6 +30,45 @@ from .ops import LRELU
 # ----------------------------------------------------------------------------- helpers
 
 
+
+# ----------------------------------------------------------------------------- weight-gradient lane
+# The weight gradients of a backward hang off its input-gradient chain (each needs that layer's incoming
+# gradient and saved input; nothing on the chain needs them), so they run on a side stream per calling
+# stream and overlap the rest of the chain -- most of the deep (1x1-8x8) layers' kernels are latency-bound
+# small grids.  Joined before the backward returns its gradients.
+WGRAD_OVERLAP = True
+# interleaved A/B (scripts/train_steps.py --ab): none 13.74, <= 32x32 13.45, <= 64x64 13.64, all 13.75 ms/step
+WGRAD_OVERLAP_MAX_PIX = 32 * 32
+_WG_SIDE = {}
+
+
+class _WgradLane:
+    def __init__(self):
+        self.cur = torch.cuda.current_stream() if WGRAD_OVERLAP else None
+        self.side = None
+        if self.cur is not None:
+            self.side = _WG_SIDE.get(self.cur.cuda_stream)
+            if self.side is None:
+                self.side = _WG_SIDE[self.cur.cuda_stream] = torch.cuda.Stream(self.cur.device)
+
+    def run(self, fn, *reads, pixels=0):
+        """fn() on the side stream, after everything queued so far on the calling stream; ``reads``: the
+        calling stream's tensors fn reads that may be freed before the backward ends.  Only layers of at
+        most WGRAD_OVERLAP_MAX_PIX output pixels per image go to the side (the big ones fill the GPU alone;
+        overlapping them measured slower)."""
+        if self.side is None or pixels > WGRAD_OVERLAP_MAX_PIX:
+            return fn()
+        self.side.wait_stream(self.cur)
+        for t in reads:
+            t.record_stream(self.side)
+        with torch.cuda.stream(self.side):
+            return fn()
+
+    def join(self):
+        if self.side is not None:
+            self.cur.wait_stream(self.side)
+
+
 def _nhwc(B, H, W, C, dt, dev, zero=False):
     f = torch.zeros if zero else torch.empty
     return f((B, H, W, C), dtype=dt, device=dev)
@@ -166,6 +205,7 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
     B = y.shape[0]
     grads = {}
     gy = gy.contiguous()
+    lane = _WgradLane() if need_w else None
 
     def put(p, g):
         if need_w:
@@ -185,7 +225,9 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
         cg = cp if k == 0 else cout_t
         dqv = L.nhwc_view(dq)
         if need_w:  # D = convT input (grid S[k+1]), G = dq gathered at stride 2
-            put(plan.convT[k].weight, ops.wgrad(B, 2, L.nhwc_view(cr[k]), cin_t, dqv, cg, cout_t, dt, device=dev))
+            put(plan.convT[k].weight, lane.run(lambda k=k, dqv=dqv, cin_t=cin_t, cg=cg, cout_t=cout_t: ops.wgrad(
+                B, 2, L.nhwc_view(cr[k]), cin_t, dqv, cg, cout_t, dt, device=dev), dq,
+                pixels=S[k + 1][0] * S[k + 1][1]))
         wd = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_DGRAD, cin_t, cg, dt)
         if k < Lv - 1:
             ah, aw = _pad2(S, k + 1)
@@ -218,8 +260,9 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
         drv = L.nhwc_view(dr)
         if k == 0:
             if need_w:
-                put(plan.conv[0].weight, ops.wgrad(B, 2, drv, co[0], L.nhwc_view(xin), saved["cin_pad"],
-                                                   saved["cin"], dt, device=dev))
+                put(plan.conv[0].weight, lane.run(lambda drv=drv: ops.wgrad(
+                    B, 2, drv, co[0], L.nhwc_view(xin), saved["cin_pad"], saved["cin"], dt, device=dev), dr,
+                    pixels=S[1][0] * S[1][1]))
             if need_src:
                 wd = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_DGRAD, saved["cin_pad"], co[0], dt)
                 gx = _nhwc(B, 2 * S[1][0], 2 * S[1][1], saved["cin_pad"], dt, dev)
@@ -232,8 +275,9 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
             break
         cprev = co[k - 1]
         if need_w:  # D = dr_k (grid S[k+1]), G = conv_k input = ad[k-1]
-            put(plan.conv[k].weight, ops.wgrad(B, 2, drv, co[k], L.nhwc_view(ad[k - 1]), cprev, cprev, dt,
-                                               device=dev))
+            put(plan.conv[k].weight, lane.run(lambda k=k, drv=drv, cprev=cprev: ops.wgrad(
+                B, 2, drv, co[k], L.nhwc_view(ad[k - 1]), cprev, cprev, dt, device=dev), dr,
+                pixels=S[k + 1][0] * S[k + 1][1]))
         wd = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_DGRAD, cprev, co[k], dt)
         ga = _nhwc(B, 2 * S[k + 1][0], 2 * S[k + 1][1], cprev, dt, dev)
         # r_{k-1} feeds the skip (ReLU) and conv_k (LeakyReLU); then BN_down[k-1] (absent for k-1 == 0)
@@ -252,6 +296,8 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
                                           g_other=g1, s_other=0.0, dxv=L.nhwc_view(dr))
             put(bn.weight, dg)
             put(bn.bias, db)
+    if lane is not None:
+        lane.join()
     return src_grads, grads
 
 
@@ -351,17 +397,22 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
     ops.gather([gout.contiguous()], g, dt)
     gch = cp
     src_grads = None
+    lane = _WgradLane() if need_w else None
     for i in range(n - 1, -1, -1):
         cv = plan.convs[i]
         s = plan.strides[i]
         cout = cv.out_channels
         gv = L.nhwc_view(g, 0, h, w)  # gradient wrt conv_i output (pre-activation / pre-BN), gch channels
         if need_w:
-            dW = ops.wgrad(B, s, gv, gch, L.nhwc_view(act[i]), chans[i], saved["cin"] if i == 0 else chans[i], dt,
-                           device=dev, rows=cout)
+            def wg(i=i, s=s, cout=cout, gv=gv, gch=gch, cv=cv):
+                dW = ops.wgrad(B, s, gv, gch, L.nhwc_view(act[i]), chans[i], saved["cin"] if i == 0 else chans[i],
+                               dt, device=dev, rows=cout)
+                db = ops.chan_sum(B, gv, gch, cout, dt, dev) if cv.bias is not None else None
+                return dW, db
+            dW, dbias = lane.run(wg, g, pixels=h * w)
             grads[id(cv.weight)] = dW[:cout] if gch != cout else dW
             if cv.bias is not None:
-                grads[id(cv.bias)] = ops.chan_sum(B, gv, gch, cout, dt, dev)
+                grads[id(cv.bias)] = dbias
         if i == 0:
             if need_src:
                 wd = ops.packed(cache, cv.weight, L.PACK_CONV_DGRAD, saved["cin_pad"], gch, dt)
@@ -400,6 +451,8 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
                 grads[id(bn.weight)] = dg
                 grads[id(bn.bias)] = db
         g, gch, h, w = gn, cin, ph, pw
+    if lane is not None:
+        lane.join()
     return src_grads, grads
 
 
