@@ -1,6 +1,7 @@
 """K bf16 bs=32 256^2 train steps (the bench workload) and nothing else: the command profiled by
 scripts/gpu_steps.sh, so per-step kernel totals are the rocprof totals / (K + W)."""
 import argparse
+import json
 import os
 import sys
 import time
@@ -22,6 +23,9 @@ ap.add_argument("--fused", type=int, default=1)
 ap.add_argument("--repeat", type=int, default=1)
 ap.add_argument("--wgrad-overlap", type=int, default=1)
 ap.add_argument("--ab", default="", help="comma list of wgrad-overlap settings cycled per repeat (same process)")
+ap.add_argument("--ab-attr", default="", help="name=v1,v2: trainer attribute (int) cycled per repeat (same process)")
+ap.add_argument("--ab-plans", default="", help="JSON list of {name, conv: [[key..., cfg, ks]], wgrad: [[key..., cfg, "
+                "splits]]} plan-override settings cycled per repeat (same process)")
 args = ap.parse_args()
 engine.WGRAD_OVERLAP = args.wgrad_overlap > 0
 if args.wgrad_overlap > 1:
@@ -41,8 +45,33 @@ for _ in range(args.warmup):
     tr.train_step(x, m, y)
 torch.cuda.synchronize()
 ab = [int(v) for v in args.ab.split(",")] if args.ab else None
+plans = json.loads(args.ab_plans) if args.ab_plans else None
 res = {}
+attr = None
+if args.ab_attr:
+    an, av = args.ab_attr.split("=")
+    attr = (an, [int(v) for v in av.split(",")])
 for rep in range(args.repeat):
+    if attr:
+        v = attr[1][rep % len(attr[1])]
+        setattr(tr, attr[0], type(getattr(tr, attr[0]))(v))
+        args.wgrad_overlap = f"{attr[0]}={v}"
+        for _ in range(2):
+            tr.train_step(x, m, y)
+        torch.cuda.synchronize()
+    if plans:
+        from stcgan_amd import ops
+        pl = plans[rep % len(plans)]
+        ops.FORCE_CONV.clear()
+        ops.FORCE_WGRAD.clear()
+        for e in pl.get("conv", []):
+            ops.FORCE_CONV[tuple(e[:6])] = tuple(e[6:8])
+        for e in pl.get("wgrad", []):
+            ops.FORCE_WGRAD[tuple(e[:5])] = tuple(e[5:7])
+        args.wgrad_overlap = pl["name"]
+        for _ in range(2):
+            tr.train_step(x, m, y)
+        torch.cuda.synchronize()
     if ab:
         o = ab[rep % len(ab)]
         engine.WGRAD_OVERLAP = o > 0
@@ -58,6 +87,6 @@ for rep in range(args.repeat):
     print(f"{(time.perf_counter() - t0) / args.steps * 1e3:.3f} ms/step ({args.steps} steps, streams={args.streams}, "
           f"fused={args.fused}, wgrad_overlap={args.wgrad_overlap})", flush=True)
     res.setdefault(args.wgrad_overlap, []).append((time.perf_counter() - t0) / args.steps * 1e3)
-if ab:
+if ab or plans or attr:
     for k, v in res.items():
         print(f"wgrad_overlap={k}: median {sorted(v)[len(v) // 2]:.3f} ms/step over {len(v)}", flush=True)

@@ -496,7 +496,7 @@ class NetFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, ctrl, *tensors):
-        plan, kind, train, dt, cache, nsrc, group, inputs = ctrl
+        plan, kind, train, dt, cache, nsrc, group, inputs, _ = ctrl
         sources = [t.contiguous().float() for t in tensors[:nsrc]]
         save = train and any(ctx.needs_input_grad[1:])
         ops.refresh_packs(cache)  # all operands packed since the last optimiser step, one launch
@@ -511,7 +511,7 @@ class NetFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        plan, kind, train, dt, cache, nsrc, _, _ = ctx.ctrl
+        plan, kind, train, dt, cache, nsrc, _, _, consumer = ctx.ctrl
         saved = ctx.saved_net
         if saved is None:
             raise RuntimeError("stcgan_amd: backward through a network called in eval mode is not supported")
@@ -532,6 +532,10 @@ class NetFn(torch.autograd.Function):
         out = [None]
         for i in range(nsrc):
             out.append(src_grads[i] if (src_grads is not None and need[i]) else None)
+            if consumer is not None and out[-1] is not None:
+                # a side-stream network's input gradient is read (and freed) on the consumer's stream: keep
+                # its block from being reused on this stream before the consumer is done with it
+                out[-1].record_stream(consumer)
         for j, p in enumerate(plan.params):
             out.append(grads.get(id(p)) if need[nsrc + j] else None)
         return tuple(out)

@@ -80,10 +80,13 @@ class _ObjectiveFn(torch.autograd.Function):
         ctx.args, ctx.wab = args, wab
         ctx.save_for_backward(*preds, *[t_ if t_ is not None else preds[0] for t_ in targets])
         ctx.mark_non_differentiable(vals)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the non-differentiable parts
         return total, vals
 
     @staticmethod
     def backward(ctx, gout, _gparts):
+        if gout is None:
+            return (None,) * 13
         preds = ctx.saved_tensors[:4]
         need = ctx.needs_input_grad[5:9]
         grads = [torch.empty_like(p_) if nd else None for p_, nd in zip(preds, need)]

@@ -60,6 +60,9 @@ class _HipNet(nn.Module):
         # dict reusing gathered inputs across this network's calls on the same tensors (set by the trainer
         # for one train step), or None
         self.input_cache = None
+        # stream that consumes this network's input gradients when it runs on a side stream (set by the
+        # trainer), or None
+        self.grad_consumer = None
 
     def set_compute_dtype(self, dtype):
         """'fp32' (default, parity path) or 'bf16' (bf16 operands, fp32 accumulation/BN/master weights)."""
@@ -78,7 +81,7 @@ class _HipNet(nn.Module):
             self._plan = self._make_plan()
         params = self._plan.params
         ctrl = (self._plan, self.kind, self.training, self.compute_dtype, self._pack_cache, len(sources),
-                self.weight_grad_group, self.input_cache)
+                self.weight_grad_group, self.input_cache, self.grad_consumer)
         return engine.NetFn.apply(ctrl, *sources, *params)
 
     def _apply(self, fn, *args, **kwargs):

@@ -104,11 +104,20 @@ def conv_query(kind, B, gh, gw, cin, cout, dt, out_f32=False, force=None):
     return ws.value, nch.value, tuple(po)
 
 
+# Tuning hooks (scripts/train_steps.py --ab-plans): per-shape plan overrides of the forward convs with
+# fused statistics, keyed (kind, B, gh, gw, cin, cout), and of the weight gradients, keyed
+# (B, Hd, Wd, R, Cg); values {tile config, splits}.  Empty in production.
+FORCE_CONV = {}
+FORCE_WGRAD = {}
+
+
 def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
     """Conv forward + fused BatchNorm partial statistics of its output (stc_conv_fwd_ex).
     Returns (part [chunks, cout, 4] fp32, chunks) for bn_finalize."""
     dev = w_packed.device
     gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
+    if force is None and FORCE_CONV:
+        force = FORCE_CONV.get((kind, B, gh, gw, cin, cout))
     nbytes, nch, plan = conv_query(kind, B, gh, gw, cin, cout, dt, force=force)
     ws, nb = _ws(nbytes, dev)
     part = torch.empty((nch, cout, 4), dtype=torch.float32, device=dev)
@@ -269,6 +278,8 @@ def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=Non
             timer.append(("wgrad_rows_kernel", True, 2.0 * B * Dv.H * Dv.W * R * 16 * Cg, e0, e1,
                           f"wgrad s1 P={B * Dv.H * Dv.W} R{R} (real {rows}) Cg{Cg}"))
         return dW
+    if force is None and FORCE_WGRAD:
+        force = FORCE_WGRAD.get((B, Dv.H, Dv.W, R, Cg))
     nbytes, plan = wgrad_query(B, Dv.H, Dv.W, R, Cg, dt, force)
     ws, nb = _ws(nbytes, device)
     dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)

@@ -96,6 +96,8 @@ class STCGAN(object):
         self.sync_D.enable_overlap()
         # discriminators on side HIP streams (train_step / _lanes); off for a strictly serial step
         self.streams = bool(getattr(args, "streams", True))
+        self.lane_carry = bool(getattr(args, "lane_carry", True))
+        self._lane_inputs = None
         # loss type "normal": the D and G objectives as one fused node each (loss.d_objective / g_objective)
         self.fused_objectives = bool(getattr(args, "fused_objectives", True))
         self._side = None
@@ -225,9 +227,18 @@ class STCGAN(object):
         self.optim_D.zero_grad()
         self.optim_G.zero_grad()
         main, l1, l2 = self._lanes()
-        if l1 is not None:  # side lanes start after everything queued so far (last optimizer step)
-            l1.wait_stream(main)
-            l2.wait_stream(main)
+        if l1 is not None:
+            # The side lanes start with the discriminators' real-input forwards, which need the D weights of
+            # the last D update (the lanes waited for it before the previous G step) and the inputs.  With the
+            # inputs of the previous step (same tensors, unmodified) they need nothing else from the main
+            # stream and overlap its G backward and G update; new inputs were produced on the main stream.
+            # Lane-allocated tensors read on the main stream are record_stream'ed (outputs, input gradients).
+            key = tuple((id(t), t._version, t.data_ptr()) for t in (x, m, y))
+            if not (self.lane_carry and key == self._lane_inputs):
+                l1.wait_stream(main)
+                l2.wait_stream(main)
+            self._lane_inputs = key
+            self.D1.grad_consumer = self.D2.grad_consumer = main
         # each discriminator sees the same real and fake inputs in the D and the G step: gather them once
         self.D1.input_cache, self.D2.input_cache = {}, {}
         try:

@@ -1,0 +1,44 @@
+"""The side-stream schedule (discriminators on their own streams, the weight-gradient lane, the lanes
+carrying over into the next step's real-input forwards when the inputs repeat) computes exactly what the
+one-stream schedule computes: every parameter, BN buffer and loss bit-identical after several steps."""
+import types
+
+import pytest
+import torch
+
+from stcgan_amd import engine
+from stcgan_amd.stcgan import STCGAN
+
+pytestmark = pytest.mark.gpu
+NETS = ("G1", "G2", "D1", "D2")
+
+
+def _run(streams, carry, overlap, loss_type, nsteps=3):
+    torch.manual_seed(3)
+    a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5, beta2=0.999,
+                              D_loss_fn="standard", D_loss_type=loss_type, ngf=16, dtype="bf16",
+                              load_weights_g1=None, load_weights_g2=None, load_weights_d1=None,
+                              load_weights_d2=None, streams=streams, lane_carry=carry)
+    prev = engine.WGRAD_OVERLAP
+    engine.WGRAD_OVERLAP = overlap
+    try:
+        tr = STCGAN(a)
+        g = torch.Generator().manual_seed(9)
+        x, m, y = (torch.rand((4, c, 256, 256), generator=g).cuda() * 2 - 1 for c in (3, 1, 3))
+        losses = [tr.train_step(x, m, y) for _ in range(nsteps)]
+        torch.cuda.synchronize()
+    finally:
+        engine.WGRAD_OVERLAP = prev
+    state = {n: {k: v.cpu() for k, v in getattr(tr, n).state_dict().items()} for n in NETS}
+    return state, [{k: float(v) for k, v in d.items()} for d in losses]
+
+
+@pytest.mark.parametrize("loss_type", ["normal", "rel_avg"])
+def test_stream_schedules_bit_identical(loss_type):
+    ref_state, ref_losses = _run(False, False, False, loss_type)
+    for streams, carry, overlap in ((True, False, False), (True, True, True)):
+        state, losses = _run(streams, carry, overlap, loss_type)
+        assert losses == ref_losses, (streams, carry, overlap)
+        for n in NETS:
+            for k, v in ref_state[n].items():
+                assert torch.equal(state[n][k], v), (streams, carry, overlap, n, k)
