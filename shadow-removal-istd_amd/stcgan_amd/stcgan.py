@@ -219,7 +219,7 @@ class STCGAN(object):
         out.record_stream(torch.cuda.current_stream(self.device))
         return out
 
-    def train_step(self, x, m, y, training=True, acc=None):
+    def train_step(self, x, m, y, training=True, acc=None, inputs_ready=None):
         """One iteration of STCGAN.run_epoch (STCGAN/stcgan.py:208-312): D step then G step.
         Returns the on-device loss scalars (no host sync).  The call order of every network
         (and so every BN running-statistics update) is the reference's; with ``streams`` the
@@ -227,14 +227,25 @@ class STCGAN(object):
         self.optim_D.zero_grad()
         self.optim_G.zero_grad()
         main, l1, l2 = self._lanes()
+        if l1 is None and inputs_ready is not None:
+            main.wait_event(inputs_ready)
         if l1 is not None:
             # The side lanes start with the discriminators' real-input forwards, which need the D weights of
             # the last D update (the lanes waited for it before the previous G step) and the inputs.  With the
             # inputs of the previous step (same tensors, unmodified) they need nothing else from the main
             # stream and overlap its G backward and G update; new inputs were produced on the main stream.
             # Lane-allocated tensors read on the main stream are record_stream'ed (outputs, input gradients).
+            # inputs_ready: an event after which x, m, y are complete (produced on another stream, not read
+            # by anything but this step), e.g. run_epoch's input stream
             key = tuple((id(t), t._version, t.data_ptr()) for t in (x, m, y))
-            if not (self.lane_carry and key == self._lane_inputs):
+            if inputs_ready is not None:
+                for t in (x, m, y):
+                    t.record_stream(main)
+                main.wait_event(inputs_ready)
+            if inputs_ready is not None and self.lane_carry:
+                l1.wait_event(inputs_ready)
+                l2.wait_event(inputs_ready)
+            elif not (self.lane_carry and key == self._lane_inputs):
                 l1.wait_stream(main)
                 l2.wait_stream(main)
             self._lane_inputs = key
@@ -327,11 +338,28 @@ class STCGAN(object):
         acc = {k: torch.zeros((), device=self.device) for k in keys + ["D1_real", "D1_fake", "D2_real", "D2_fake"]}
         data_loader = self.train_loader if training else self.valid_loader
         n_batches = 0
-        for (_, x, m, y) in data_loader:
-            x = x.to(self.device, non_blocking=True)
-            m = m.to(self.device, non_blocking=True)
-            y = y.to(self.device, non_blocking=True)
-            self.train_step(x, m, y, training=training, acc=acc)
+        # with the side lanes, batches are prepared on an input stream and handed over with an event, so the
+        # lanes wait for the batch only (not for the main stream's G backward and update of the last step)
+        lanes = self._lanes()[1] is not None
+        if lanes and getattr(self, "_in_stream", None) is None:
+            self._in_stream = torch.cuda.Stream(self.device)
+        it = iter(data_loader)
+        while True:
+            if lanes:
+                with torch.cuda.stream(self._in_stream):
+                    b = next(it, None)
+                    if b is not None:
+                        b = [t.to(self.device, non_blocking=True) for t in b[1:]]
+                    ready = self._in_stream.record_event()
+            else:
+                b = next(it, None)
+                if b is not None:
+                    b = [t.to(self.device, non_blocking=True) for t in b[1:]]
+                ready = None
+            if b is None:
+                break
+            x, m, y = b
+            self.train_step(x, m, y, training=training, acc=acc, inputs_ready=ready)
             n_batches += 1
         # global-batch values on every rank (DataParallel computes the losses on the gathered
         # batch), so each rank's ReduceLROnPlateau sees the same sums: one collective, one host sync

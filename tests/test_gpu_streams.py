@@ -42,3 +42,28 @@ def test_stream_schedules_bit_identical(loss_type):
         for n in NETS:
             for k, v in ref_state[n].items():
                 assert torch.equal(state[n][k], v), (streams, carry, overlap, n, k)
+
+
+def test_run_epoch_input_stream_bit_identical():
+    """run_epoch over changing batches: with the lanes, batches come through the input stream and its
+    event (the lanes do not wait for the previous step's main-stream work); the result equals the
+    one-stream epoch bit for bit."""
+    def epoch(streams):
+        torch.manual_seed(4)
+        a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5,
+                                  beta2=0.999, D_loss_fn="standard", D_loss_type="normal", ngf=16, dtype="bf16",
+                                  load_weights_g1=None, load_weights_g2=None, load_weights_d1=None,
+                                  load_weights_d2=None, streams=streams)
+        g = torch.Generator().manual_seed(11)
+        batches = [([], *(torch.rand((2, c, 256, 256), generator=g) * 2 - 1 for c in (3, 1, 3))) for _ in range(3)]
+        tr = STCGAN(a, train_loader=batches, valid_loader=batches[:1])
+        out = tr.run_epoch(training=True)
+        torch.cuda.synchronize()
+        return out, {n: {k: v.cpu() for k, v in getattr(tr, n).state_dict().items()} for n in NETS}
+
+    ref_out, ref_state = epoch(False)
+    out, state = epoch(True)
+    assert out == ref_out
+    for n in NETS:
+        for k, v in ref_state[n].items():
+            assert torch.equal(state[n][k], v), (n, k)
