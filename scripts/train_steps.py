@@ -84,7 +84,8 @@ for rep in range(args.repeat):
     for _ in range(args.steps):
         tr.train_step(x, m, y)
     torch.cuda.synchronize()
-    print(f"{(time.perf_counter() - t0) / args.steps * 1e3:.3f} ms/step ({args.steps} steps, streams={args.streams}, "
+    print(f"{(time.perf_counter() - t0) / args.steps * 1e3:.3f} ms/step  mem {torch.cuda.memory_allocated() / 2**30:.2f} GiB "
+          f"reserved {torch.cuda.memory_reserved() / 2**30:.2f} GiB ({args.steps} steps, streams={args.streams}, "
           f"fused={args.fused}, wgrad_overlap={args.wgrad_overlap})", flush=True)
     res.setdefault(args.wgrad_overlap, []).append((time.perf_counter() - t0) / args.steps * 1e3)
 if ab or plans or attr:

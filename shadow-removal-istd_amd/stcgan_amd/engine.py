@@ -69,6 +69,19 @@ class _WgradLane:
             self.cur.wait_stream(self.side)
 
 
+_ONES = {}
+
+
+def _ones_plane(B, H, W, dev):
+    """A persistent [B, 1, H, W] fp32 plane of ones (filled once, synchronously: streams share it)."""
+    key = (B, H, W, str(dev))
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.ones((B, 1, H, W), dtype=torch.float32, device=dev)
+        torch.cuda.current_stream(dev).synchronize()
+    return t
+
+
 def _nhwc(B, H, W, C, dt, dev, zero=False):
     f = torch.zeros if zero else torch.empty
     return f((B, H, W, C), dtype=dt, device=dev)
@@ -334,13 +347,18 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None):
     cin = sum(s.shape[1] for s in sources)
     assert cin == plan.in_c, f"discriminator expects {plan.in_c} input channels, got {cin}"
     cin_pad = ops.pad_channels(cin, dt)
+    # first-layer bias gradient for free: a constant-1 plane in the first padding channel (its packed weights
+    # are zero) makes the weight gradient's tap (1,1) of that channel sum the output gradient over every pixel
+    # (k4 s2 p1: input row 2*o + kh - 1 = 2*o is always inside), replacing a full pass over that gradient
+    bias_ch = cin if (plan.convs[0].bias is not None and cin < cin_pad and len(sources) < 4
+                      and plan.strides[0] == 2) else None
     key = None
     if inputs is not None:
         key = tuple((s.data_ptr(), s._version, tuple(s.shape)) for s in sources) + (dt, cin_pad)
     xin = inputs.get(key) if key is not None else None
     if xin is None:
         xin = _nhwc(B, H, W, cin_pad, dt, dev)
-        ops.gather(sources, xin, dt)
+        ops.gather(list(sources) + ([_ones_plane(B, H, W, dev)] if bias_ch is not None else []), xin, dt)
         if key is not None:
             inputs[key] = xin
     n = plan.n
@@ -379,6 +397,7 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None):
     saved = None
     if save:
         saved = dict(raw=raw, act=act, dims=dims, chans=chans, tabs=tabs, stats=stats, cin=cin, cin_pad=cin_pad,
+                     bias_ch=bias_ch,
                      src_c=[s.shape[1] for s in sources])
     return out, saved
 
@@ -405,8 +424,12 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
         gv = L.nhwc_view(g, 0, h, w)  # gradient wrt conv_i output (pre-activation / pre-BN), gch channels
         if need_w:
             def wg(i=i, s=s, cout=cout, gv=gv, gch=gch, cv=cv):
-                dW = ops.wgrad(B, s, gv, gch, L.nhwc_view(act[i]), chans[i], saved["cin"] if i == 0 else chans[i],
-                               dt, device=dev, rows=cout)
+                bc = saved["bias_ch"] if i == 0 else None
+                dW = ops.wgrad(B, s, gv, gch, L.nhwc_view(act[i]), chans[i],
+                               (saved["cin"] if bc is None else bc + 1) if i == 0 else chans[i], dt, device=dev,
+                               rows=cout)
+                if bc is not None:  # the constant-1 channel's tap (1,1) is the bias gradient (disc_forward)
+                    return dW[:, :saved["cin"]].contiguous(), dW[:cout, bc, 1, 1].contiguous()
                 db = ops.chan_sum(B, gv, gch, cout, dt, dev) if cv.bias is not None else None
                 return dW, db
             dW, dbias = lane.run(wg, g, pixels=h * w)
