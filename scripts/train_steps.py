@@ -20,6 +20,7 @@ ap.add_argument("--warmup", type=int, default=2)
 ap.add_argument("--dtype", default="bf16")
 ap.add_argument("--streams", type=int, default=1)
 ap.add_argument("--fused", type=int, default=1)
+ap.add_argument("--host-sleep-us", type=int, default=0, help="extra host time per step (host-boundness probe)")
 ap.add_argument("--repeat", type=int, default=1)
 ap.add_argument("--wgrad-overlap", type=int, default=1)
 ap.add_argument("--ab", default="", help="comma list of wgrad-overlap settings cycled per repeat (same process)")
@@ -36,6 +37,15 @@ a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2
                           streams=bool(args.streams), fused_objectives=bool(args.fused))
 torch.manual_seed(1234)
 tr = STCGAN(a)
+if args.host_sleep_us:
+    _ts = tr.train_step
+
+    def _slow(*aa, **kk):
+        t_end = time.perf_counter() + args.host_sleep_us * 1e-6
+        while time.perf_counter() < t_end:
+            pass
+        return _ts(*aa, **kk)
+    tr.train_step = _slow
 dev = torch.device("cuda", 0)
 B = 32
 x = torch.rand((B, 3, 256, 256), device=dev) * 2 - 1
