@@ -337,7 +337,7 @@ def _conv_out(h, s):
     return (h + 2 - 4) // s + 1
 
 
-def disc_forward(plan, sources, train, dt, cache, save, inputs=None):
+def disc_forward(plan, sources, train, dt, cache, save, inputs=None, stats_only=False):
     """raw[i] = conv_{i-1} raw output (raw[0] = padded input); act[i] = input of conv_i.
     inputs: optional dict reusing the gathered NHWC input across calls on the same source tensors
     (the trainer's real/fake pairs are fed to each discriminator twice per step, STCGAN/stcgan.py:215-280;
@@ -374,8 +374,9 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None):
         kind = L.CONV_S2 if s == 2 else L.CONV_S1
         if i == n - 1:
             out = torch.empty((B, cout, h, w), dtype=torch.float32, device=dev)
-            ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nchw_view(out), dt, bias=cv.bias,
-                     out_f32=True)
+            if not stats_only:
+                ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nchw_view(out), dt, bias=cv.bias,
+                         out_f32=True)
             break
         o = _nhwc(B, h, w, cout, dt, dev)
         tab, st = None, None
@@ -387,7 +388,8 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None):
         else:
             ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(o), dt, bias=cv.bias)
         a = _nhwc(B, h, w, cout, dt, dev)
-        ops.bn_apply(B, L.nhwc_view(o), cout, dt, tab, L.nhwc_view(a), LRELU)
+        if not (stats_only and i == n - 2):  # (stats_only: only the logits layer reads this activation)
+            ops.bn_apply(B, L.nhwc_view(o), cout, dt, tab, L.nhwc_view(a), LRELU)
         raw.append(o)
         act.append(a)
         dims.append((h, w))
@@ -519,12 +521,12 @@ class NetFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, ctrl, *tensors):
-        plan, kind, train, dt, cache, nsrc, group, inputs, _ = ctrl
+        plan, kind, train, dt, cache, nsrc, group, inputs, _, stats_only = ctrl
         sources = [t.contiguous().float() for t in tensors[:nsrc]]
         save = train and any(ctx.needs_input_grad[1:])
         ops.refresh_packs(cache)  # all operands packed since the last optimiser step, one launch
         out, saved = (gen_forward(plan, sources, train, dt, cache, save) if kind == "G" else
-                      disc_forward(plan, sources, train, dt, cache, save, inputs))
+                      disc_forward(plan, sources, train, dt, cache, save, inputs, stats_only and not save))
         ctx.ctrl = ctrl
         ctx.saved_net = saved
         ctx.group = group if (save and any(ctx.needs_input_grad[1 + nsrc:])) else None
@@ -534,7 +536,7 @@ class NetFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
-        plan, kind, train, dt, cache, nsrc, _, _, consumer = ctx.ctrl
+        plan, kind, train, dt, cache, nsrc, _, _, consumer, _ = ctx.ctrl
         saved = ctx.saved_net
         if saved is None:
             raise RuntimeError("stcgan_amd: backward through a network called in eval mode is not supported")

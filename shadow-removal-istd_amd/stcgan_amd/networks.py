@@ -63,6 +63,10 @@ class _HipNet(nn.Module):
         # stream that consumes this network's input gradients when it runs on a side stream (set by the
         # trainer), or None
         self.grad_consumer = None
+        # a call whose output is not used but whose BatchNorm running statistics must advance (the trainer's
+        # G-step real-input discriminator calls with loss type "normal"): the layers after the last
+        # BatchNorm are skipped and the output is left unwritten
+        self.stats_only = False
 
     def set_compute_dtype(self, dtype):
         """'fp32' (default, parity path) or 'bf16' (bf16 operands, fp32 accumulation/BN/master weights)."""
@@ -81,7 +85,7 @@ class _HipNet(nn.Module):
             self._plan = self._make_plan()
         params = self._plan.params
         ctrl = (self._plan, self.kind, self.training, self.compute_dtype, self._pack_cache, len(sources),
-                self.weight_grad_group, self.input_cache, self.grad_consumer)
+                self.weight_grad_group, self.input_cache, self.grad_consumer, self.stats_only)
         return engine.NetFn.apply(ctrl, *sources, *params)
 
     def _apply(self, fn, *args, **kwargs):

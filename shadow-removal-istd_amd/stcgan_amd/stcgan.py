@@ -296,9 +296,15 @@ class STCGAN(object):
                 if l1 is not None:  # after optim_D.step
                     l1.wait_stream(main)
                     l2.wait_stream(main)
+                # loss type "normal": the G objective does not read C_real; the calls still run (the reference
+                # makes them, STCGAN/stcgan.py:269-272) for their BatchNorm running statistics, minus the
+                # logits layer (engine: stats_only)
+                unused = self.d_loss_type == "normal"
+                self.D1.stats_only = self.D2.stats_only = unused
                 C1_real = self._on(l1, self.D1, [x, m])
-                C1_fake = self._on(l1, self.D1, [x, m_pred])
                 C2_real = self._on(l2, self.D2, [x, m, y])
+                self.D1.stats_only = self.D2.stats_only = False
+                C1_fake = self._on(l1, self.D1, [x, m_pred])
                 C2_fake = self._on(l2, self.D2, [x, m_pred, y_pred])
                 if l1 is not None:
                     main.wait_stream(l1)
