@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--ngf", type=int, default=64)
     ap.add_argument("--dtype", default=os.environ.get("STC_BENCH_DTYPE", "bf16"), choices=["fp32", "bf16"])
+    ap.add_argument("--no-graph", action="store_true", help="eager steps (default: the step captured as one HIP "
+                    "graph and replayed, STCGAN.capture; the same kernels, bit-identical results)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the parity / other-config measurements")
     ap.add_argument("--cpu-batch", type=int, default=32, help="batch of the timed CPU train step (C3: 32)")
@@ -372,15 +374,22 @@ def main():
     for net in (tr.G1, tr.G2, tr.D1, tr.D2):
         net.train()
 
+    step, mode = (lambda: tr.train_step(x, m, y)), "eager"
+    if not args.no_graph:
+        try:  # (a capture failure, e.g. a backend that cannot be captured, falls back to eager steps)
+            step, mode = tr.capture(x, m, y, warmup=1), "hip-graph"
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: graph capture failed ({type(e).__name__}: {e}); eager steps", file=sys.stderr)
+            torch.cuda.synchronize()
     for _ in range(args.warmup):
-        tr.train_step(x, m, y)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        tr.train_step(x, m, y)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -416,7 +425,7 @@ def main():
                "data": "synthetic (x,y~U(-1,1), m=+-1; reference weights_init)",
                "config": {"workload": "full ST-CGAN train step (G1,G2,D1,D2 fwd/bwd + MSE-cGAN/L1 + Adam), "
                                       f"{s}x{s}", "global_batch": B * world, "per_gpu_batch": B,
-                          "image_size": s, "ngf": args.ngf, "parallelism": f"dp{world}"},
+                          "image_size": s, "ngf": args.ngf, "parallelism": f"dp{world}", "step_launch": mode},
                "roofline": roofline, "cpu_baseline": cpu, **extras}
         print(json.dumps(out), flush=True)
     if world > 1:

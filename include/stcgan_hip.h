@@ -372,6 +372,15 @@ int stc_adam_elems_per_block(void);
  * would (padding entries are left as they are).  Same Adam arithmetic as stc_adam_step.           */
 int stc_adam_pack_step(const int64_t* table, int ntensors, int64_t total_blocks,
                        float lr, float beta1, float beta2, float eps, int step, void* stream);
+/* stc_adam_pack_step with the step count on the device, for a train step captured as a HIP graph and
+ * replayed (torch.optim.Adam's host-side step count would be frozen into the graph): one thread
+ * advances *step_dev and forms lr/(1 - beta1^step) (double, then float) and sqrt(1 - beta2^step)
+ * from bc1_tab[s] = 1 - beta1^s (double) and bc2s_tab[s] = (float)sqrt(1 - beta2^s), tables of tab_len
+ * entries the caller fills with the host formulas, and *lr_dev (the double value of the float lr);
+ * coef_dev: 2 floats of scratch.  Bit-identical to stc_adam_pack_step at the same step.            */
+int stc_adam_pack_step_dev(const int64_t* table, int ntensors, int64_t total_blocks, int64_t* step_dev,
+                           const double* lr_dev, const double* bc1_tab, const float* bc2s_tab, int tab_len,
+                           float* coef_dev, float beta1, float beta2, float eps, void* stream);
 /* dst[e] += src[e] (fp32, numel[e] elements) for ntensors <= 16 tensors in one launch (host arrays of
  * device pointers).  Sums the weight gradients of two calls of one network inside one differentiated
  * graph -- the discriminators' real and fake calls, STCGAN/stcgan.py:215-227 -- which autograd would

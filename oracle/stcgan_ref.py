@@ -30,6 +30,63 @@ BN_MOMENTUM = 0.1   # nn.BatchNorm2d default
 LRELU = 0.2         # STCGAN/networks.py:102,158
 
 
+# --------------------------------------------------------------------------- bf16 mode
+class _RoundFwd(torch.autograd.Function):
+    """Value rounded to bf16 (round-to-nearest-even), gradient passed through unchanged."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGrad(torch.autograd.Function):
+    """Value unchanged, gradient rounded to bf16."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+class Precision:
+    """Where a computation keeps bf16 copies.  ``Precision(bf16=True)`` restates the HIP bf16 mode
+    (the BASELINE C3/C4 configuration), which keeps the reference's algorithm and changes only storage:
+      * conv / convT operands are bf16 (weights rounded from the fp32 masters, activations as stored),
+        products accumulated in fp32;
+      * every activation tensor between layers is stored in bf16 -- the gathered network input, each raw
+        conv/convT output, each post-activation tensor (LeakyReLU conv input, ReLU skip half, ReLU up half);
+      * every gradient tensor between layers is stored in bf16 -- the gradient w.r.t. each raw conv/convT
+        output (after the fused activation + BatchNorm backward), w.r.t. each post-activation tensor (the
+        input-gradient GEMM outputs) and w.r.t. the network inputs;
+      * BatchNorm batch statistics come from the fp32 conv results (the GEMM epilogue's accumulators) and
+        normalise the stored bf16 values; the running statistics, the weight gradients (fp32 accumulation
+        of bf16 products), the network outputs (tanh / logits), losses and Adam stay fp32.
+    ``FP32`` (the default) is the reference itself."""
+
+    def __init__(self, bf16=False):
+        self.bf16 = bf16
+
+    def fq(self, x):
+        return _RoundFwd.apply(x) if self.bf16 else x
+
+    def gq(self, x):
+        return _RoundGrad.apply(x) if self.bf16 else x
+
+    def fgq(self, x):
+        return _RoundGrad.apply(_RoundFwd.apply(x)) if self.bf16 else x
+
+
+FP32 = Precision(False)
+BF16 = Precision(True)
+
+
 # --------------------------------------------------------------------------- keys
 def gen_block_prefix(level):
     """Prefix of the UnetSkipConnectionBlock at ``level`` (0 = outermost)."""
@@ -149,17 +206,76 @@ def _gen_block(st, x, level, num_downs, train):
     return torch.cat([skip, u], 1)
 
 
-def generator_forward(st, x, train=True, num_downs=8):
+def _batch_norm_q(st, prefix, r, train, prec):
+    """BatchNorm2d of a conv result r as the bf16 mode computes it: statistics (and the running update)
+    from the fp32 result, normalisation of its stored bf16 copy."""
+    w, b = st[prefix + "weight"], st[prefix + "bias"]
+    rm, rv = st[prefix + "running_mean"], st[prefix + "running_var"]
+    rs = prec.fq(r)
+    if train:
+        n = r.numel() // r.shape[1]
+        mean = r.mean(dim=(0, 2, 3))
+        var = r.var(dim=(0, 2, 3), unbiased=False)
+        with torch.no_grad():
+            rm.mul_(1 - BN_MOMENTUM).add_(mean.detach() * BN_MOMENTUM)
+            rv.mul_(1 - BN_MOMENTUM).add_(var.detach() * (n / max(n - 1, 1)) * BN_MOMENTUM)
+            st[prefix + "num_batches_tracked"].add_(1)
+        xhat = (rs - mean[None, :, None, None]) * torch.rsqrt(var + BN_EPS)[None, :, None, None]
+    else:
+        xhat = (rs - rm[None, :, None, None]) * torch.rsqrt(rv + BN_EPS)[None, :, None, None]
+    return xhat * w[None, :, None, None] + b[None, :, None, None]
+
+
+def _gen_block_q(st, n, level, num_downs, train, prec):
+    """_gen_block in the bf16 mode: returns the parent ConvT's input as stored,
+    [ReLU(n) | ReLU(BN_up(convT_level(...)))] (ReLU(LeakyReLU(v)) = ReLU(v))."""
+    p = gen_block_prefix(level)
+    h, w = n.shape[2], n.shape[3]
+    odd = (h % 2) or (w % 2)
+    nin = F.pad(n, (0, w % 2, 0, h % 2)) if odd else n
+    a = prec.fgq(F.leaky_relu(nin, LRELU))   # conv_level input (the in-place LeakyReLU, networks.py:106)
+    skip = prec.fgq(F.relu(n))               # skip half of the parent's ConvT input
+    r = prec.gq(F.conv2d(a, prec.fq(st[p + "1.weight"]), None, 2, 1))
+    if level == num_downs - 1:  # innermost: no down-norm (STCGAN/networks.py:118-124)
+        c = prec.fgq(F.relu(prec.fq(r)))
+        rq = prec.gq(F.conv_transpose2d(c, prec.fq(st[p + "3.weight"]), None, 2, 1))
+        u = _batch_norm_q(st, p + "4.", rq, train, prec)
+    else:
+        d = _batch_norm_q(st, p + "2.", r, train, prec)
+        c = _gen_block_q(st, d, level + 1, num_downs, train, prec)
+        rq = prec.gq(F.conv_transpose2d(c, prec.fq(st[p + "5.weight"]), None, 2, 1))
+        u = _batch_norm_q(st, p + "6.", rq, train, prec)
+    if odd:
+        u = u[:, :, :h, :w]
+    return torch.cat([skip, prec.fgq(F.relu(u))], 1)
+
+
+def generator_forward(st, x, train=True, num_downs=8, prec=FP32):
     """UnetGenerator.forward (STCGAN/networks.py:74-76, outermost block :111-117)."""
     p = gen_block_prefix(0)
+    if prec.bf16:
+        r = prec.gq(F.conv2d(prec.fgq(x), prec.fq(st[p + "0.weight"]), None, 2, 1))
+        c = _gen_block_q(st, prec.fq(r), 1, num_downs, train, prec)
+        z = prec.gq(F.conv_transpose2d(c, prec.fq(st[p + "3.weight"]), None, 2, 1))
+        return torch.tanh(z + st[p + "3.bias"][None, :, None, None])
     h = F.conv2d(x, st[p + "0.weight"], None, 2, 1)
     c = _gen_block(st, h, 1, num_downs, train)
     y = F.conv_transpose2d(F.relu(c), st[p + "3.weight"], st[p + "3.bias"], 2, 1)
     return torch.tanh(y)
 
 
-def discriminator_forward(st, x, train=True, n_layers=3):
+def discriminator_forward(st, x, train=True, n_layers=3, prec=FP32):
     """NLayerDiscriminator.forward (STCGAN/networks.py:147-192), use_sigmoid=False."""
+    if prec.bf16:
+        o = prec.gq(F.conv2d(prec.fgq(x), prec.fq(st["model.0.weight"]), st["model.0.bias"], 2, 1))
+        h = prec.fgq(F.leaky_relu(prec.fq(o), LRELU))
+        idx = 2
+        for n in range(1, n_layers + 1):
+            stride = 2 if n < n_layers else 1
+            r = prec.gq(F.conv2d(h, prec.fq(st[f"model.{idx}.weight"]), None, stride, 1))
+            h = prec.fgq(F.leaky_relu(_batch_norm_q(st, f"model.{idx + 1}.", r, train, prec), LRELU))
+            idx += 3
+        return prec.gq(F.conv2d(h, prec.fq(st[f"model.{idx}.weight"]), st[f"model.{idx}.bias"], 1, 1))
     h = F.leaky_relu(F.conv2d(x, st["model.0.weight"], st["model.0.bias"], 2, 1), LRELU)
     idx = 2
     for n in range(1, n_layers + 1):
@@ -232,7 +348,14 @@ class Adam:
 class OracleSTCGAN:
     """Functional restatement of STCGAN.run_epoch (STCGAN/stcgan.py:186-330)."""
 
-    def __init__(self, states, lr_G=5e-5, lr_D=2e-5, betas=(0.5, 0.999), loss_type="normal", ls=False):
+    def __init__(self, states, lr_G=5e-5, lr_D=2e-5, betas=(0.5, 0.999), loss_type="normal", ls=False, prec=FP32,
+                 shards=1):
+        self.prec = prec
+        # shards > 1: the reference's nn.DataParallel over that many devices (STCGAN/stcgan.py:53-59): every
+        # network call scatters the batch on dim 0, each replica normalises its own shard (per-shard
+        # BatchNorm), only device 0's replica keeps its running-statistics update, and the outputs are
+        # gathered, so the losses see the whole batch
+        self.shards = shards
         self.st = states  # {"G1":…, "G2":…, "D1":…, "D2":…}; float tensors are leaf params
         for s in self.st.values():
             for k, v in s.items():
@@ -247,11 +370,22 @@ class OracleSTCGAN:
     def _params(self, name):
         return [v for k, v in self.st[name].items() if v.is_floating_point() and not _is_buffer(k)]
 
+    def _replicas(self, name, x, fwd, train):
+        if self.shards == 1:
+            return fwd(self.st[name], x, train, prec=self.prec)
+        outs = []
+        for i, xs in enumerate(torch.chunk(x, self.shards, dim=0)):
+            st = self.st[name]
+            if i > 0:  # replica on device i: shared parameters, its own (discarded) copy of the buffers
+                st = {k: (v.clone() if _is_buffer(k) else v) for k, v in st.items()}
+            outs.append(fwd(st, xs, train, prec=self.prec))
+        return torch.cat(outs, 0)
+
     def G(self, name, x, train):
-        return generator_forward(self.st[name], x, train)
+        return self._replicas(name, x, generator_forward, train)
 
     def D(self, name, x, train):
-        return discriminator_forward(self.st[name], x, train)
+        return self._replicas(name, x, discriminator_forward, train)
 
     def adv(self, out, is_real):
         return adversarial_loss(out, is_real, self.ls)

@@ -42,8 +42,6 @@ dev = torch.device("cuda", 0)
 x = torch.rand((32, 3, 256, 256), device=dev) * 2 - 1
 m = (torch.rand((32, 1, 256, 256), device=dev) < 0.5).float() * 2 - 1
 y = torch.rand((32, 3, 256, 256), device=dev) * 2 - 1
-wrap(tr, "sync_G", "sync")
-wrap(tr, "sync_D", "sync")
 for _ in range(3):
     tr.train_step(x, m, y)
 torch.cuda.synchronize()

@@ -69,8 +69,13 @@ __device__ __forceinline__ float adam_elem(float pi, float gi, float& mi, float&
 }
 
 __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, int ntensors, float lr_over_bc1,
-                                                        float bc2_sqrt, float beta1, float beta2, float eps) {
+                                                        float bc2_sqrt, float beta1, float beta2, float eps,
+                                                        const float* __restrict__ coef) {
   __shared__ __attribute__((aligned(16))) float tile[16][16][20];  // [p][tap][q] (rows of 20: 16-byte aligned q quads)
+  if (coef != nullptr) {  // device-resident step (graph replay): the coefficients adam_coef_kernel computed
+    lr_over_bc1 = coef[0];
+    bc2_sqrt = coef[1];
+  }
   int lo = 0, hi = ntensors - 1;
   const int blk = blockIdx.x;
   while (lo < hi) {
@@ -193,6 +198,22 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, 
   }
 }
 
+// ---- device-resident step count (a captured train step replays with the count advancing on the GPU):
+// one thread advances the group's step and turns it into the two Adam coefficients exactly as the host
+// path does -- lr / (1 - beta1^step) in double, rounded to float, and the float sqrt(1 - beta2^step) --
+// from tables of 1 - beta1^s (double) and sqrt(1 - beta2^s) (float) the host filled with the same
+// libm formulas (bit-identical to stc_adam_pack_step at every step).
+__global__ void adam_coef_kernel(long long* __restrict__ step, const double* __restrict__ lr,
+                                 const double* __restrict__ bc1_tab, const float* __restrict__ bc2s_tab, int tab_len,
+                                 float* __restrict__ coef) {
+  if (threadIdx.x != 0) return;
+  const long long s = step[0] + 1;
+  step[0] = s;
+  const int i = (int)(s < tab_len ? s : tab_len - 1);
+  coef[0] = (float)(lr[0] / bc1_tab[i]);
+  coef[1] = bc2s_tab[i];
+}
+
 // ---- multi-tensor gradient accumulation: dst[e] += src[e] for up to GA_MAX tensors in one launch.
 // Replaces the per-parameter ATen adds autograd issues when a network is called twice in one
 // differentiated graph (the discriminators' real + fake calls, STCGAN/stcgan.py:215-227).
@@ -246,7 +267,23 @@ extern "C" int stc_adam_pack_step(const int64_t* table, int ntensors, int64_t to
   const double bc1 = 1.0 - pow((double)beta1, (double)step);
   const double bc2 = 1.0 - pow((double)beta2, (double)step);
   hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
-                     (const long long*)table, ntensors, (float)((double)lr / bc1), (float)sqrt(bc2), beta1, beta2, eps);
+                     (const long long*)table, ntensors, (float)((double)lr / bc1), (float)sqrt(bc2), beta1, beta2, eps,
+                     (const float*)nullptr);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stc_adam_pack_step_dev(const int64_t* table, int ntensors, int64_t total_blocks, int64_t* step_dev,
+                                      const double* lr_dev, const double* bc1_tab, const float* bc2s_tab, int tab_len,
+                                      float* coef_dev, float beta1, float beta2, float eps, void* stream) {
+  STC_REQUIRE(ntensors > 0 && step_dev && lr_dev && bc1_tab && bc2s_tab && coef_dev && tab_len >= 2,
+              "stc_adam_pack_step_dev: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_coef_kernel, dim3(1), dim3(64), 0, st, (long long*)step_dev, lr_dev, bc1_tab, bc2s_tab,
+                     tab_len, coef_dev);
+  STC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)total_blocks), dim3(256), 0, st, (const long long*)table,
+                     ntensors, 0.f, 1.f, beta1, beta2, eps, (const float*)coef_dev);
   STC_CHECK_LAUNCH();
   return 0;
 }

@@ -391,9 +391,14 @@ namespace stc {
 // One non-packed v_fma_f32.  The compiler otherwise pairs these accumulations into v_pk_fma_f32 with
 // op_sel; in that form the kernel returned sporadically different low-half sums (one (tap, even
 // channel) accumulator of a whole wave) when two processes shared the GPU (tests/test_gpu_dist.py).
+// STC_ROWS_PACKED: diagnostic build only (scripts/rows_stress.py) -- the compiler's packed form.
 __device__ __forceinline__ float fma_scalar(float a, float b, float c) {
+#ifdef STC_ROWS_PACKED
+  return __builtin_fmaf(a, b, c);
+#else
   asm("v_fma_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
   return c;
+#endif
 }
 
 template <typename T, int RO>

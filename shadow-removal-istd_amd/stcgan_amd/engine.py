@@ -31,6 +31,22 @@ from .ops import LRELU
 
 
 
+# ----------------------------------------------------------------------------- tracing (tests)
+# TRACE: None, or a dict that collects, per network call, the forward's saved buffers and the backward's
+# per-level gradient tensors (tests/test_gpu_c3_layers.py checks every layer against torch on those).
+TRACE = None
+
+
+def _trace(kind, key, t):
+    if TRACE is not None:
+        TRACE.setdefault(kind, [{}])[-1][key] = t
+
+
+def _trace_new(kind):
+    if TRACE is not None:
+        TRACE.setdefault(kind, []).append({})
+
+
 # ----------------------------------------------------------------------------- weight-gradient lane
 # The weight gradients of a backward hang off its input-gradient chain (each needs that layer's incoming
 # gradient and saved input; nothing on the chain needs them), so they run on a side stream per calling
@@ -57,7 +73,9 @@ class _WgradLane:
         most WGRAD_OVERLAP_MAX_PIX output pixels per image go to the side (the big ones fill the GPU alone;
         overlapping them measured slower)."""
         if self.side is None or pixels > WGRAD_OVERLAP_MAX_PIX:
+            self.last_side = False
             return fn()
+        self.last_side = True
         self.side.wait_stream(self.cur)
         for t in reads:
             t.record_stream(self.side)
@@ -67,6 +85,50 @@ class _WgradLane:
     def join(self):
         if self.side is not None:
             self.cur.wait_stream(self.side)
+
+
+class GradWriter:
+    """Where one backward writes its network's parameter gradients: the network's flat gradient buffer
+    (parallel.FlatGrads; each ``p.grad`` is a view of it), so no gradient is allocated, copied into an
+    exchange buffer or accumulated by autograd.  torch's accumulation semantics are kept: a parameter
+    whose ``.grad`` is None (the optimiser's zero_grad) gets its view and the kernels write it in place; a
+    parameter that already holds a gradient (the discriminator's real and fake calls inside one graph,
+    STCGAN/stcgan.py:219-227) gets a scratch result that ``flush`` adds to it (one multi-tensor launch),
+    old + new in that order.  With data parallelism the network's BucketExchange is told as each layer's
+    gradients are enqueued (``done``), so its buckets are all-reduced while the backward continues."""
+
+    def __init__(self, net):
+        from .parallel import flat_grads
+        self.flat = flat_grads(net)
+        self.exchange = getattr(net, "grad_exchange", None)
+        self.acc = []
+        self._acc_ids = set()
+
+    def dest(self, p):
+        g = p.grad
+        if g is None:
+            p.grad = self.flat.view(p)
+            return p.grad
+        s = torch.empty(p.shape, dtype=torch.float32, device=p.device)
+        self.acc.append((g, s, p))
+        self._acc_ids.add(id(p))
+        return s
+
+    def done(self, params, lane=None):
+        """Gradients of ``params`` enqueued (on the lane's side stream when its last job went there)."""
+        if self.exchange is None:
+            return
+        fresh = [p for p in params if id(p) not in self._acc_ids]
+        if fresh:
+            side = lane.side if (lane is not None and getattr(lane, "last_side", False)) else None
+            self.exchange.ready(fresh, side)
+
+    def flush(self):
+        if self.acc:
+            ops.grad_accumulate([(g, s) for g, s, _ in self.acc])
+            if self.exchange is not None:
+                self.exchange.ready([p for _, _, p in self.acc])
+            self.acc, self._acc_ids = [], set()
 
 
 _ONES = {}
@@ -206,30 +268,35 @@ def gen_forward(plan, sources, train, dt, cache, save):
     if save:
         saved = dict(S=S, xin=xin, rd=rd, ad=ad, cr=cr, rq=rq, tab_d=tab_d, tab_u=tab_u, st_d=st_d, st_u=st_u,
                      y=y, cin=cin, cin_pad=cin_pad, src_c=[s.shape[1] for s in sources])
+        if TRACE is not None:
+            _trace_new("G")
+            _trace("G", "saved", saved)
     return y, saved
 
 
-def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
-    """Returns (list of source grads (NCHW fp32 or None), dict param-id -> grad)."""
+def gen_backward(plan, saved, gy, dt, cache, need_src, W):
+    """Returns the list of source grads (NCHW fp32 or None); the parameter gradients go to the
+    GradWriter ``W`` (None: not needed)."""
     S, xin, rd, ad, cr, rq = saved["S"], saved["xin"], saved["rd"], saved["ad"], saved["cr"], saved["rq"]
     tab_d, tab_u, st_d, st_u, y = saved["tab_d"], saved["tab_u"], saved["st_d"], saved["st_u"], saved["y"]
     Lv, co = plan.L, plan.co
     dev = y.device
     B = y.shape[0]
-    grads = {}
     gy = gy.contiguous()
+    need_w = W is not None
     lane = _WgradLane() if need_w else None
 
-    def put(p, g):
-        if need_w:
-            grads[id(p)] = g
+    def dest(p):
+        return W.dest(p) if need_w else None
 
     # ---- tanh + bias
     cp = ops.vec(dt)
     Ho, Wo = y.shape[2], y.shape[3]
     dq = _nhwc(B, Ho, Wo, cp, dt, dev)
-    dbias0 = ops.tanh_bias_bwd(y, gy, L.nhwc_view(dq), dt)
-    put(plan.convT[0].bias, dbias0)
+    ops.tanh_bias_bwd(y, gy, L.nhwc_view(dq), dt, dbias=dest(plan.convT[0].bias))
+    if need_w:
+        W.done([plan.convT[0].bias])
+    _trace("G", ("dq", 0), dq)
     # ---- up path backward: convT_k, then BN_up[k+1]
     gcat = [None] * Lv
     for k in range(Lv):
@@ -238,15 +305,18 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
         cg = cp if k == 0 else cout_t
         dqv = L.nhwc_view(dq)
         if need_w:  # D = convT input (grid S[k+1]), G = dq gathered at stride 2
-            put(plan.convT[k].weight, lane.run(lambda k=k, dqv=dqv, cin_t=cin_t, cg=cg, cout_t=cout_t: ops.wgrad(
-                B, 2, L.nhwc_view(cr[k]), cin_t, dqv, cg, cout_t, dt, device=dev), dq,
-                pixels=S[k + 1][0] * S[k + 1][1]))
+            wT = plan.convT[k].weight
+            lane.run(lambda k=k, dqv=dqv, cin_t=cin_t, cg=cg, cout_t=cout_t, out=W.dest(wT): ops.wgrad(
+                B, 2, L.nhwc_view(cr[k]), cin_t, dqv, cg, cout_t, dt, device=dev, out=out), dq,
+                pixels=S[k + 1][0] * S[k + 1][1])
+            W.done([wT], lane)
         wd = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_DGRAD, cin_t, cg, dt)
         if k < Lv - 1:
             ah, aw = _pad2(S, k + 1)
             gcat[k] = _nhwc(B, ah, aw, cin_t, dt, dev, zero=(ah, aw) != S[k + 1])
         else:
             gcat[k] = _nhwc(B, *S[Lv], cin_t, dt, dev)
+        _trace("G", ("gcat", k), gcat[k])
         if k == Lv - 1:
             ops.conv(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt)
             break
@@ -258,11 +328,14 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
         mean, rstd = st_u[k + 1]
         t = tab_u[k + 1]
         dq = _nhwc(B, ah, aw, C, dt, dev)
-        dg, db = ops.conv_bn_backward(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt,
-                                      bn_x=L.nhwc_view(rq[k + 1]), C=C, bn_state=(t[0], t[1], mean, rstd),
-                                      gamma=plan.bnu[k + 1].weight, s_self=0.0, ch_off=C, dxv=L.nhwc_view(dq))
-        put(plan.bnu[k + 1].weight, dg)
-        put(plan.bnu[k + 1].bias, db)
+        bn = plan.bnu[k + 1]
+        ops.conv_bn_backward(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt,
+                             bn_x=L.nhwc_view(rq[k + 1]), C=C, bn_state=(t[0], t[1], mean, rstd),
+                             gamma=bn.weight, s_self=0.0, ch_off=C, dxv=L.nhwc_view(dq),
+                             dgamma=dest(bn.weight), dbeta=dest(bn.bias))
+        if need_w:
+            W.done([bn.weight, bn.bias])
+        _trace("G", ("dq", k + 1), dq)
     # ---- innermost r_{L-1}: ReLU backward (no BN)
     dr = _nhwc(B, *S[Lv], co[Lv - 1], dt, dev)
     ops.bn_backward(B, L.nhwc_view(rd[Lv - 1]), co[Lv - 1], dt, L.nhwc_view(dr), g1=L.nhwc_view(gcat[Lv - 1]),
@@ -271,28 +344,34 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
     src_grads = None
     for k in range(Lv - 1, -1, -1):
         drv = L.nhwc_view(dr)
+        _trace("G", ("dr", k), dr)
         if k == 0:
             if need_w:
-                put(plan.conv[0].weight, lane.run(lambda drv=drv: ops.wgrad(
-                    B, 2, drv, co[0], L.nhwc_view(xin), saved["cin_pad"], saved["cin"], dt, device=dev), dr,
-                    pixels=S[1][0] * S[1][1]))
+                w0 = plan.conv[0].weight
+                lane.run(lambda drv=drv, out=W.dest(w0): ops.wgrad(
+                    B, 2, drv, co[0], L.nhwc_view(xin), saved["cin_pad"], saved["cin"], dt, device=dev, out=out),
+                    dr, pixels=S[1][0] * S[1][1])
+                W.done([w0], lane)
             if need_src:
                 wd = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_DGRAD, saved["cin_pad"], co[0], dt)
                 gx = _nhwc(B, 2 * S[1][0], 2 * S[1][1], saved["cin_pad"], dt, dev)
                 ops.conv(L.CONVT_S2, B, drv, co[0], wd, saved["cin_pad"], L.nhwc_view(gx), dt)
-                H, W = S[0]
+                H, W_ = S[0]
                 # only the sources that need a gradient; the scatter writes every element of those
-                src_grads = [torch.empty((B, c, H, W), dtype=torch.float32, device=dev) if nd else None
+                src_grads = [torch.empty((B, c, H, W_), dtype=torch.float32, device=dev) if nd else None
                              for c, nd in zip(saved["src_c"], need_src)]
-                ops.scatter(gx, src_grads, saved["src_c"], dt, H, W)
+                ops.scatter(gx, src_grads, saved["src_c"], dt, H, W_)
             break
         cprev = co[k - 1]
         if need_w:  # D = dr_k (grid S[k+1]), G = conv_k input = ad[k-1]
-            put(plan.conv[k].weight, lane.run(lambda k=k, drv=drv, cprev=cprev: ops.wgrad(
-                B, 2, drv, co[k], L.nhwc_view(ad[k - 1]), cprev, cprev, dt, device=dev), dr,
-                pixels=S[k + 1][0] * S[k + 1][1]))
+            wk = plan.conv[k].weight
+            lane.run(lambda k=k, drv=drv, cprev=cprev, out=W.dest(wk): ops.wgrad(
+                B, 2, drv, co[k], L.nhwc_view(ad[k - 1]), cprev, cprev, dt, device=dev, out=out), dr,
+                pixels=S[k + 1][0] * S[k + 1][1])
+            W.done([wk], lane)
         wd = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_DGRAD, cprev, co[k], dt)
         ga = _nhwc(B, 2 * S[k + 1][0], 2 * S[k + 1][1], cprev, dt, dev)
+        _trace("G", ("ga", k), ga)
         # r_{k-1} feeds the skip (ReLU) and conv_k (LeakyReLU); then BN_down[k-1] (absent for k-1 == 0)
         dr = _nhwc(B, *S[k], cprev, dt, dev)
         xv = L.nhwc_view(rd[k - 1])
@@ -304,14 +383,15 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, need_w):
             mean, rstd = st_d[k - 1]
             t = tab_d[k - 1]
             bn = plan.bnd[k - 1]
-            dg, db = ops.conv_bn_backward(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt, bn_x=xv, C=cprev,
-                                          bn_state=(t[0], t[1], mean, rstd), gamma=bn.weight, s_self=LRELU,
-                                          g_other=g1, s_other=0.0, dxv=L.nhwc_view(dr))
-            put(bn.weight, dg)
-            put(bn.bias, db)
+            ops.conv_bn_backward(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt, bn_x=xv, C=cprev,
+                                 bn_state=(t[0], t[1], mean, rstd), gamma=bn.weight, s_self=LRELU,
+                                 g_other=g1, s_other=0.0, dxv=L.nhwc_view(dr), dgamma=dest(bn.weight),
+                                 dbeta=dest(bn.bias))
+            if need_w:
+                W.done([bn.weight, bn.bias])
     if lane is not None:
         lane.join()
-    return src_grads, grads
+    return src_grads
 
 
 # ----------------------------------------------------------------------------- discriminator
@@ -373,10 +453,12 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None, stats_only=
         wp = ops.packed(cache, cv.weight, L.PACK_CONV_FWD, cout, chans[i], dt)
         kind = L.CONV_S2 if s == 2 else L.CONV_S1
         if i == n - 1:
+            if stats_only:  # logits not computed: a zero-element placeholder, so that no caller can read garbage
+                out = torch.empty((B, cout, 0, 0), dtype=torch.float32, device=dev)
+                break
             out = torch.empty((B, cout, h, w), dtype=torch.float32, device=dev)
-            if not stats_only:
-                ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nchw_view(out), dt, bias=cv.bias,
-                         out_f32=True)
+            ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nchw_view(out), dt, bias=cv.bias,
+                     out_f32=True)
             break
         o = _nhwc(B, h, w, cout, dt, dev)
         tab, st = None, None
@@ -401,16 +483,20 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None, stats_only=
         saved = dict(raw=raw, act=act, dims=dims, chans=chans, tabs=tabs, stats=stats, cin=cin, cin_pad=cin_pad,
                      bias_ch=bias_ch,
                      src_c=[s.shape[1] for s in sources])
+        if TRACE is not None:
+            _trace_new("D")
+            _trace("D", "saved", saved)
     return out, saved
 
 
-def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
+def disc_backward(plan, saved, gout, dt, cache, need_src, W):
+    """Returns the list of source grads (NCHW fp32 or None); parameter gradients go to the GradWriter ``W``."""
     raw, act, dims, chans, tabs, stats = (saved["raw"], saved["act"], saved["dims"], saved["chans"], saved["tabs"],
                                           saved["stats"])
     dev = gout.device
     B = gout.shape[0]
     n = plan.n
-    grads = {}
+    need_w = W is not None
     cp = ops.vec(dt)
     h, w = gout.shape[2], gout.shape[3]
     # gradient of the logits [B,1,h,w] -> NHWC with cp channels (channel counts are vector multiples)
@@ -424,30 +510,37 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
         s = plan.strides[i]
         cout = cv.out_channels
         gv = L.nhwc_view(g, 0, h, w)  # gradient wrt conv_i output (pre-activation / pre-BN), gch channels
+        _trace("D", ("g", i), g)
         if need_w:
-            def wg(i=i, s=s, cout=cout, gv=gv, gch=gch, cv=cv):
-                bc = saved["bias_ch"] if i == 0 else None
-                dW = ops.wgrad(B, s, gv, gch, L.nhwc_view(act[i]), chans[i],
-                               (saved["cin"] if bc is None else bc + 1) if i == 0 else chans[i], dt, device=dev,
-                               rows=cout)
+            bc = saved["bias_ch"] if i == 0 else None
+            if bc is None:
+                dw_out = W.dest(cv.weight)
+                db_out = W.dest(cv.bias) if cv.bias is not None else None
+            else:  # the weight gradient of the padded input (+ the constant-1 channel) goes through a scratch
+                dw_out, db_out = W.dest(cv.weight), W.dest(cv.bias)
+
+            def wg(i=i, s=s, cout=cout, gv=gv, gch=gch, cv=cv, bc=bc, dw_out=dw_out, db_out=db_out):
                 if bc is not None:  # the constant-1 channel's tap (1,1) is the bias gradient (disc_forward)
-                    return dW[:, :saved["cin"]].contiguous(), dW[:cout, bc, 1, 1].contiguous()
-                db = ops.chan_sum(B, gv, gch, cout, dt, dev) if cv.bias is not None else None
-                return dW, db
-            dW, dbias = lane.run(wg, g, pixels=h * w)
-            grads[id(cv.weight)] = dW[:cout] if gch != cout else dW
-            if cv.bias is not None:
-                grads[id(cv.bias)] = dbias
+                    dW = ops.wgrad(B, s, gv, gch, L.nhwc_view(act[i]), chans[i], bc + 1, dt, device=dev, rows=cout)
+                    dw_out.copy_(dW[:cout, :saved["cin"]])
+                    db_out.copy_(dW[:cout, bc, 1, 1])
+                    return
+                ops.wgrad(B, s, gv, gch, L.nhwc_view(act[i]), chans[i], saved["cin"] if i == 0 else chans[i], dt,
+                          device=dev, rows=cout, out=dw_out)
+                if cv.bias is not None:
+                    ops.chan_sum(B, gv, gch, cout, dt, dev, out=db_out)
+            lane.run(wg, g, pixels=h * w)
+            W.done([cv.weight] + ([cv.bias] if cv.bias is not None else []), lane)
         if i == 0:
             if need_src:
                 wd = ops.packed(cache, cv.weight, L.PACK_CONV_DGRAD, saved["cin_pad"], gch, dt)
-                H, W = dims[0]
+                H, W_ = dims[0]
                 gx = _nhwc(B, 2 * h, 2 * w, saved["cin_pad"], dt, dev)
                 ops.conv(L.CONVT_S2, B, gv, gch, wd, saved["cin_pad"], L.nhwc_view(gx), dt)
                 # only the sources that need a gradient; the scatter writes every element of those
-                src_grads = [torch.empty((B, c, H, W), dtype=torch.float32, device=dev) if nd else None
+                src_grads = [torch.empty((B, c, H, W_), dtype=torch.float32, device=dev) if nd else None
                              for c, nd in zip(saved["src_c"], need_src)]
-                ops.scatter(gx, src_grads, saved["src_c"], dt, H, W)
+                ops.scatter(gx, src_grads, saved["src_c"], dt, H, W_)
             break
         # input gradient of conv_i (grad wrt act[i])
         ph, pw = dims[i]
@@ -462,6 +555,7 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
         # through LeakyReLU (and the BN of layer i-1's output, when present: its reduction fused
         # into the input-gradient conv)
         gn = _nhwc(B, ph, pw, cin, dt, dev)
+        _trace("D", ("ga", i), ga)
         xv = L.nhwc_view(raw[i])
         if tabs[i] is None:
             ops.conv(dkind, B, gv, gch, wd, cin, L.nhwc_view(ga), dt)
@@ -469,59 +563,32 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, need_w):
         else:
             mean, rstd = stats[i]
             bn = plan.bns[i - 2]
-            dg, db = ops.conv_bn_backward(dkind, B, gv, gch, wd, cin, L.nhwc_view(ga), dt, bn_x=xv, C=cin,
-                                          bn_state=(tabs[i][0], tabs[i][1], mean, rstd), gamma=bn.weight,
-                                          s_self=LRELU, dxv=L.nhwc_view(gn))
+            ops.conv_bn_backward(dkind, B, gv, gch, wd, cin, L.nhwc_view(ga), dt, bn_x=xv, C=cin,
+                                 bn_state=(tabs[i][0], tabs[i][1], mean, rstd), gamma=bn.weight,
+                                 s_self=LRELU, dxv=L.nhwc_view(gn),
+                                 dgamma=W.dest(bn.weight) if need_w else None,
+                                 dbeta=W.dest(bn.bias) if need_w else None)
             if need_w:
-                grads[id(bn.weight)] = dg
-                grads[id(bn.bias)] = db
+                W.done([bn.weight, bn.bias])
         g, gch, h, w = gn, cin, ph, pw
     if lane is not None:
         lane.join()
-    return src_grads, grads
+    return src_grads
 
 
 # ----------------------------------------------------------------------------- autograd
 
 
-class WeightGradGroup:
-    """Calls of one network inside one differentiated graph (the discriminator's real and fake calls,
-    STCGAN/stcgan.py:215-227) whose weight gradients the engine sums itself -- one
-    stc_grad_accumulate launch -- instead of autograd's one ATen add per parameter: every member's
-    backward but the last returns no weight gradient, the last returns the sum.  Every member's
-    backward must run (one loss over all of them, as train_step builds); use a fresh group per graph."""
-
-    def __init__(self):
-        self.members = 0
-        self.done = 0
-        self.stash = None
-
-    def join(self):
-        if self.done:
-            raise RuntimeError("WeightGradGroup: a call joined after its backward started; use a fresh group")
-        self.members += 1
-
-    def add(self, grads):
-        """Fold one member's {id(param): grad}; returns the sum after the last member, else None."""
-        self.done += 1
-        if self.stash is None:
-            self.stash = grads
-        else:
-            ops.grad_accumulate([(self.stash[k], g) for k, g in grads.items() if k in self.stash])
-            for k, g in grads.items():
-                self.stash.setdefault(k, g)
-        if self.done < self.members:
-            return None
-        out, self.stash = self.stash, None
-        return out
-
-
 class NetFn(torch.autograd.Function):
-    """One autograd node per network call.  inputs: (ctrl, *sources, *params)."""
+    """One autograd node per network call.  inputs: (ctrl, *sources, *params).
+
+    The backward returns gradients for the sources only: the parameters' gradients are written by the
+    kernels straight into the network's flat gradient buffer (GradWriter), so autograd never allocates,
+    accumulates or hooks them (``p.grad`` is set by the backward itself)."""
 
     @staticmethod
     def forward(ctx, ctrl, *tensors):
-        plan, kind, train, dt, cache, nsrc, group, inputs, _, stats_only = ctrl
+        plan, kind, train, dt, cache, nsrc, inputs, _, stats_only = ctrl
         sources = [t.contiguous().float() for t in tensors[:nsrc]]
         save = train and any(ctx.needs_input_grad[1:])
         ops.refresh_packs(cache)  # all operands packed since the last optimiser step, one launch
@@ -529,20 +596,17 @@ class NetFn(torch.autograd.Function):
                       disc_forward(plan, sources, train, dt, cache, save, inputs, stats_only and not save))
         ctx.ctrl = ctrl
         ctx.saved_net = saved
-        ctx.group = group if (save and any(ctx.needs_input_grad[1 + nsrc:])) else None
-        if ctx.group is not None:
-            ctx.group.join()
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        plan, kind, train, dt, cache, nsrc, _, _, consumer, _ = ctx.ctrl
+        plan, kind, train, dt, cache, nsrc, _, consumer, _ = ctx.ctrl
         saved = ctx.saved_net
         if saved is None:
             raise RuntimeError("stcgan_amd: backward through a network called in eval mode is not supported")
         need = ctx.needs_input_grad[1:]
         need_src = list(need[:nsrc]) if any(need[:nsrc]) else None  # per source, or None
-        need_w = any(need[nsrc:])
+        W = GradWriter(plan.net) if any(need[nsrc:]) else None
         if gout.is_cuda:
             # a side-stream network's incoming gradient is allocated on the main stream (the loss
             # backward): autograd orders this stream after it, but does not keep the caching allocator
@@ -550,10 +614,10 @@ class NetFn(torch.autograd.Function):
             # kernels enqueued here may still read it
             gout.record_stream(torch.cuda.current_stream(gout.device))
         bwd = gen_backward if kind == "G" else disc_backward
-        src_grads, grads = bwd(plan, saved, gout, dt, cache, need_src, need_w)
+        src_grads = bwd(plan, saved, gout, dt, cache, need_src, W)
+        if W is not None:
+            W.flush()
         ctx.saved_net = None
-        if ctx.group is not None:
-            grads = ctx.group.add(grads) or {}
         out = [None]
         for i in range(nsrc):
             out.append(src_grads[i] if (src_grads is not None and need[i]) else None)
@@ -561,6 +625,5 @@ class NetFn(torch.autograd.Function):
                 # a side-stream network's input gradient is read (and freed) on the consumer's stream: keep
                 # its block from being reused on this stream before the consumer is done with it
                 out[-1].record_stream(consumer)
-        for j, p in enumerate(plan.params):
-            out.append(grads.get(id(p)) if need[nsrc + j] else None)
+        out.extend([None] * len(plan.params))
         return tuple(out)

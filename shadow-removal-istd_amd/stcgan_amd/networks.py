@@ -54,9 +54,9 @@ class _HipNet(nn.Module):
         self.compute_dtype = torch.float32
         self._pack_cache = {}
         self._plan = None
-        # engine.WeightGradGroup that this network's calls join (set by the trainer around the calls
-        # of one graph whose weight gradients the engine sums), or None
-        self.weight_grad_group = None
+        # parallel.BucketExchange averaging this network's gradients over the ranks while its backward runs
+        # (set by the trainer when world > 1), or None
+        self.grad_exchange = None
         # dict reusing gathered inputs across this network's calls on the same tensors (set by the trainer
         # for one train step), or None
         self.input_cache = None
@@ -85,13 +85,17 @@ class _HipNet(nn.Module):
             self._plan = self._make_plan()
         params = self._plan.params
         ctrl = (self._plan, self.kind, self.training, self.compute_dtype, self._pack_cache, len(sources),
-                self.weight_grad_group, self.input_cache, self.grad_consumer, self.stats_only)
+                self.input_cache, self.grad_consumer, self.stats_only)
         return engine.NetFn.apply(ctrl, *sources, *params)
 
     def _apply(self, fn, *args, **kwargs):
         self._pack_cache.clear()
         ops.invalidate_packs()
         self._plan = None
+        # the flat gradient buffer (parallel.flat_grads) lives on the parameters' device: a new one is made
+        # on the next backward; an exchange bound to the old buffer is dropped with it
+        self._flat_grads = None
+        self.grad_exchange = None
         return super()._apply(fn, *args, **kwargs)
 
 

@@ -171,11 +171,11 @@ def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=False):
 
 
 def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state, gamma, s_self, ch_off=0,
-                     g_other=None, s_other=0.0, dxv=None):
+                     g_other=None, s_other=0.0, dxv=None, dgamma=None, dbeta=None):
     """Input-gradient conv (output yv) whose output feeds a BatchNorm backward, with the BN
     reduction fused into the conv (stc_conv_bwd_bn), then the BN apply (stc_bn_bwd_apply):
     dx = BN-backward of dn = out*act'(n, s_self) [+ g_other*act'(n, s_other)].
-    bn_state = (scale, shift, mean, rstd); returns (dgamma, dbeta)."""
+    bn_state = (scale, shift, mean, rstd); returns (dgamma, dbeta) (written into ``dgamma``/``dbeta`` when given)."""
     dev = w_packed.device
     l = lib()
     gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
@@ -199,8 +199,8 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
     # apply: g1 = the conv output at the BN channels over the BN extent
     g1 = L.View(yv.p, bn_x.H, bn_x.W, yv.bs, yv.rs, yv.ps, yv.co + ch_off, yv.cs, 0)
     g1._keep = yv
-    dgamma = torch.empty(C, dtype=torch.float32, device=dev)
-    dbeta = torch.empty(C, dtype=torch.float32, device=dev)
+    dgamma = _out1(dgamma, C, dev)
+    dbeta = _out1(dbeta, C, dev)
     check(l.stc_bn_bwd_apply(L.dtype_code(dt), B, bn_x, C, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), ptr(gamma),
                              g1, float(s_self), g_other if g_other is not None else L.NULL_VIEW, float(s_other),
                              ptr(part), nch, dxv, ptr(dgamma), ptr(dbeta), stream()), "stc_bn_bwd_apply")
@@ -256,17 +256,36 @@ def _wgrad_kernel_name(plan, Hd, Wd):
 _ROWS_DEFAULT = os.environ.get("STC_WGRAD_ROWS", "1") == "1"
 
 
+def _out1(t, n, device):
+    """A caller-provided fp32 output of n elements (e.g. a view of a flat gradient buffer), or a new one."""
+    if t is None:
+        return torch.empty(n, dtype=torch.float32, device=device)
+    assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n, "output: fp32, contiguous, n elements"
+    return t
+
+
+def _out_w(t, R, Cg_out, device):
+    if t is None:
+        return torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)
+    assert t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == (R, Cg_out, 4, 4), \
+        f"wgrad output: fp32 contiguous [{R}, {Cg_out}, 4, 4], got {tuple(t.shape)}"
+    return t
+
+
 def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None,
-          force=None, rows=None, rows_kernel=None):
-    """Weight gradient [R][Cg_out][4][4] fp32 (stc_conv_wgrad_ex; force = optional {tile config, splits}).
+          force=None, rows=None, rows_kernel=None, out=None):
+    """Weight gradient [R][Cg_out][4][4] fp32 (stc_conv_wgrad_ex; force = optional {tile config, splits}),
+    written into ``out`` when given (e.g. a view of a flat gradient buffer).
     rows: the number of nonzero (real) channels of D when the rest is padding -- a stride-1 layer with
-    1-2 of them goes to stc_conv_wgrad_rows."""
+    1-2 of them goes to stc_conv_wgrad_rows (which then writes only R = ``rows`` rows when R == rows)."""
     l = lib()
     if (rows is not None and rows <= 2 and stride == 1 and (_ROWS_DEFAULT if rows_kernel is None else rows_kernel) and dpro is None and gpro is None and dslope is None
             and gslope is None and force is None and Cg % 64 == 0 and ((Dv.H + 4) * (Dv.W + 4) + 16384) * rows <= 40000):
         nbytes = l.stc_conv_wgrad_rows_workspace(B, Gv.H, rows, Cg)
         ws, nb = _ws(nbytes, device)
-        dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)
+        if out is not None and out.shape[0] == rows:  # only the real rows (e.g. straight into a gradient view)
+            R = rows
+        dW = _out_w(out, R, Cg_out, device)
         timer = _timer
         if timer is not None:
             e0, e1 = _main_events()
@@ -278,11 +297,15 @@ def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=Non
             timer.append(("wgrad_rows_kernel", True, 2.0 * B * Dv.H * Dv.W * R * 16 * Cg, e0, e1,
                           f"wgrad s1 P={B * Dv.H * Dv.W} R{R} (real {rows}) Cg{Cg}"))
         return dW
+    if out is not None and out.shape[0] != R:  # real rows of a padded R: through a scratch
+        full = wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro, dslope, gpro, gslope, device, force)
+        out.copy_(full[:out.shape[0]])
+        return out
     if force is None and FORCE_WGRAD:
         force = FORCE_WGRAD.get((B, Dv.H, Dv.W, R, Cg))
     nbytes, plan = wgrad_query(B, Dv.H, Dv.W, R, Cg, dt, force)
     ws, nb = _ws(nbytes, device)
-    dW = torch.empty((R, Cg_out, 4, 4), dtype=torch.float32, device=device)
+    dW = _out_w(out, R, Cg_out, device)
     dsc, dsh = _pro(dpro)
     gsc, gsh = _pro(gpro)
     fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
@@ -441,7 +464,7 @@ def bn_apply(B, xv, C, dt, table, y1, s1, y2=None, s2=1.0):
                              y2 if y2 is not None else L.NULL_VIEW, float(s2), stream()), "stc_bn_apply")
 
 
-def bn_backward(B, xv, C, dt, dxv, g1=None, s1=0.0, g2=None, s2=0.0, bn_state=None):
+def bn_backward(B, xv, C, dt, dxv, g1=None, s1=0.0, g2=None, s2=0.0, bn_state=None, dgamma=None, dbeta=None):
     """Fused activation + BatchNorm backward.  bn_state = (scale, shift, mean, rstd, gamma) or None
     (no BN: dx = g1*act1'(x) + g2*act2'(x)).  Returns (dgamma, dbeta) or (None, None)."""
     l = lib()
@@ -458,28 +481,29 @@ def bn_backward(B, xv, C, dt, dxv, g1=None, s1=0.0, g2=None, s2=0.0, bn_state=No
     part = torch.empty((nch, C, 2), dtype=torch.float32, device=dev_t)
     check(l.stc_bn_bwd_reduce(L.dtype_code(dt), B, xv, C, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), g1v,
                               float(s1), g2v, float(s2), ptr(part), nch, stream()), "stc_bn_bwd_reduce")
-    dgamma = torch.empty(C, dtype=torch.float32, device=dev_t)
-    dbeta = torch.empty(C, dtype=torch.float32, device=dev_t)
+    dgamma = _out1(dgamma, C, dev_t)
+    dbeta = _out1(dbeta, C, dev_t)
     check(l.stc_bn_bwd_apply(L.dtype_code(dt), B, xv, C, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), ptr(gamma),
                              g1v, float(s1), g2v, float(s2), ptr(part), nch, dxv, ptr(dgamma), ptr(dbeta), stream()),
           "stc_bn_bwd_apply")
     return dgamma, dbeta
 
 
-def chan_sum(B, xv, C, Cout, dt, device):
+def chan_sum(B, xv, C, Cout, dt, device, out=None):
     nch = stats_chunks(B, xv.H, xv.W)
     part = torch.empty((nch, C), dtype=torch.float32, device=device)
-    out = torch.empty(Cout, dtype=torch.float32, device=device)
+    out = _out1(out, Cout, device)
     check(lib().stc_chan_sum(L.dtype_code(dt), B, xv, C, Cout, ptr(part), nch, ptr(out), stream()), "stc_chan_sum")
     return out
 
 
-def tanh_bias_bwd(y, gy, dqv, dt):
-    """dq = gy*(1-y^2) into the NHWC view dqv (padded channels zero); returns dbias [C]."""
+def tanh_bias_bwd(y, gy, dqv, dt, dbias=None):
+    """dq = gy*(1-y^2) into the NHWC view dqv (padded channels zero); returns dbias [C] (into ``dbias``
+    when given)."""
     B, C, H, W = y.shape
     nch = stats_chunks(B, H, W)
     part = torch.empty((nch, C), dtype=torch.float32, device=y.device)
-    dbias = torch.empty(C, dtype=torch.float32, device=y.device)
+    dbias = _out1(dbias, C, y.device)
     check(lib().stc_tanh_bias_bwd(L.dtype_code(dt), B, C, H, W, ptr(y), ptr(gy), dqv, ptr(dbias), ptr(part), nch,
                                   stream()), "stc_tanh_bias_bwd")
     return dbias

@@ -22,6 +22,7 @@ class Adam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False))
         self._epb = None
         self.fuse_pack = True  # False: update only (the packed operands are then refreshed lazily)
+        self._dev = None  # device-resident step counts (device_step), per group
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -140,8 +141,14 @@ class Adam(torch.optim.Optimizer):
         step = f["step"] + 1
         b1, b2 = group["betas"]
         torch._foreach_add_(f["step_tensors"], 1.0)
-        check(lib().stc_adam_pack_step(ptr(f["table"]), len(plist), f["blocks"], float(group["lr"]), float(b1),
-                                       float(b2), float(group["eps"]), step, stream()), "stc_adam_pack_step")
+        if self._dev is not None:
+            d = self._dev_state(gi, group, f["step"], plist[0].device)
+            check(lib().stc_adam_pack_step_dev(ptr(f["table"]), len(plist), f["blocks"], ptr(d["step"]), ptr(d["lr_dev"]),
+                                               ptr(d["bc1"]), ptr(d["bc2s"]), d["tab_len"], ptr(d["coef"]), float(b1),
+                                               float(b2), float(group["eps"]), stream()), "stc_adam_pack_step_dev")
+        else:
+            check(lib().stc_adam_pack_step(ptr(f["table"]), len(plist), f["blocks"], float(group["lr"]), float(b1),
+                                           float(b2), float(group["eps"]), step, stream()), "stc_adam_pack_step")
         ops.bump(plist)
         for p, targets, st in zip(plist, f["targets"], f["step_tensors"]):
             self._steps[id(p)] = (st, step)
@@ -151,6 +158,71 @@ class Adam(torch.optim.Optimizer):
                     cache[pkey] = (ver, out)
         f["step"] = step
         return True
+
+    # ------------------------------------------------------------------ device-resident step count
+    def device_step(self, on=True, tab_len=1 << 17):
+        """Keep each parameter group's step count on the device (stc_adam_pack_step_dev), so that a train
+        step captured as a HIP graph advances it at every replay; the host-side counts are brought back by
+        sync_steps() (state_dict() does it).  The steady-state path only: call after one ordinary step."""
+        if on and self._dev is None:
+            self._dev = {}
+            self._tab_len = int(tab_len)
+        elif not on and self._dev is not None:
+            self.sync_steps()
+            self._dev = None
+
+    def _dev_state(self, gi, group, host_step, device):
+        import math
+        import numpy as np
+        d = self._dev.get(gi)
+        if d is None:
+            b1, b2 = (float(np.float32(b)) for b in group["betas"])  # the float betas the kernel receives
+            n = self._tab_len
+            # exactly the host path's formulas: 1 - pow(beta1, step) in double; (float)sqrt(1 - pow(beta2, step))
+            bc1 = [1.0] + [1.0 - math.pow(b1, float(k)) for k in range(1, n)]
+            bc2s = [1.0] + [math.sqrt(1.0 - math.pow(b2, float(k))) for k in range(1, n)]
+            d = dict(tab_len=n, lr=None,
+                     bc1=torch.tensor(bc1, dtype=torch.float64, device=device),
+                     bc2s=torch.tensor(np.asarray(bc2s, dtype=np.float64).astype(np.float32), device=device),
+                     step=torch.tensor([int(host_step)], dtype=torch.int64, device=device),
+                     lr_dev=torch.zeros(1, dtype=torch.float64, device=device),
+                     coef=torch.zeros(2, dtype=torch.float32, device=device))
+            self._dev[gi] = d
+        if host_step + 1 >= d["tab_len"]:
+            raise RuntimeError("stcgan_amd Adam: device step table exhausted; device_step(tab_len=...) larger")
+        if d["lr"] != group["lr"]:  # the double value of the float lr the host path passes
+            d["lr_dev"].fill_(float(np.float32(group["lr"])))
+            d["lr"] = group["lr"]
+        return d
+
+    def sync_lr(self):
+        """Push a changed learning rate (a scheduler step) to the device copies the captured step reads."""
+        if not self._dev:
+            return
+        import numpy as np
+        for gi, d in self._dev.items():
+            lr = self.param_groups[gi]["lr"]
+            if d["lr"] != lr:
+                d["lr_dev"].fill_(float(np.float32(lr)))
+                d["lr"] = lr
+
+    def sync_steps(self):
+        """Host step counts (state["step"], the steady-state mirrors) from the device counters."""
+        if not self._dev:
+            return
+        for gi, d in self._dev.items():
+            s = int(d["step"].item())
+            f = self._fast.get(gi)
+            if f is None:
+                continue
+            f["step"] = s
+            for p, st in zip(f["plist"], f["step_tensors"]):
+                st.fill_(float(s))
+                self._steps[id(p)] = (st, s)
+
+    def state_dict(self):
+        self.sync_steps()
+        return super().state_dict()
 
     @staticmethod
     def _nblocks(p, row):

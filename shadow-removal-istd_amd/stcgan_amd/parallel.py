@@ -16,17 +16,15 @@ reference:
     all-reduced inside the graph (``global_mean0``); the epoch loss sums fed to
     ReduceLROnPlateau (STCGAN/stcgan.py:314-315) are all-reduced (``average_scalars``)
     so every rank's scheduler sees the same (global) values.
-Exchange per optimiser step: one all-reduce of the gradients per network (sum,
-then scaled by 1/world).
-
-Overlap: every network's gradients arrive in one autograd node (engine.NetFn),
-so a post-accumulate-grad hook counts arrivals per network and launches that
-network's bucketed all-reduce asynchronously the moment its last gradient lands
--- G2's 218 MB exchange runs while G1's backward still computes.  Groups are
-launched in index order on every rank (a completed group waits for the groups
-before it), so the collective sequence is identical across ranks whatever the
-hook timing.  ``__call__`` launches whatever did not fire, waits, and scatters
-the averages back.
+Exchange per optimiser step (``BucketExchange``): each network's parameter gradients live in
+one flat fp32 buffer (``FlatGrads``; every ``p.grad`` is a view of it, the weight-gradient kernels
+write straight into those views), laid out in backward-completion order and cut into buckets of
+~``bucket_mb``.  The engine reports each layer's gradients as it enqueues them (engine.GradWriter), and
+a bucket's all-reduce is launched -- asynchronously, on a stream ordered after the streams that wrote
+it -- the moment its last parameter is complete: the exchange of the deep layers runs while the
+large-resolution layers of the same backward still compute.  The average is RCCL's ``AVG``
+(gloo: sum, then a 1/world scale); there is no gather into or scatter out of a separate buffer.
+Every rank runs the same program, so the collective sequence is identical on all ranks.
 """
 import torch
 import torch.distributed as dist
@@ -108,123 +106,151 @@ def average_scalars(values):
     return {k: t[i] for i, k in enumerate(keys)}
 
 
-class GradAllReduce:
-    """Average the .grad of parameter groups over all ranks.
+class FlatGrads:
+    """The parameter gradients of one network in one flat fp32 buffer; ``view(p)`` is the slice that
+    becomes ``p.grad``.  Parameters are laid out in reverse module order, which is the order their
+    gradients are produced in (the generator's backward walks the up path from the outermost block
+    inwards, then the down path outwards; the discriminator's from the logits layer down), so the
+    buckets of a BucketExchange complete one after the other."""
 
-    groups: list of parameter lists (one per network); expected[g]: how many
-    backward passes accumulate into group g before one exchange (autograd sums
-    the uses of a parameter inside one graph before it accumulates, so a
-    network called twice in one differentiated graph still counts once).
-    Each group is exchanged in flat fp32 buckets of ~bucket_mb (few, large
-    collectives: ring bandwidth on xGMI is per link)."""
+    def __init__(self, params):
+        self.params = list(params)
+        dev = self.params[0].device
+        self.spans = {}
+        n = 0
+        for p in reversed(self.params):
+            self.spans[id(p)] = (n, p.numel())
+            n += p.numel()
+        self.numel = n
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.views = {}
+        for p in self.params:
+            o, k = self.spans[id(p)]
+            self.views[id(p)] = self.flat[o:o + k].view(p.shape)
 
-    def __init__(self, groups, expected=None, bucket_mb=64):
-        self.groups = [[p for p in g] for g in groups]
-        self.expected = list(expected) if expected is not None else [1] * len(self.groups)
+    def view(self, p):
+        return self.views[id(p)]
+
+    def owns(self, g, p):
+        """Whether the tensor g is p's view of this buffer."""
+        v = self.views.get(id(p))
+        return v is not None and g is not None and g.data_ptr() == v.data_ptr() and g.shape == v.shape
+
+
+def flat_grads(net):
+    """The FlatGrads of a network module (created on first use on the parameters' device; dropped when
+    the module moves: networks._HipNet._apply)."""
+    fg = getattr(net, "_flat_grads", None)
+    if fg is None:
+        fg = FlatGrads(list(net.parameters()))
+        net._flat_grads = fg
+    return fg
+
+
+class BucketExchange:
+    """Average one FlatGrads over all ranks, bucket by bucket, as the buckets complete.
+
+    ``ready(params, stream)``: those parameters' gradients are enqueued (on ``stream``, or the current
+    stream); a bucket is launched once each of its parameters has been reported ``expected`` times (the
+    discriminator's real and fake calls both write into its gradients in the D step).  ``finish()``
+    launches whatever is left, makes the current stream wait for every bucket and resets the counts."""
+
+    def __init__(self, flat, bucket_mb=32, active=None):
+        self.flat = flat
+        # active: exchange even at world size 1 (tests drive the collective path on one GPU)
+        self.active = (world() > 1) if active is None else bool(active)
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) // 4))
-        self.buckets = []  # per group: list of param lists
-        for g in self.groups:
-            bks, cur, n = [], [], 0
-            for p in g:
-                cur.append(p)
-                n += p.numel()
-                if n >= self.bucket_elems:
-                    bks.append(cur)
-                    cur, n = [], 0
-            if cur:
-                bks.append(cur)
-            self.buckets.append(bks)
-        self.flat = None
-        self.works = [None] * len(self.groups)
-        self.count = [0] * len(self.groups)
-        self.ready = [False] * len(self.groups)
-        self.hooks = []
-        self.overlap = False
-        # streams the gradients of each group were accumulated on (autograd runs a leaf's
-        # AccumulateGrad, and so the hook, on the stream of the backward that produced it; the
-        # discriminators' backwards run on side streams): the exchange waits for all of them
-        self.arrival_streams = [dict() for _ in self.groups]
-        self.cuda = bool(self.groups) and bool(self.groups[0]) and self.groups[0][0].is_cuda
+        self.ranges, self.members, self.bucket_of = [], [], {}
+        cur, start, n = [], 0, 0
+        for p in reversed(flat.params):
+            o, k = flat.spans[id(p)]
+            cur.append(id(p))
+            n += k
+            if n >= self.bucket_elems:
+                self._cut(cur, start, o + k)
+                cur, start, n = [], o + k, 0
+        if cur:
+            self._cut(cur, start, flat.numel)
+        self.expected = 1
+        self.launch_order = []  # bucket indices in launch order (diagnostics / tests)
+        self.reset()
 
-    # ---- hooks --------------------------------------------------------------------
-    def enable_overlap(self):
-        """Launch each group's exchange from the backward as soon as it is complete."""
-        if self.overlap or world() == 1:
+    def _cut(self, ids, a, e):
+        b = len(self.ranges)
+        self.ranges.append((a, e))
+        self.members.append(list(ids))
+        for i in ids:
+            self.bucket_of[i] = b
+
+    def reset(self):
+        self.count = {}
+        self.left = [len(m) for m in self.members]
+        self.works = [None] * len(self.ranges)
+
+    def _op(self):
+        # RCCL/NCCL average in the collective (a power-of-two world scales exactly); gloo has no AVG
+        return dist.ReduceOp.AVG if dist.get_backend() == "nccl" else dist.ReduceOp.SUM
+
+    def _launch(self, b, stream=None):
+        a, e = self.ranges[b]
+        if stream is not None:  # a side stream that wrote part of the bucket: it also waits for the calling
+            stream.wait_stream(torch.cuda.current_stream())  # stream, which wrote the rest
+        if stream is None:
+            self.works[b] = dist.all_reduce(self.flat.flat[a:e], op=self._op(), async_op=True)
+        else:
+            with torch.cuda.stream(stream):
+                self.works[b] = dist.all_reduce(self.flat.flat[a:e], op=self._op(), async_op=True)
+        self.launch_order.append(b)
+
+    def ready(self, params, stream=None):
+        if not self.active:
             return
-        for gi, g in enumerate(self.groups):
-            for p in g:
-                if p.requires_grad:
-                    self.hooks.append(p.register_post_accumulate_grad_hook(lambda _p, gi=gi: self._arrived(gi)))
-        self.overlap = True
+        for p in params:
+            c = self.count.get(id(p), 0) + 1
+            self.count[id(p)] = c
+            if c == self.expected:
+                b = self.bucket_of[id(p)]
+                self.left[b] -= 1
+                if self.left[b] == 0:
+                    self._launch(b, stream)
 
-    def _arrived(self, gi):
-        self.count[gi] += 1
-        if self.cuda:
-            st = torch.cuda.current_stream()
-            self.arrival_streams[gi].setdefault(st.cuda_stream, st)
-        need = self.expected[gi] * sum(1 for p in self.groups[gi] if p.requires_grad)
-        if self.count[gi] == need:
-            self.ready[gi] = True
-            # launch in index order: group gi only after groups 0..gi-1 (same sequence on every rank)
-            for gj in range(len(self.groups)):
-                if self.works[gj] is not None:
-                    continue
-                if not self.ready[gj]:
-                    break
-                self._launch(gj)
+    def finish(self):
+        w = world()
+        if not self.active:
+            self.reset()
+            return
+        for b in range(len(self.ranges)):
+            if self.works[b] is None:
+                self._launch(b)
+        for wk in self.works:
+            wk.wait()
+        if self._op() == dist.ReduceOp.SUM and w > 1:
+            self.flat.flat.mul_(1.0 / w)
+        self.reset()
 
-    # ---- exchange -------------------------------------------------------------------
-    def _ensure_flat(self):
-        if self.flat is None:
-            dev = self.groups[0][0].device
-            self.flat = [[torch.empty(sum(p.numel() for p in b), dtype=torch.float32, device=dev) for b in bks]
-                         for bks in self.buckets]
 
-    def _launch(self, gi):
-        self._ensure_flat()
-        # the launching hook may run on another group's stream (a group completing early waits
-        # for the groups before it): order the gather after every stream this group's gradients
-        # were written on
-        if self.arrival_streams[gi]:
-            cur = torch.cuda.current_stream()
-            for key, st in self.arrival_streams[gi].items():
-                if key != cur.cuda_stream:
-                    cur.wait_stream(st)
-            self.arrival_streams[gi].clear()
-        works = []
-        for b, flat in zip(self.buckets[gi], self.flat[gi]):
-            grads = [p.grad.reshape(-1) if p.grad is not None else None for p in b]
-            if all(g is not None for g in grads):
-                torch.cat(grads, out=flat)  # one gather kernel per bucket
-            else:
-                off = 0
-                for p, g in zip(b, grads):
-                    n = p.numel()
-                    if g is None:
-                        flat[off:off + n].zero_()
-                    else:
-                        flat[off:off + n].copy_(g)
-                    off += n
-            works.append(dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True))
-        self.works[gi] = works
+class GradAllReduce:
+    """Average the gradients of groups of ordinary autograd leaves over all ranks (for parameters that
+    are not written by the engine): each group gets a FlatGrads whose zero-filled views are attached as
+    the leaves' ``.grad`` (autograd accumulates into them in place) and a BucketExchange fed by
+    post-accumulate-grad hooks.  ``__call__`` finishes the exchange (the engine's networks use
+    FlatGrads/BucketExchange directly: engine.GradWriter)."""
+
+    def __init__(self, groups, bucket_mb=32):
+        self.flats = [FlatGrads(g) for g in groups]
+        self.exchanges = [BucketExchange(f, bucket_mb) for f in self.flats]
+        self.hooks = []
+        for f, ex in zip(self.flats, self.exchanges):
+            for p in f.params:
+                if p.grad is not None:  # a gradient computed before the exchange was set up moves into the view
+                    f.view(p).copy_(p.grad)
+                p.grad = f.view(p)
+                if p.requires_grad and world() > 1:
+                    self.hooks.append(p.register_post_accumulate_grad_hook(lambda q, ex=ex: ex.ready([q])))
+
+    def enable_overlap(self):  # (hooks are registered at construction)
+        pass
 
     def __call__(self):
-        w = world()
-        if w == 1:
-            return
-        for gi in range(len(self.groups)):
-            if self.works[gi] is None:
-                self._launch(gi)
-        for gi in range(len(self.groups)):
-            for wk in self.works[gi]:
-                wk.wait()
-            for b, flat in zip(self.buckets[gi], self.flat[gi]):
-                flat.mul_(1.0 / w)
-                for p in b:
-                    if p.grad is None:
-                        p.grad = torch.empty_like(p)
-                parts = [s.view_as(p) for s, p in zip(torch.split(flat, [p.numel() for p in b]), b)]
-                torch._foreach_copy_([p.grad for p in b], parts)  # one multi-tensor launch per bucket
-        self.works = [None] * len(self.groups)
-        self.count = [0] * len(self.groups)
-        self.ready = [False] * len(self.groups)
+        for ex in self.exchanges:
+            ex.finish()

@@ -27,7 +27,6 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import engine
 from . import networks
 from . import parallel
 from .loss import AdversarialLoss, DataLoss, d_objective, g_objective
@@ -60,8 +59,7 @@ class STCGAN(object):
         self.logger = logging.getLogger(__name__)
         if not torch.cuda.is_available():
             raise RuntimeError("stcgan_amd.STCGAN needs a ROCm GPU")
-        dev = args.devices[0] if getattr(args, "devices", None) else "cuda"
-        self.device = torch.device(dev)
+        self.device = torch.device(self._device_of(args))
         ngf = getattr(args, "ngf", 64)
         self.G1 = networks.get_generator(in_channels=3, out_channels=1, ngf=ngf)
         self.G2 = networks.get_generator(in_channels=3 + 1, out_channels=3, ngf=ngf)
@@ -88,16 +86,17 @@ class STCGAN(object):
                             lr=args.lr_D, betas=(args.beta1, args.beta2))
         self.decay_G = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_G, cooldown=10, min_lr=1e-7, factor=0.8)
         self.decay_D = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_D, cooldown=10, min_lr=1e-7, factor=0.8)
-        # one gradient exchange per network, launched from the backward as soon as that
-        # network's gradients are complete (one backward per step: STCGAN/stcgan.py:227,292)
-        self.sync_G = parallel.GradAllReduce([list(self.G2.parameters()), list(self.G1.parameters())])
-        self.sync_D = parallel.GradAllReduce([list(self.D2.parameters()), list(self.D1.parameters())])
-        self.sync_G.enable_overlap()
-        self.sync_D.enable_overlap()
+        # data parallelism: each network's gradients (one flat buffer, parallel.FlatGrads) are averaged over
+        # the ranks bucket by bucket while its backward runs (parallel.BucketExchange, fed by the engine)
+        self.bucket_mb = float(getattr(args, "bucket_mb", 32))
+        if parallel.world() > 1:
+            for net in (self.G1, self.G2, self.D1, self.D2):
+                net.grad_exchange = parallel.BucketExchange(parallel.flat_grads(net), self.bucket_mb)
         # discriminators on side HIP streams (train_step / _lanes); off for a strictly serial step
         self.streams = bool(getattr(args, "streams", True))
         self.lane_carry = bool(getattr(args, "lane_carry", True))
         self._lane_inputs = None
+        self._lanes_stale = True  # the side lanes must wait for the main stream before their next work
         # loss type "normal": the D and G objectives as one fused node each (loss.d_objective / g_objective)
         self.fused_objectives = bool(getattr(args, "fused_objectives", True))
         self._side = None
@@ -125,6 +124,37 @@ class STCGAN(object):
             self.valid_interval = getattr(args, "valid_every", 10)
         if "infer" in tasks:
             self.inferd_dir = getattr(args, "infered", None)
+
+    @staticmethod
+    def _device_of(args):
+        """The reference trains on ``args.devices`` with nn.DataParallel (STCGAN/stcgan.py:53-59).  Here
+        data parallelism is one process per GPU: each rank takes ``devices[local rank]``.  A multi-device
+        list in a single process cannot be honoured silently, so it is an error."""
+        devs = list(getattr(args, "devices", None) or ["cuda"])
+        w = parallel.world()
+        if len(devs) > 1 and w == 1:
+            raise RuntimeError(
+                f"stcgan_amd: args.devices lists {len(devs)} devices, but data parallelism runs one process per "
+                f"GPU: launch the script with `torchrun --nproc-per-node {len(devs)} ...` (each rank uses "
+                f"devices[LOCAL_RANK] and the gradients are all-reduced over RCCL), or pass one device")
+        if w > 1:
+            local = int(os.environ.get("LOCAL_RANK", parallel.rank()))
+            return devs[local] if len(devs) >= w else f"cuda:{local % max(torch.cuda.device_count(), 1)}"
+        return devs[0]
+
+    def _exchange(self, names, expected):
+        """Set how many backward calls write each network's gradients in this step (the discriminators are
+        called on real and on fake inputs inside the D step's graph)."""
+        for n in names:
+            ex = getattr(self, n).grad_exchange
+            if ex is not None:
+                ex.expected = expected
+
+    def _finish_exchange(self, names):
+        for n in names:
+            ex = getattr(self, n).grad_exchange
+            if ex is not None:
+                ex.finish()
 
     def istd_loaders(self, args):
         """The reference's train/valid loaders (STCGAN/stcgan.py:73-104) on data.ISTDLoader."""
@@ -207,7 +237,9 @@ class STCGAN(object):
         return (main,) + self._side
 
     def _on(self, lane, net, srcs, after=None):
-        """net(srcs) on ``lane`` (None = the current stream), after the main-stream event ``after``."""
+        """net(srcs) on ``lane`` (None = the current stream), after the main-stream event ``after``.
+        (A lane output read by several main-stream ops gets its gradients summed by autograd; that sum is
+        safe across streams on this torch: tests/test_gpu_stream_hazards.py.)"""
         if lane is None:
             return net(srcs)
         with torch.cuda.stream(lane):
@@ -237,18 +269,26 @@ class STCGAN(object):
             # Lane-allocated tensors read on the main stream are record_stream'ed (outputs, input gradients).
             # inputs_ready: an event after which x, m, y are complete (produced on another stream, not read
             # by anything but this step), e.g. run_epoch's input stream
-            key = tuple((id(t), t._version, t.data_ptr()) for t in (x, m, y))
+            # the previous step's inputs are held (not an id/address key: both are reused once a tensor dies)
+            same = (self._lane_inputs is not None
+                    and all(a is b and a._version == v for a, b, v in zip((x, m, y), *self._lane_inputs)))
             if inputs_ready is not None:
                 for t in (x, m, y):
                     t.record_stream(main)
                 main.wait_event(inputs_ready)
-            if inputs_ready is not None and self.lane_carry:
-                l1.wait_event(inputs_ready)
-                l2.wait_event(inputs_ready)
-            elif not (self.lane_carry and key == self._lane_inputs):
+            if self._lanes_stale or not self.lane_carry:
+                # D state written on the main stream outside the step (construction, broadcasts, checkpoint
+                # loads, a validation pass): the lanes start after it
                 l1.wait_stream(main)
                 l2.wait_stream(main)
-            self._lane_inputs = key
+                self._lanes_stale = False
+            elif inputs_ready is not None:
+                l1.wait_event(inputs_ready)
+                l2.wait_event(inputs_ready)
+            elif not same:
+                l1.wait_stream(main)
+                l2.wait_stream(main)
+            self._lane_inputs = ((x, m, y), tuple(t._version for t in (x, m, y)))
             self.D1.grad_consumer = self.D2.grad_consumer = main
         # each discriminator sees the same real and fake inputs in the D and the G step: gather them once
         self.D1.input_cache, self.D2.input_cache = {}, {}
@@ -262,9 +302,6 @@ class STCGAN(object):
             self.optim_D.zero_grad()
             self.D1.requires_grad_(True)
             self.D2.requires_grad_(True)
-            # each discriminator's real + fake weight gradients summed by the engine (one launch)
-            self.D1.weight_grad_group = engine.WeightGradGroup()
-            self.D2.weight_grad_group = engine.WeightGradGroup()
             C1_real = self._on(l1, self.D1, [x, m])
             C2_real = self._on(l2, self.D2, [x, m, y])
             m_pred = self.G1(x)
@@ -273,7 +310,6 @@ class STCGAN(object):
             y_pred = self.G2([x, m_pred])
             ev_y = main.record_event() if l1 is not None else None
             C2_fake = self._on(l2, self.D2, [x, m_pred.detach(), y_pred.detach()], after=ev_y)
-            self.D1.weight_grad_group = self.D2.weight_grad_group = None
             if l1 is not None:
                 main.wait_stream(l1)
                 main.wait_stream(l2)
@@ -284,8 +320,9 @@ class STCGAN(object):
                 D1_loss, D2_loss = self._d_losses(C1_real, C1_fake, C2_real, C2_fake)
                 D_loss = self.lambda2 * D1_loss + self.lambda3 * D2_loss
             if training:
+                self._exchange(("D1", "D2"), 2)  # real + fake calls
                 D_loss.backward()
-                self.sync_D()
+                self._finish_exchange(("D2", "D1"))
                 self.optim_D.step()
             d_out = (C1_real.detach(), C1_fake.detach(), C2_real.detach(), C2_fake.detach())
 
@@ -304,6 +341,8 @@ class STCGAN(object):
                 C1_real = self._on(l1, self.D1, [x, m])
                 C2_real = self._on(l2, self.D2, [x, m, y])
                 self.D1.stats_only = self.D2.stats_only = False
+                if unused:  # (zero-element placeholders: the logits were not computed)
+                    C1_real = C2_real = None
                 C1_fake = self._on(l1, self.D1, [x, m_pred])
                 C2_fake = self._on(l2, self.D2, [x, m_pred, y_pred])
                 if l1 is not None:
@@ -318,8 +357,9 @@ class STCGAN(object):
                 data2_loss = self.data_loss(y_pred, y)
                 G_loss = data1_loss + self.lambda1 * data2_loss + self.lambda2 * G1_loss + self.lambda3 * G2_loss
             if training:
+                self._exchange(("G1", "G2"), 1)
                 G_loss.backward()
-                self.sync_G()
+                self._finish_exchange(("G2", "G1"))
                 self.optim_G.step()
         if l1 is not None:  # nothing on the side lanes outlives the step
             main.wait_stream(l1)
@@ -335,11 +375,48 @@ class STCGAN(object):
             acc["D2_fake"] = acc["D2_fake"] + d_out[3].mean()
         return vals
 
+    def capture(self, x, m, y, warmup=1):
+        """train_step(x, m, y) captured as one HIP graph; returns ``replay()``, which runs one more full
+        train step (both D and G updates) on whatever x, m, y then hold (refill them in place: the graph
+        keeps their addresses).  Kernels, streams and memory are those of the eager step -- the side lanes
+        and weight-gradient streams become branches of the graph, every activation lives in the graph's
+        private pool -- but the ~700 launches of a step leave the host: one graph launch per step.  The
+        optimisers switch to device-resident step counts (optim.Adam.device_step) so that replays advance
+        them; their host-side counts are synced by state_dict().  Replay is bit-identical to the eager
+        step (tests/test_gpu_graph.py).  World size > 1 needs the RCCL backend (collectives are captured
+        too)."""
+        import torch.distributed as dist
+        if parallel.world() > 1 and dist.get_backend() != "nccl":
+            raise RuntimeError("STCGAN.capture: multi-process capture needs the nccl (RCCL) backend")
+        main = torch.cuda.current_stream(self.device)
+        cap = torch.cuda.Stream(self.device)
+        cap.wait_stream(main)
+        with torch.cuda.stream(cap):
+            for _ in range(max(1, warmup)):  # steady state: packed operands, tables, streams, flat gradients
+                self.train_step(x, m, y)
+            for o in (self.optim_G, self.optim_D):
+                o.device_step(True)
+            self.train_step(x, m, y)  # one eager step in device-step mode (creates the device counters)
+        main.wait_stream(cap)
+        torch.cuda.synchronize(self.device)
+        graph = torch.cuda.CUDAGraph()
+        self._lanes_stale = True  # inside the capture the lanes must fork from the capturing stream
+        with torch.cuda.graph(graph, stream=cap):
+            self.train_step(x, m, y)
+        self._graph = graph
+
+        def replay():
+            for o in (self.optim_G, self.optim_D):
+                o.sync_lr()
+            graph.replay()
+        return replay
+
     def run_epoch(self, training=True):
         for net in (self.G1, self.G2, self.D1, self.D2):
             net.train(training)
         if not training:  # eval-mode replicas use dev0's running statistics
             parallel.broadcast_buffers([self.G1, self.G2, self.D1, self.D2])
+        self._lanes_stale = True  # (the broadcast above, a checkpoint load, a caller's writes between epochs)
         keys = ["G", "D", "D1", "D2", "G1", "G2", "data1", "data2"]
         acc = {k: torch.zeros((), device=self.device) for k in keys + ["D1_real", "D1_fake", "D2_real", "D2_fake"]}
         data_loader = self.train_loader if training else self.valid_loader
@@ -441,6 +518,7 @@ class STCGAN(object):
         """Resume from save_checkpoint (src/cgan.py:513-523; restores decay_G as well -- the
         reference loads decay_D twice)."""
         ck = torch.load(path, map_location=self.device, weights_only=True)
+        self._lanes_stale = True  # the loads below write D state on the main stream
         self.start_epoch = ck["epoch"]
         for k in ("G1", "G2", "D1", "D2"):
             getattr(self, k).load_state_dict(ck[k])

@@ -9,7 +9,7 @@ Checks the reference's DataParallel semantics that the RCCL path keeps
   * ranks that initialise from different seeds hold rank 0's weights after
     ``broadcast_state`` (DataParallel replicates dev0's module);
   * the epoch loss sums fed to ReduceLROnPlateau are the global ones on every rank;
-  * gradient groups are exchanged in index order whatever order they complete in.
+  * each network's flat gradient buffer is exchanged bucket by bucket as the buckets complete.
 The networks here are the CPU oracle (test infrastructure) -- only the exchange
 logic is under test.
 """
@@ -48,19 +48,20 @@ def _worker(rank, world, port, out):
     z = uniform((4, 4, 64, 64), 8)
     plist = [v for k, v in params.items() if v.requires_grad]
     half = len(plist) // 2
-    # two groups; the net is used twice in the graph (real + fake) but autograd sums the
-    # uses before accumulating, so each parameter's hook fires once per backward
+    # two groups, each one flat buffer (the leaves' .grad are views of it) cut into several buckets; the
+    # net is used twice in the graph (real + fake) but autograd sums the uses before accumulating, so each
+    # parameter's hook fires once per backward
     sync = parallel.GradAllReduce([plist[:half], plist[half:]], bucket_mb=0.002)
-    assert all(len(b) > 1 for b in sync.buckets)  # several buckets per group
-    sync.enable_overlap()
+    assert all(len(ex.ranges) > 1 for ex in sync.exchanges)  # several buckets per group
+    assert all(sync.flats[i].owns(p.grad, p) for i, grp in enumerate((plist[:half], plist[half:])) for p in grp)
     sl = slice(rank * 2, (rank + 1) * 2)
     out_a = ref.discriminator_forward(params, x[sl], True)
     out_b = ref.discriminator_forward(params, z[sl], True)
     loss = (((out_a - 1.0) ** 2).mean() + (out_b ** 2).mean()) * 0.5
     loss.backward()
-    assert all(w is not None for w in sync.works)  # launched from the backward hooks
+    assert all(w is not None for ex in sync.exchanges for w in ex.works)  # launched from the backward hooks
     sync()
-    assert sync.works == [None, None] and sync.count == [0, 0]
+    assert all(w is None for ex in sync.exchanges for w in ex.works) and all(not ex.count for ex in sync.exchanges)
     if rank == 0:
         import io
         buf = io.BytesIO()
@@ -180,19 +181,24 @@ def _worker_semantics(rank, world, port, out):
     acc = {"G": torch.tensor(float(rank + 1)), "D": torch.tensor(10.0 * (rank + 1))}
     avg = parallel.average_scalars(acc)
     res["sched"] = (float(avg["G"]), float(avg["D"]))
-    # (4) launch order: group 1 completes first, is held until group 0 has launched
-    a = torch.ones(3, requires_grad=True)
-    b = torch.ones(3, requires_grad=True)
-    sync2 = parallel.GradAllReduce([[a], [b]])
-    sync2.enable_overlap()
-    order = []
-    orig = sync2._launch
-    sync2._launch = lambda gi: (order.append(gi), orig(gi))
-    (b * (rank + 1)).sum().backward()  # only group 1 completes
-    held = list(order)
-    (a * 2.0).sum().backward()
-    sync2()
-    res["order"] = (held, order, a.grad.clone(), b.grad.clone())
+    # (4) engine-style exchange: gradients written into the flat views and reported per layer; with
+    # expected = 2 (the discriminator's real and fake calls) a bucket launches on its second report, in
+    # completion order (b's bucket before a's: b is later in module order, so earlier in the flat buffer)
+    a = torch.zeros(3, requires_grad=True)
+    b = torch.zeros(5, requires_grad=True)
+    fg = parallel.FlatGrads([a, b])
+    ex = parallel.BucketExchange(fg, bucket_mb=1e-6)  # one parameter per bucket
+    ex.expected = 2
+    fg.view(a).fill_(2.0 * (rank + 1))
+    fg.view(b).fill_(float(rank + 1))
+    ex.ready([b])
+    held = list(ex.launch_order)
+    ex.ready([b])
+    ex.ready([a])
+    ex.ready([a])
+    order = list(ex.launch_order)
+    ex.finish()
+    res["order"] = (held, order, fg.view(a).clone(), fg.view(b).clone(), [fg.spans[id(a)], fg.spans[id(b)]])
     import io
     buf = io.BytesIO()
     torch.save(res, buf)  # bytes, not shared-memory tensors: the worker exits before the parent reads
@@ -228,6 +234,7 @@ def test_dataparallel_semantics_world2():
         for g, w in zip(r["rel_avg_grads"], want):
             assert torch.allclose(g, w, atol=1e-6, rtol=1e-5)
         assert r["sched"] == (1.5, 15.0)
-        held, order, ga, gb = r["order"]
+        held, order, ga, gb, spans = r["order"]
+        assert spans == [(5, 3), (0, 5)]  # reverse module order: b first
         assert held == [] and order == [0, 1]
-        assert torch.allclose(ga, torch.full((3,), 2.0)) and torch.allclose(gb, torch.full((3,), 1.5))
+        assert torch.equal(ga, torch.full((3,), 3.0)) and torch.equal(gb, torch.full((5,), 1.5))

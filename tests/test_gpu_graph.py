@@ -1,0 +1,74 @@
+"""The train step captured as one HIP graph (STCGAN.capture) and replayed must be the eager step, bit
+for bit: same kernels, same memory contents, the side-stream branches and the device-resident Adam step
+count included.  Two trainers from one initial state: eager steps on one, capture + replays on the
+other; every parameter, BatchNorm buffer and Adam moment must agree exactly after each replay, and the
+optimiser's host-side step counts must come back right (state_dict)."""
+import types
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+NETS = ("G1", "G2", "D1", "D2")
+
+
+def _trainer(dtype, ngf, loss_type):
+    from stcgan_amd.stcgan import STCGAN
+    torch.manual_seed(7)
+    a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5, beta2=0.999,
+                              D_loss_fn="standard", D_loss_type=loss_type, ngf=ngf, dtype=dtype,
+                              load_weights_g1=None, load_weights_g2=None, load_weights_d1=None,
+                              load_weights_d2=None)
+    return STCGAN(a)
+
+
+def _state(tr):
+    torch.cuda.synchronize()
+    st = {n: {k: v.detach().clone() for k, v in getattr(tr, n).state_dict().items()} for n in NETS}
+    for oname in ("optim_G", "optim_D"):
+        o = getattr(tr, oname)
+        o.sync_steps()
+        st[oname] = [(float(o.state[p]["step"]), o.state[p]["exp_avg"].clone(), o.state[p]["exp_avg_sq"].clone())
+                     for g in o.param_groups for p in g["params"]]
+    return st
+
+
+def _same(a, b):
+    bad = []
+    for n in NETS:
+        for k in a[n]:
+            if not torch.equal(a[n][k], b[n][k]):
+                bad.append((n, k))
+    for oname in ("optim_G", "optim_D"):
+        for i, (x, y) in enumerate(zip(a[oname], b[oname])):
+            if x[0] != y[0] or not torch.equal(x[1], y[1]) or not torch.equal(x[2], y[2]):
+                bad.append((oname, i))
+    return bad
+
+
+@pytest.mark.parametrize("dtype,ngf,loss_type", [("bf16", 64, "normal"), ("fp32", 16, "rel_avg")])
+def test_captured_step_is_bit_identical(dtype, ngf, loss_type):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    B = 4
+    x = torch.rand((B, 3, 256, 256), generator=g, device="cuda") * 2 - 1
+    m = (torch.rand((B, 1, 256, 256), generator=g, device="cuda") < 0.5).float() * 2 - 1
+    y = torch.rand((B, 3, 256, 256), generator=g, device="cuda") * 2 - 1
+    eager = _trainer(dtype, ngf, loss_type)
+    graphed = _trainer(dtype, ngf, loss_type)
+    replay = graphed.capture(x, m, y, warmup=1)  # 2 eager steps (warm-up + one in device-step mode) inside
+    for _ in range(2):
+        eager.train_step(x, m, y)
+    assert not _same(_state(eager), _state(graphed))
+    for i in range(3):
+        eager.train_step(x, m, y)
+        replay()
+        bad = _same(_state(eager), _state(graphed))
+        assert not bad, (i, bad[:8])
+    # new batch contents in place: the replay reads them
+    x.copy_(torch.rand((B, 3, 256, 256), generator=g, device="cuda") * 2 - 1)
+    eager.train_step(x, m, y)
+    replay()
+    assert not _same(_state(eager), _state(graphed))
+    assert float(graphed.optim_G.state[next(graphed.G1.parameters())]["step"]) == 6.0
