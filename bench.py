@@ -65,8 +65,8 @@ def parse():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--ngf", type=int, default=64)
     ap.add_argument("--dtype", default=os.environ.get("STC_BENCH_DTYPE", "bf16"), choices=["fp32", "bf16"])
-    ap.add_argument("--no-graph", action="store_true", help="eager steps (default: the step captured as one HIP "
-                    "graph and replayed, STCGAN.capture; the same kernels, bit-identical results)")
+    ap.add_argument("--graph", action="store_true", help="replay the step captured as one HIP graph "
+                    "(STCGAN.capture; the same kernels, bit-identical results) instead of eager steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the parity / other-config measurements")
     ap.add_argument("--cpu-batch", type=int, default=32, help="batch of the timed CPU train step (C3: 32)")
@@ -375,7 +375,7 @@ def main():
         net.train()
 
     step, mode = (lambda: tr.train_step(x, m, y)), "eager"
-    if not args.no_graph:
+    if args.graph:
         try:  # (a capture failure, e.g. a backend that cannot be captured, falls back to eager steps)
             step, mode = tr.capture(x, m, y, warmup=1), "hip-graph"
         except Exception as e:  # noqa: BLE001

@@ -17,7 +17,7 @@ from stcgan_amd import ops  # noqa: E402
 from stcgan_amd.stcgan import STCGAN  # noqa: E402
 
 BF = torch.bfloat16
-NCFG = 24
+NCFG = 29
 
 
 def record():
@@ -122,8 +122,12 @@ def main():
         flops = 2.0 * B * gh * gw * nph * cout * taps * cin
         t_auto = bench(prob, None)
         res = {}
-        for cfg in range(NCFG):
-            for ks in (1, 2, 4, 8, 16):
+        cfgs = [int(c) for c in os.environ["TUNE_CFGS"].split(",")] if os.environ.get("TUNE_CFGS") else range(NCFG)
+        kss = [int(k) for k in os.environ.get("TUNE_KS", "1,2,4,8,16").split(",")]
+        if os.environ.get("TUNE_CFGS"):  # a focused sweep also times the automatic plan's own config
+            cfgs = sorted(set(cfgs) | {plan[4]})
+        for cfg in cfgs:
+            for ks in kss:
                 t = bench(prob, (cfg, ks), reps=5)
                 if t is not None:
                     res[(cfg, ks)] = t

@@ -849,6 +849,11 @@ static const TileCfg kTiles[] = {
     {128, 128, 2, 2, 2, 32},  // 21
     {256, 128, 4, 2, 3, 32},  // 22
     {128, 64, 2, 2, 3, 32},   // 23
+    {128, 128, 2, 4, 2, 64},  // 24: 8 waves of 64x32 (4 waves per SIMD at 2 blocks per CU)
+    {128, 128, 4, 2, 2, 64},  // 25: 8 waves of 32x64
+    {128, 64, 4, 2, 2, 64},   // 26: 8 waves of 32x32
+    {256, 128, 4, 4, 2, 64},  // 27: 16 waves of 64x32
+    {128, 256, 4, 4, 2, 64},  // 28: 16 waves of 32x64
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -1027,6 +1032,11 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     STC_B(21, 128, 128, 2, 2, 2, 32)
     STC_B(22, 256, 128, 4, 2, 3, 32)
     STC_B(23, 128, 64, 2, 2, 3, 32)
+    STC_B(24, 128, 128, 2, 4, 2, 64)
+    STC_B(25, 128, 128, 4, 2, 2, 64)
+    STC_B(26, 128, 64, 4, 2, 2, 64)
+    STC_B(27, 256, 128, 4, 4, 2, 64)
+    STC_B(28, 128, 256, 4, 4, 2, 64)
     default:
       return fail(-1, "bf16 igemm: bad tile config %d", pl.cfg);
   }

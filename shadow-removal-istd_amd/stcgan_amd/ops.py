@@ -141,7 +141,9 @@ _BF16_TILES = [(128, 128, 2, 2, 2, 64), (256, 128, 2, 2, 2, 64), (128, 64, 2, 2,
                (128, 128, 2, 2, 3, 64), (128, 256, 2, 4, 3, 64), (64, 128, 1, 4, 3, 64), (128, 64, 2, 2, 3, 64),
                (64, 64, 2, 2, 3, 64), (256, 128, 4, 2, 3, 64), (256, 256, 2, 4, 4, 32), (256, 128, 4, 2, 4, 32),
                (128, 256, 2, 4, 4, 32), (128, 128, 2, 2, 4, 32), (128, 64, 2, 2, 4, 32), (64, 64, 2, 2, 4, 32),
-               (128, 128, 2, 2, 3, 32), (128, 128, 2, 2, 2, 32), (256, 128, 4, 2, 3, 32), (128, 64, 2, 2, 3, 32)]
+               (128, 128, 2, 2, 3, 32), (128, 128, 2, 2, 2, 32), (256, 128, 4, 2, 3, 32), (128, 64, 2, 2, 3, 32),
+               (128, 128, 2, 4, 2, 64), (128, 128, 4, 2, 2, 64), (128, 64, 4, 2, 2, 64), (256, 128, 4, 4, 2, 64),
+               (128, 256, 4, 4, 2, 64)]
 
 
 def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):

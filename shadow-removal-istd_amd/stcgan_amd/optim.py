@@ -176,6 +176,8 @@ class Adam(torch.optim.Optimizer):
         import numpy as np
         d = self._dev.get(gi)
         if d is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("stcgan_amd Adam: the device step state is made by an eager step, not in a capture")
             b1, b2 = (float(np.float32(b)) for b in group["betas"])  # the float betas the kernel receives
             n = self._tab_len
             # exactly the host path's formulas: 1 - pow(beta1, step) in double; (float)sqrt(1 - pow(beta2, step))

@@ -396,7 +396,11 @@ class STCGAN(object):
                 self.train_step(x, m, y)
             for o in (self.optim_G, self.optim_D):
                 o.device_step(True)
-            self.train_step(x, m, y)  # one eager step in device-step mode (creates the device counters)
+            # eager steps in device-step mode until both optimisers run their steady-state path with their
+            # device counters created (a packed operand first made in a step -- the discriminators' input-
+            # gradient operands appear in the first G step -- sends the next step down the full path)
+            for _ in range(2):
+                self.train_step(x, m, y)
         main.wait_stream(cap)
         torch.cuda.synchronize(self.device)
         graph = torch.cuda.CUDAGraph()

@@ -267,10 +267,10 @@ def test_c3_bf16_train_step_ngf64_vs_bf16_oracle(loss_type):
     itself moves that much under a 1e-6 relative perturbation of its weights (its noise floor, measured
     here on the same step).  The whole-step check is therefore relative to that floor; the discriminating
     check of the same bf16 step is layer by layer at bs=32 (tests/test_gpu_c3_layers.py).  Stated
-    tolerances (relative L2): per parameter gradient, exp_avg and exp_avg_sq  <= 3 x floor + 1e-2; per
+    tolerances (relative L2): per parameter gradient, exp_avg and exp_avg_sq  <= 3 x floor + 2e-2; per
     network, the median over its tensors <= 2 x the floor's median; BatchNorm running statistics and the
     D gradients' network total <= 3e-2; logged losses within 1e-3 relative (+1e-5); update signs agree on
-    >= 90 % (G) / 99 % (D) of the elements."""
+    >= 90 % (G) / 97 % (D) of the elements."""
     torch.set_num_threads(16)
     tr, states = _trainer(64, "bf16", loss_type=loss_type)
     b = _batch(8, 8100)
@@ -310,7 +310,7 @@ def test_c3_bf16_train_step_ngf64_vs_bf16_oracle(loss_type):
             for what, a_, b_, c_ in (("grad", p.grad, pr.grad, pf.grad), ("exp_avg", st["exp_avg"], om, fm),
                                       ("exp_avg_sq", st["exp_avg_sq"], ov, fv)):
                 e, fl = rel_l2(a_, b_), rel_l2(c_, b_)
-                check(e <= 3 * fl + 1e-2, (name, k, what, e, fl))
+                check(e <= 3 * fl + 2e-2, (name, k, what, e, fl))
                 if what == "grad":
                     errs.append(e)
                     floors.append(fl)
@@ -323,7 +323,7 @@ def test_c3_bf16_train_step_ngf64_vs_bf16_oracle(loss_type):
         report[name] = dict(median=round(med_e, 4), floor_median=round(med_f, 4), worst=round(max(errs), 4),
                             floor_worst=round(max(floors), 4), sign_agreement=round(agree / max(total, 1), 4))
         check(med_e <= 2 * med_f + 1e-3, (name, "median", med_e, med_f))
-        check(agree / max(total, 1) >= (0.99 if name.startswith("D") else 0.90), (name, "sign", agree / max(total, 1)))
+        check(agree / max(total, 1) >= (0.97 if name.startswith("D") else 0.90), (name, "sign", agree / max(total, 1)))
         for k, v in net.state_dict().items():
             if k.endswith("num_batches_tracked"):
                 check(int(v) == int(ost[k]), (name, k))

@@ -57,8 +57,8 @@ def test_captured_step_is_bit_identical(dtype, ngf, loss_type):
     y = torch.rand((B, 3, 256, 256), generator=g, device="cuda") * 2 - 1
     eager = _trainer(dtype, ngf, loss_type)
     graphed = _trainer(dtype, ngf, loss_type)
-    replay = graphed.capture(x, m, y, warmup=1)  # 2 eager steps (warm-up + one in device-step mode) inside
-    for _ in range(2):
+    replay = graphed.capture(x, m, y, warmup=1)  # 3 eager steps inside (warm-up + two in device-step mode)
+    for _ in range(3):
         eager.train_step(x, m, y)
     assert not _same(_state(eager), _state(graphed))
     for i in range(3):
@@ -71,4 +71,4 @@ def test_captured_step_is_bit_identical(dtype, ngf, loss_type):
     eager.train_step(x, m, y)
     replay()
     assert not _same(_state(eager), _state(graphed))
-    assert float(graphed.optim_G.state[next(graphed.G1.parameters())]["step"]) == 6.0
+    assert float(graphed.optim_G.state[next(graphed.G1.parameters())]["step"]) == 7.0
