@@ -381,6 +381,16 @@ int stc_adam_pack_step(const int64_t* table, int ntensors, int64_t total_blocks,
 int stc_adam_pack_step_dev(const int64_t* table, int ntensors, int64_t total_blocks, int64_t* step_dev,
                            const double* lr_dev, const double* bc1_tab, const float* bc2s_tab, int tab_len,
                            float* coef_dev, float beta1, float beta2, float eps, void* stream);
+/* The update of one optimiser step split over several launches -- each a table of a subset of the
+ * parameters, launched as the backward completes their gradients (the optimiser overlapped with the
+ * backward; torch.optim.Adam.step() of STCGAN/stcgan.py:229/303 updates every tensor independently, so
+ * the split changes no result).  stc_adam_coef_dev: the device step count advanced once for the step
+ * (the first half of stc_adam_pack_step_dev).  stc_adam_pack_apply: one table launch with either the
+ * host coefficients of (lr, step) (coef_dev == NULL, as stc_adam_pack_step) or the device ones.      */
+int stc_adam_coef_dev(int64_t* step_dev, const double* lr_dev, const double* bc1_tab, const float* bc2s_tab,
+                      int tab_len, float* coef_dev, void* stream);
+int stc_adam_pack_apply(const int64_t* table, int ntensors, int64_t total_blocks, float lr, int step,
+                        const float* coef_dev, float beta1, float beta2, float eps, void* stream);
 /* dst[e] += src[e] (fp32, numel[e] elements) for ntensors <= 16 tensors in one launch (host arrays of
  * device pointers).  Sums the weight gradients of two calls of one network inside one differentiated
  * graph -- the discriminators' real and fake calls, STCGAN/stcgan.py:215-227 -- which autograd would

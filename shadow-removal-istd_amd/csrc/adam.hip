@@ -288,6 +288,36 @@ extern "C" int stc_adam_pack_step_dev(const int64_t* table, int ntensors, int64_
   return 0;
 }
 
+// The two halves of stc_adam_pack_step_dev, for an update split into several launches (the buckets of a
+// network's gradients updated as the backward completes them, optim.Adam overlap): the step count advanced
+// once, then any number of table launches reading its coefficients.
+extern "C" int stc_adam_coef_dev(int64_t* step_dev, const double* lr_dev, const double* bc1_tab, const float* bc2s_tab,
+                                 int tab_len, float* coef_dev, void* stream) {
+  STC_REQUIRE(step_dev && lr_dev && bc1_tab && bc2s_tab && coef_dev && tab_len >= 2, "stc_adam_coef_dev: bad arguments");
+  hipLaunchKernelGGL(adam_coef_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (long long*)step_dev, lr_dev, bc1_tab,
+                     bc2s_tab, tab_len, coef_dev);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
+// One table launch of the update with host coefficients (coef_dev == nullptr: lr / (1 - beta1^step) and
+// sqrt(1 - beta2^step) computed here exactly as stc_adam_pack_step) or the device ones stc_adam_coef_dev wrote.
+extern "C" int stc_adam_pack_apply(const int64_t* table, int ntensors, int64_t total_blocks, float lr, int step,
+                                   const float* coef_dev, float beta1, float beta2, float eps, void* stream) {
+  STC_REQUIRE(ntensors > 0 && (coef_dev != nullptr || step >= 1), "stc_adam_pack_apply: bad arguments");
+  float lbc1 = 0.f, bc2s = 1.f;
+  if (coef_dev == nullptr) {
+    const double bc1 = 1.0 - pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - pow((double)beta2, (double)step);
+    lbc1 = (float)((double)lr / bc1);
+    bc2s = (float)sqrt(bc2);
+  }
+  hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const long long*)table, ntensors, lbc1, bc2s, beta1, beta2, eps, coef_dev);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int stc_adam_step(const int64_t* table, int ntensors, int64_t total_blocks, float lr, float beta1,
                              float beta2, float eps, int step, void* stream) {
   STC_REQUIRE(ntensors > 0 && step >= 1, "stc_adam_step: bad arguments");

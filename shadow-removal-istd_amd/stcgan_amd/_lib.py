@@ -88,6 +88,8 @@ _SIGS = {
     "stc_conv_wgrad_rows_workspace": (_i64, [_i32, _i32, _i32, _i32]),
     "stc_adam_pack_step": (_i32, [_vp, _i32, _i64, _f32, _f32, _f32, _f32, _i32, _vp]),
     "stc_adam_pack_step_dev": (_i32, [_vp, _i32, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _f32, _f32, _f32, _vp]),
+    "stc_adam_coef_dev": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "stc_adam_pack_apply": (_i32, [_vp, _i32, _i64, _f32, _i32, _vp, _f32, _f32, _f32, _vp]),
     "stc_grad_accumulate": (_i32, [_i32, _vp, _vp, _vp, _vp]),
     "stc_infer_output": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "stc_istd_errors_workspace": (_i64, [_i32, _i32, _i32]),

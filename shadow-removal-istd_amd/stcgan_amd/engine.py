@@ -56,12 +56,21 @@ WGRAD_OVERLAP = True
 # interleaved A/B (scripts/train_steps.py --ab): none 13.74, <= 32x32 13.45, <= 64x64 13.64, all 13.75 ms/step
 WGRAD_OVERLAP_MAX_PIX = 32 * 32
 _WG_SIDE = {}
+# streams (raw handles) whose backward keeps its weight gradients on the stream itself while a HIP graph
+# is being captured: the discriminator lanes (STCGAN.capture).  A weight-gradient side stream forked from a
+# lane, itself forked from the capturing stream, made the capture's end fault on this ROCm (round-3 probe:
+# scripts/graph_capture_probe.py -- lanes alone and side streams of the main stream alone capture fine).
+NO_SIDE_IN_CAPTURE = set()
 
 
 class _WgradLane:
     def __init__(self):
         self.cur = torch.cuda.current_stream() if WGRAD_OVERLAP else None
         self.side = None
+        self.last_side = False
+        if (self.cur is not None and self.cur.cuda_stream in NO_SIDE_IN_CAPTURE
+                and torch.cuda.is_current_stream_capturing()):
+            self.cur = None
         if self.cur is not None:
             self.side = _WG_SIDE.get(self.cur.cuda_stream)
             if self.side is None:
@@ -309,7 +318,6 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
             lane.run(lambda k=k, dqv=dqv, cin_t=cin_t, cg=cg, cout_t=cout_t, out=W.dest(wT): ops.wgrad(
                 B, 2, L.nhwc_view(cr[k]), cin_t, dqv, cg, cout_t, dt, device=dev, out=out), dq,
                 pixels=S[k + 1][0] * S[k + 1][1])
-            W.done([wT], lane)
         wd = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_DGRAD, cin_t, cg, dt)
         if k < Lv - 1:
             ah, aw = _pad2(S, k + 1)
@@ -319,6 +327,8 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
         _trace("G", ("gcat", k), gcat[k])
         if k == Lv - 1:
             ops.conv(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt)
+            if need_w:  # (after the last read of the weight: the optimiser may update it from here on)
+                W.done([plan.convT[k].weight], lane)
             break
         # BN_up[k+1] over q_{k+1}: full (padded) extent; the cropped rows carry zero gradient.
         # Its gradient is the second half of gcat[k] (ReLU of the concat), so the BN reduction
@@ -334,6 +344,7 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
                              gamma=bn.weight, s_self=0.0, ch_off=C, dxv=L.nhwc_view(dq),
                              dgamma=dest(bn.weight), dbeta=dest(bn.bias))
         if need_w:
+            W.done([plan.convT[k].weight], lane)
             W.done([bn.weight, bn.bias])
         _trace("G", ("dq", k + 1), dq)
     # ---- innermost r_{L-1}: ReLU backward (no BN)
@@ -351,7 +362,6 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
                 lane.run(lambda drv=drv, out=W.dest(w0): ops.wgrad(
                     B, 2, drv, co[0], L.nhwc_view(xin), saved["cin_pad"], saved["cin"], dt, device=dev, out=out),
                     dr, pixels=S[1][0] * S[1][1])
-                W.done([w0], lane)
             if need_src:
                 wd = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_DGRAD, saved["cin_pad"], co[0], dt)
                 gx = _nhwc(B, 2 * S[1][0], 2 * S[1][1], saved["cin_pad"], dt, dev)
@@ -361,6 +371,8 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
                 src_grads = [torch.empty((B, c, H, W_), dtype=torch.float32, device=dev) if nd else None
                              for c, nd in zip(saved["src_c"], need_src)]
                 ops.scatter(gx, src_grads, saved["src_c"], dt, H, W_)
+            if need_w:
+                W.done([plan.conv[0].weight], lane)
             break
         cprev = co[k - 1]
         if need_w:  # D = dr_k (grid S[k+1]), G = conv_k input = ad[k-1]
@@ -368,7 +380,6 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
             lane.run(lambda k=k, drv=drv, cprev=cprev, out=W.dest(wk): ops.wgrad(
                 B, 2, drv, co[k], L.nhwc_view(ad[k - 1]), cprev, cprev, dt, device=dev, out=out), dr,
                 pixels=S[k + 1][0] * S[k + 1][1])
-            W.done([wk], lane)
         wd = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_DGRAD, cprev, co[k], dt)
         ga = _nhwc(B, 2 * S[k + 1][0], 2 * S[k + 1][1], cprev, dt, dev)
         _trace("G", ("ga", k), ga)
@@ -378,6 +389,8 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
         g1 = L.nhwc_view(gcat[k - 1], 0, *S[k])
         if k - 1 == 0:
             ops.conv(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt)
+            if need_w:
+                W.done([plan.conv[k].weight], lane)
             ops.bn_backward(B, xv, cprev, dt, L.nhwc_view(dr), g1=g1, s1=0.0, g2=L.nhwc_view(ga, 0, *S[k]), s2=LRELU)
         else:  # BN reduction fused into the input-gradient conv that produces ga
             mean, rstd = st_d[k - 1]
@@ -388,6 +401,7 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
                                  g_other=g1, s_other=0.0, dxv=L.nhwc_view(dr), dgamma=dest(bn.weight),
                                  dbeta=dest(bn.bias))
             if need_w:
+                W.done([plan.conv[k].weight], lane)
                 W.done([bn.weight, bn.bias])
     if lane is not None:
         lane.join()
@@ -530,7 +544,7 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, W):
                 if cv.bias is not None:
                     ops.chan_sum(B, gv, gch, cout, dt, dev, out=db_out)
             lane.run(wg, g, pixels=h * w)
-            W.done([cv.weight] + ([cv.bias] if cv.bias is not None else []), lane)
+        own = [cv.weight] + ([cv.bias] if cv.bias is not None else [])
         if i == 0:
             if need_src:
                 wd = ops.packed(cache, cv.weight, L.PACK_CONV_DGRAD, saved["cin_pad"], gch, dt)
@@ -541,6 +555,8 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, W):
                 src_grads = [torch.empty((B, c, H, W_), dtype=torch.float32, device=dev) if nd else None
                              for c, nd in zip(saved["src_c"], need_src)]
                 ops.scatter(gx, src_grads, saved["src_c"], dt, H, W_)
+            if need_w:
+                W.done(own, lane)
             break
         # input gradient of conv_i (grad wrt act[i])
         ph, pw = dims[i]
@@ -559,6 +575,8 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, W):
         xv = L.nhwc_view(raw[i])
         if tabs[i] is None:
             ops.conv(dkind, B, gv, gch, wd, cin, L.nhwc_view(ga), dt)
+            if need_w:
+                W.done(own, lane)
             ops.bn_backward(B, xv, cin, dt, L.nhwc_view(gn), g1=L.nhwc_view(ga), s1=LRELU)
         else:
             mean, rstd = stats[i]
@@ -569,6 +587,7 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, W):
                                  dgamma=W.dest(bn.weight) if need_w else None,
                                  dbeta=W.dest(bn.bias) if need_w else None)
             if need_w:
+                W.done(own, lane)
                 W.done([bn.weight, bn.bias])
         g, gch, h, w = gn, cin, ph, pw
     if lane is not None:

@@ -23,6 +23,10 @@ class Adam(torch.optim.Optimizer):
         self._epb = None
         self.fuse_pack = True  # False: update only (the packed operands are then refreshed lazily)
         self._dev = None  # device-resident step counts (device_step), per group
+        self._ov_stream = None  # overlap(): the side stream of the per-bucket updates
+        self._ov_done = {}      # group -> {position in the group's steady-state plist} updated this step
+        self._ov_coef = set()   # groups whose device step count this step already advanced
+        self._gi_of = None
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -30,75 +34,89 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._init_state()
+        for gi, group in enumerate(self.param_groups):
+            done = self._ov_done.pop(gi, None)
+            if done:
+                self._finish_overlap(gi, group, done)
+                continue
+            if self._fast_step(gi, group):
+                continue
+            self._full_step(gi, group)
+        self._ov_coef.clear()
+        return loss
+
+    def _init_state(self):
         if self._epb is None:
             self._epb = lib().stc_adam_elems_per_block()
             self._steps = {}    # id(param) -> (state step tensor, its value as a Python int)
             self._tables = {}   # (group, step) -> (pointer key, device table, blocks)
             self._fast = {}     # group -> the last step's table and per-parameter records (see _fast_step)
-        for gi, group in enumerate(self.param_groups):
-            if self._fast_step(gi, group):
+
+    def _full_step(self, gi, group, skip=()):
+        """The general path (first steps, moved tensors, new packed operands); ``skip``: parameters already
+        updated this step (by overlap), left out."""
+        b1, b2 = group["betas"]
+        # group params by step count (all equal in practice).  The step count is mirrored in a
+        # Python int (no per-parameter tensor op / .item() on the host path), and the state's
+        # "step" tensors are advanced with one foreach call.
+        by_step, step_tensors = {}, []
+        for p in group["params"]:
+            if p.grad is None or id(p) in skip:
                 continue
-            b1, b2 = group["betas"]
-            # group params by step count (all equal in practice).  The step count is mirrored in a
-            # Python int (no per-parameter tensor op / .item() on the host path), and the state's
-            # "step" tensors are advanced with one foreach call.
-            by_step, step_tensors = {}, []
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
-                if not p.is_cuda or p.dtype != torch.float32:
-                    raise RuntimeError("stcgan_amd Adam: fp32 CUDA parameters only")
-                if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
-                    p.grad = p.grad.float().contiguous()
-                st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                mirror = self._steps.get(id(p))
-                n = mirror[1] + 1 if mirror is not None and mirror[0] is st["step"] else int(st["step"].item()) + 1
-                self._steps[id(p)] = (st["step"], n)
-                step_tensors.append(st["step"])
-                by_step.setdefault(n, []).append(p)
-            if step_tensors:
-                torch._foreach_add_(step_tensors, 1.0)
-            for step, plist in by_step.items():
-                recs = [self._record(p) for p in plist]
-                key = tuple(r[0] for r in recs)
-                cached = self._tables.get(gi)
-                if cached is not None and cached[0] == key:
-                    table, blocks = cached[1], cached[2]
-                else:
-                    # pointer table, rebuilt when a tensor or packed operand moved (the gradients are new
-                    # tensors every step, so in practice every step: a few hundred rows)
-                    rows, blocks = [], 0
-                    for row, nblk, _ in recs:
-                        rows.append(list(row[:5]) + [blocks] + list(row[5:]))
-                        blocks += nblk
-                    # pinned + non_blocking: a stream-ordered copy -- a pageable H2D copy would block the
-                    # host until the GPU has drained everything queued before it (one full step)
-                    table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(plist[0].device, non_blocking=True)
-                    self._tables[gi] = (key, table, blocks)
-                check(lib().stc_adam_pack_step(ptr(table), len(key), blocks, float(group["lr"]), float(b1),
-                                               float(b2), float(group["eps"]), int(step), stream()),
-                      "stc_adam_pack_step")
-                ops.bump(plist)
-                for p, (_, _, targets) in zip(plist, recs):  # the packed operands written above are current
-                    ver = ops.pack_version(p)
-                    for (pkey, cache, out) in targets:
-                        cache[pkey] = (ver, out)
-            self._fast.pop(gi, None)
-            if len(by_step) == 1:
-                (step, plist), = by_step.items()
-                recs = [self._record(p) for p in plist]
-                self._fast[gi] = dict(
-                    key=tuple((id(p), p.data_ptr(), p.grad.data_ptr()) for p in plist), plist=plist,
-                    rows=[list(r[0]) for r in recs], table=self._tables[gi][1], blocks=self._tables[gi][2],
-                    targets=[r[2] for r in recs], step=step, epoch=ops.PACK_EPOCH,
-                    step_tensors=[self.state[p]["step"] for p in plist])
-                f = self._fast[gi]
-                f["tables"] = {f["key"]: (f["table"], f["blocks"])}
-        return loss
+            if not p.is_cuda or p.dtype != torch.float32:
+                raise RuntimeError("stcgan_amd Adam: fp32 CUDA parameters only")
+            if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
+                p.grad = p.grad.float().contiguous()
+            st = self.state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            mirror = self._steps.get(id(p))
+            n = mirror[1] + 1 if mirror is not None and mirror[0] is st["step"] else int(st["step"].item()) + 1
+            self._steps[id(p)] = (st["step"], n)
+            step_tensors.append(st["step"])
+            by_step.setdefault(n, []).append(p)
+        if step_tensors:
+            torch._foreach_add_(step_tensors, 1.0)
+        for step, plist in by_step.items():
+            recs = [self._record(p) for p in plist]
+            key = tuple(r[0] for r in recs)
+            cached = self._tables.get(gi)
+            if cached is not None and cached[0] == key:
+                table, blocks = cached[1], cached[2]
+            else:
+                # pointer table, rebuilt when a tensor or packed operand moved (the gradients are new
+                # tensors every step, so in practice every step: a few hundred rows)
+                rows, blocks = [], 0
+                for row, nblk, _ in recs:
+                    rows.append(list(row[:5]) + [blocks] + list(row[5:]))
+                    blocks += nblk
+                # pinned + non_blocking: a stream-ordered copy -- a pageable H2D copy would block the
+                # host until the GPU has drained everything queued before it (one full step)
+                table = torch.tensor(rows, dtype=torch.int64).pin_memory().to(plist[0].device, non_blocking=True)
+                self._tables[gi] = (key, table, blocks)
+            check(lib().stc_adam_pack_step(ptr(table), len(key), blocks, float(group["lr"]), float(b1),
+                                           float(b2), float(group["eps"]), int(step), stream()),
+                  "stc_adam_pack_step")
+            ops.bump(plist)
+            for p, (_, _, targets) in zip(plist, recs):  # the packed operands written above are current
+                ver = ops.pack_version(p)
+                for (pkey, cache, out) in targets:
+                    cache[pkey] = (ver, out)
+        self._fast.pop(gi, None)
+        if len(by_step) == 1 and not skip:
+            (step, plist), = by_step.items()
+            recs = [self._record(p) for p in plist]
+            self._fast[gi] = dict(
+                key=tuple((id(p), p.data_ptr(), p.grad.data_ptr()) for p in plist), plist=plist,
+                rows=[list(r[0]) for r in recs], table=self._tables[gi][1], blocks=self._tables[gi][2],
+                targets=[r[2] for r in recs], step=step, epoch=ops.PACK_EPOCH,
+                step_tensors=[self.state[p]["step"] for p in plist],
+                index={id(p): i for i, p in enumerate(plist)}, subs={})
+            f = self._fast[gi]
+            f["tables"] = {f["key"]: (f["table"], f["blocks"])}
 
     def _fast_step(self, gi, group):
         """The steady-state step of a group without per-parameter record building: valid while the
@@ -137,6 +155,7 @@ class Adam(torch.optim.Optimizer):
                 hit = f["tables"][key] = (table, blocks)
             f["table"], f["blocks"] = hit
             f["key"] = key
+            f["subs"] = {}  # subset tables hold the old gradient addresses
             self._tables[gi] = (None, f["table"], f["blocks"])
         step = f["step"] + 1
         b1, b2 = group["betas"]
@@ -158,6 +177,139 @@ class Adam(torch.optim.Optimizer):
                     cache[pkey] = (ver, out)
         f["step"] = step
         return True
+
+    # ------------------------------------------------------------------ overlap with the backward
+    def overlap(self, exchanges, on=True):
+        """Update the parameters bucket by bucket while the backward still runs.  Each network's gradient
+        buckets (parallel.BucketExchange, fed by engine.GradWriter) are handed over the moment the backward
+        has written them and no longer reads their parameters (a layer is reported after its input-gradient
+        convolution); the bucket's update is launched on a side stream ordered after the streams that wrote
+        it and after its all-reduce.  ``step()`` updates what is left and joins the side stream.  Every
+        tensor's update is the same kernel arithmetic on the same values as one whole-group launch (Adam
+        updates each tensor independently), so results are bit-identical; only the steady state overlaps (a
+        first step, a moved tensor or a new packed operand leaves everything to step())."""
+        for ex in exchanges:
+            ex.on_complete = self._bucket_ready if on else None
+
+    def _bucket_ready(self, params, stream, work):
+        if self._epb is None:
+            return
+        if self._gi_of is None:
+            self._gi_of = {id(p): gi for gi, g in enumerate(self.param_groups) for p in g["params"]}
+        by_group = {}
+        for p in params:
+            gi = self._gi_of.get(id(p))
+            if gi is not None:
+                by_group.setdefault(gi, []).append(p)
+        for gi, ps in by_group.items():
+            self._launch_subset(gi, ps, stream, work)
+
+    def _subset(self, f, sel):
+        """(device table, blocks) of the steady-state records at positions ``sel`` (cached)."""
+        key = tuple(sel)
+        sub = f["subs"].get(key)
+        if sub is None:
+            rows, blocks = [], 0
+            for i in sel:
+                r = f["rows"][i]
+                rows.append(r[:5] + [blocks] + r[5:])
+                blocks += self._nblocks(f["plist"][i], r)
+            dev = f["plist"][0].device
+            sub = f["subs"][key] = (torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True),
+                                    blocks)
+        return sub
+
+    def _launch_subset(self, gi, ps, stream, work):
+        f = self._fast.get(gi)
+        if f is None or f["epoch"] != ops.PACK_EPOCH:
+            return
+        done = self._ov_done.get(gi, {})
+        sel = []
+        for p in ps:
+            i = f["index"].get(id(p))
+            g = p.grad
+            if (i is None or i in done or g is None or g.dtype is not torch.float32 or not g.is_contiguous()
+                    or g.data_ptr() != f["rows"][i][1] or p.data_ptr() != f["rows"][i][0]):
+                return  # left to step()
+            sel.append(i)
+        sel.sort()
+        if tuple(sel) not in f["subs"] and torch.cuda.is_current_stream_capturing():
+            return  # (no table upload inside a capture)
+        table, blocks = self._subset(f, sel)
+        dev = f["plist"][0].device
+        if self._ov_stream is None:
+            self._ov_stream = torch.cuda.Stream(dev)
+        ost = self._ov_stream
+        ost.wait_stream(torch.cuda.current_stream(dev))
+        if stream is not None:
+            ost.wait_stream(stream)
+        with torch.cuda.stream(ost):
+            if work is not None:
+                work.wait()
+            self._apply(gi, f, table, len(sel), blocks)
+        self._ov_done.setdefault(gi, {}).update((i, True) for i in sel)
+
+    def _apply(self, gi, f, table, n, blocks):
+        """One table launch of this step's update of group ``gi`` on the current stream."""
+        group = self.param_groups[gi]
+        b1, b2 = group["betas"]
+        coef = None
+        if self._dev is not None:
+            d = self._dev_state(gi, group, f["step"], f["plist"][0].device)
+            if gi not in self._ov_coef:  # the device step count advances once per step
+                check(lib().stc_adam_coef_dev(ptr(d["step"]), ptr(d["lr_dev"]), ptr(d["bc1"]), ptr(d["bc2s"]),
+                                              d["tab_len"], ptr(d["coef"]), stream()), "stc_adam_coef_dev")
+                self._ov_coef.add(gi)
+            coef = ptr(d["coef"])
+        check(lib().stc_adam_pack_apply(ptr(table), n, blocks, float(group["lr"]), f["step"] + 1, coef, float(b1),
+                                        float(b2), float(group["eps"]), stream()), "stc_adam_pack_apply")
+
+    def _finish_overlap(self, gi, group, done):
+        """step() of a group part of which overlap() already updated this step."""
+        f = self._fast[gi]
+        plist = f["plist"]
+        torch.cuda.current_stream(plist[0].device).wait_stream(self._ov_stream)
+        with_grad = [p for p in group["params"] if p.grad is not None]
+        ok = f["epoch"] == ops.PACK_EPOCH and len(with_grad) == len(plist)
+        rest = []
+        for p in with_grad:
+            i = f["index"].get(id(p))
+            if i is None:
+                ok = False
+                break
+            if i in done:
+                continue
+            g = p.grad
+            if (g.dtype is not torch.float32 or not g.is_contiguous() or g.data_ptr() != f["rows"][i][1]
+                    or p.data_ptr() != f["rows"][i][0]):
+                ok = False
+            rest.append(i)
+        step = f["step"] + 1
+        if ok:
+            if rest:
+                table, blocks = self._subset(f, rest)
+                self._apply(gi, f, table, len(rest), blocks)
+            torch._foreach_add_(f["step_tensors"], 1.0)
+            upd = plist
+        else:  # the rest on the general path; the updated part's host-side state advanced here
+            upd = [plist[i] for i in done]
+            torch._foreach_add_([f["step_tensors"][i] for i in done], 1.0)
+        ops.bump(upd)
+        for p in upd:
+            i = f["index"][id(p)]
+            self._steps[id(p)] = (f["step_tensors"][i], step)
+            ver = ops.pack_version(p)
+            for (pkey, cache, out) in f["targets"][i]:
+                cache[pkey] = (ver, out)
+        if ok:
+            f["step"] = step
+        else:
+            self._full_step(gi, group, skip={id(p) for p in upd})
+
+    def zero_grad(self, set_to_none=True):
+        if self._ov_done:  # a backward overlapped some updates and no step() followed: finish them
+            self.step()
+        super().zero_grad(set_to_none=set_to_none)
 
     # ------------------------------------------------------------------ device-resident step count
     def device_step(self, on=True, tab_len=1 << 17):

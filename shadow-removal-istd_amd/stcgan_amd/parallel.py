@@ -151,14 +151,18 @@ class BucketExchange:
     """Average one FlatGrads over all ranks, bucket by bucket, as the buckets complete.
 
     ``ready(params, stream)``: those parameters' gradients are enqueued (on ``stream``, or the current
-    stream); a bucket is launched once each of its parameters has been reported ``expected`` times (the
-    discriminator's real and fake calls both write into its gradients in the D step).  ``finish()``
+    stream) and the backward no longer reads the parameters themselves; a bucket is complete once each of
+    its parameters has been reported ``expected`` times (the discriminator's real and fake calls both
+    write into its gradients in the D step).  A complete bucket is all-reduced (when ``active``) and then
+    handed to ``on_complete(params, stream, work)`` -- the optimiser's per-bucket update (optim.Adam.overlap)
+    -- when the average is final on the device (world size 1, or RCCL's in-collective AVG).  ``finish()``
     launches whatever is left, makes the current stream wait for every bucket and resets the counts."""
 
     def __init__(self, flat, bucket_mb=32, active=None):
         self.flat = flat
         # active: exchange even at world size 1 (tests drive the collective path on one GPU)
         self.active = (world() > 1) if active is None else bool(active)
+        self.on_complete = None
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) // 4))
         self.ranges, self.members, self.bucket_of = [], [], {}
         cur, start, n = [], 0, 0
@@ -171,6 +175,8 @@ class BucketExchange:
                 cur, start, n = [], o + k, 0
         if cur:
             self._cut(cur, start, flat.numel)
+        by_id = {id(p): p for p in flat.params}
+        self.member_params = [[by_id[i] for i in m] for m in self.members]
         self.expected = 1
         self.launch_order = []  # bucket indices in launch order (diagnostics / tests)
         self.reset()
@@ -203,7 +209,7 @@ class BucketExchange:
         self.launch_order.append(b)
 
     def ready(self, params, stream=None):
-        if not self.active:
+        if not self.active and self.on_complete is None:
             return
         for p in params:
             c = self.count.get(id(p), 0) + 1
@@ -212,7 +218,11 @@ class BucketExchange:
                 b = self.bucket_of[id(p)]
                 self.left[b] -= 1
                 if self.left[b] == 0:
-                    self._launch(b, stream)
+                    if self.active:
+                        self._launch(b, stream)
+                    # gloo sums (the 1/world scale comes in finish): no early consumer then
+                    if self.on_complete is not None and (not self.active or self._op() != dist.ReduceOp.SUM):
+                        self.on_complete(self.member_params[b], stream, self.works[b])
 
     def finish(self):
         w = world()

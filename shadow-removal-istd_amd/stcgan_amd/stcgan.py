@@ -86,12 +86,18 @@ class STCGAN(object):
                             lr=args.lr_D, betas=(args.beta1, args.beta2))
         self.decay_G = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_G, cooldown=10, min_lr=1e-7, factor=0.8)
         self.decay_D = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_D, cooldown=10, min_lr=1e-7, factor=0.8)
-        # data parallelism: each network's gradients (one flat buffer, parallel.FlatGrads) are averaged over
-        # the ranks bucket by bucket while its backward runs (parallel.BucketExchange, fed by the engine)
-        self.bucket_mb = float(getattr(args, "bucket_mb", 32))
-        if parallel.world() > 1:
-            for net in (self.G1, self.G2, self.D1, self.D2):
-                net.grad_exchange = parallel.BucketExchange(parallel.flat_grads(net), self.bucket_mb)
+        # each network's gradients live in one flat buffer (parallel.FlatGrads), cut into buckets that the
+        # engine reports complete while the backward runs (parallel.BucketExchange): with data parallelism each
+        # bucket is averaged over the ranks (RCCL) right then, and the optimiser updates it right after
+        # (optim.Adam.overlap: the update of the deep layers runs under the backward of the shallow ones)
+        world = parallel.world()
+        self.bucket_mb = float(getattr(args, "bucket_mb", 32 if world > 1 else 8))
+        for net in (self.G1, self.G2, self.D1, self.D2):
+            net.grad_exchange = parallel.BucketExchange(parallel.flat_grads(net), self.bucket_mb)
+        self.overlap_optim = bool(getattr(args, "overlap_optim", True))
+        if self.overlap_optim:
+            self.optim_G.overlap([self.G1.grad_exchange, self.G2.grad_exchange])
+            self.optim_D.overlap([self.D1.grad_exchange, self.D2.grad_exchange])
         # discriminators on side HIP streams (train_step / _lanes); off for a strictly serial step
         self.streams = bool(getattr(args, "streams", True))
         self.lane_carry = bool(getattr(args, "lane_carry", True))
@@ -388,7 +394,10 @@ class STCGAN(object):
         import torch.distributed as dist
         if parallel.world() > 1 and dist.get_backend() != "nccl":
             raise RuntimeError("STCGAN.capture: multi-process capture needs the nccl (RCCL) backend")
-        main = torch.cuda.current_stream(self.device)
+        from . import engine
+        main, l1, l2 = self._lanes()
+        if l1 is not None:  # (see engine.NO_SIDE_IN_CAPTURE)
+            engine.NO_SIDE_IN_CAPTURE.update((l1.cuda_stream, l2.cuda_stream))
         cap = torch.cuda.Stream(self.device)
         cap.wait_stream(main)
         with torch.cuda.stream(cap):
