@@ -177,42 +177,63 @@ def roofline_of_step(tr, x, m, y, args, B, s):
     """Dominant kernel of one (untimed) train step by summed device time, and the north-star set."""
     import torch
     from stcgan_amd import engine, ops
-    ops._timer = []
-    # one stream (no side-stream networks or weight gradients): each launch's events bracket it alone
-    lanes, tr.streams = tr.streams, False
-    overlap, engine.WGRAD_OVERLAP = engine.WGRAD_OVERLAP, False
-    tr.train_step(x, m, y)
-    torch.cuda.synchronize()
-    launches, ops._timer, tr.streams = ops._timer, None, lanes
-    engine.WGRAD_OVERLAP = overlap
-    per, shapes = {}, {}
-    for name, _single, fl, e0, e1, desc in launches:
-        ms = e0.elapsed_time(e1)
-        a = per.setdefault(name, [0, 0.0, 0.0])
-        a[0] += 1
-        a[1] += fl
-        a[2] += ms
-        shapes.setdefault(name, []).append((round(ms * 1e3, 1), desc))
+    def timed_step(single):
+        # single: one stream (no side-stream networks or weight gradients), so each launch's events bracket
+        # it alone; else the bench's own overlapped step (in situ: kernels share the GPU with the lanes')
+        ops._timer = []
+        lanes, overlap = tr.streams, engine.WGRAD_OVERLAP
+        if single:
+            tr.streams, engine.WGRAD_OVERLAP = False, False
+        tr.train_step(x, m, y)
+        torch.cuda.synchronize()
+        launches, ops._timer = ops._timer, None
+        tr.streams, engine.WGRAD_OVERLAP = lanes, overlap
+        per, shapes = {}, {}
+        for name, _single, fl, e0, e1, desc in launches:
+            ms = e0.elapsed_time(e1)
+            a = per.setdefault(name, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += fl
+            a[2] += ms
+            shapes.setdefault(name, []).append((round(ms * 1e3, 1), desc))
+        return launches, per, shapes
+
+    launches, per, shapes = timed_step(True)
     dom = max(per, key=lambda k: per[k][2])
     n_dom, fl_dom, ms_dom = per[dom]
     peak = PEAK_TFLOPS[args.dtype]
     achieved = fl_dom / (ms_dom * 1e-3) / 1e12
-    # the north-star kernel set: one train-mode G1+G2 forward (770.95 GFLOP at bs=32, 256^2), HIP events
+    _, per_situ, _ = timed_step(False)
+    n_s, fl_s, ms_s = per_situ.get(dom, (n_dom, fl_dom, float("nan")))
+    achieved_situ = fl_s / (ms_s * 1e-3) / 1e12
+    # the north-star kernel set: one train-mode G1+G2 forward (770.95 GFLOP at bs=32, 256^2), HIP events;
+    # in the bench dtype and in the other one (the reference computes in fp32)
     flops = gen_fwd_flops(3, 1, args.ngf, B, s, s) + gen_fwd_flops(4, 3, args.ngf, B, s, s)
-    with torch.no_grad():
-        mp = tr.G1(x)
-        tr.G2([x, mp])
-        reps = 3
-        st = torch.cuda.current_stream()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record(st)
-        for _ in range(reps):
+
+    def fwd_ms_of():
+        with torch.no_grad():
             mp = tr.G1(x)
             tr.G2([x, mp])
-        ev1.record(st)
-        ev1.synchronize()
-        fwd_ms = ev0.elapsed_time(ev1) / reps
+            reps = 3
+            st = torch.cuda.current_stream()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record(st)
+            for _ in range(reps):
+                mp = tr.G1(x)
+                tr.G2([x, mp])
+            ev1.record(st)
+            ev1.synchronize()
+            return ev0.elapsed_time(ev1) / reps
+
+    fwd_ms = fwd_ms_of()
     set_tf = flops / (fwd_ms * 1e-3) / 1e12
+    other = "fp32" if args.dtype == "bf16" else "bf16"
+    for g in (tr.G1, tr.G2):
+        g.set_compute_dtype(other)
+    fwd_ms_o = fwd_ms_of()
+    for g in (tr.G1, tr.G2):
+        g.set_compute_dtype(args.dtype)
+    set_tf_o = flops / (fwd_ms_o * 1e-3) / 1e12
     top = sorted(per.items(), key=lambda kv: -kv[1][2])[:10]
     # HBM traffic per launch of the dominant kernel: rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; gfx950
     # FETCH_SIZE x2 correction) over the bench command, committed under profiles/<round>/pmc_traffic.json
@@ -233,8 +254,12 @@ def roofline_of_step(tr, x, m, y, args, B, s):
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_src": traffic_src,
+            "frac_mode": "single-stream step (each launch alone); frac_in_situ: the same kernel in the bench's "
+                         "overlapped step (side-stream networks and weight gradients on)",
+            "achieved_in_situ": round(achieved_situ, 2), "frac_in_situ": round(achieved_situ / peak, 4),
             "kernel": f"{dom}: {n_dom} launches in one train step, {fl_dom / 1e9:.2f} GFLOP, {ms_dom:.3f} ms, "
-                      f"avg {ms_dom / n_dom * 1e3:.1f} us/launch (HIP events around the main kernel)",
+                      f"avg {ms_dom / n_dom * 1e3:.1f} us/launch single-stream, {ms_s / max(n_s, 1) * 1e3:.1f} us "
+                      f"in situ (HIP events around the main kernel)",
             "dominant_launches_us": shapes[dom][:40],
             "per_kernel": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 2), "ms": round(v[2], 3),
                                "avg_us": round(v[2] / v[0] * 1e3, 1),
@@ -242,7 +267,10 @@ def roofline_of_step(tr, x, m, y, args, B, s):
             "gemm_kernels_all": {"launches": len(launches), "gflop": round(conv_gf, 2), "ms": round(conv_ms, 3),
                                  "frac": round(conv_gf / conv_ms / peak, 4)},
             "g1g2_forward": {"gflop": round(flops / 1e9, 2), "ms": round(fwd_ms, 3), "tflops": round(set_tf, 2),
-                             "frac": round(set_tf / peak, 4)},
+                             "frac": round(set_tf / peak, 4), "dtype": args.dtype},
+            f"g1g2_forward_{other}": {"gflop": round(flops / 1e9, 2), "ms": round(fwd_ms_o, 3),
+                                      "tflops": round(set_tf_o, 2), "frac": round(set_tf_o / PEAK_TFLOPS[other], 4),
+                                      "dtype": other},
             "g1g2_forward_frac": round(set_tf / peak, 4)}
 
 
@@ -282,7 +310,8 @@ def g2_parity(args, local):
 
 def other_configs(args, local):
     """C2: G1+G2 forward+backward with the L1 data losses, bs=16, fp32 (parity mode); C5: 480x640
-    G1->G2 eval-mode inference, bs=8, in the bench dtype.  images/s, HIP events, random init."""
+    G1->G2 eval-mode inference, bs=8, in the bench dtype; C3 in fp32: the full train step at the bench
+    batch computed at the reference's precision.  images/s, HIP events, random init."""
     import torch
     from stcgan_amd import loss, networks
     dev = torch.device("cuda", local)
@@ -335,6 +364,22 @@ def other_configs(args, local):
     res[f"C5_infer_480x640_bs8_{args.dtype}"] = {"images_per_s": round(8 / (ms * 1e-3), 2),
                                                   "ms_per_iter": round(ms, 3),
                                                   "tflops": round(113.29e9 * 8 / (ms * 1e-3) / 1e12, 2)}
+    del g1, g2
+    torch.cuda.empty_cache()
+    # C3 at the reference's own precision: the full train step (bench workload, bs=32) computed in fp32
+    tr = make_trainer(args.ngf, "fp32", local)
+    for net in (tr.G1, tr.G2, tr.D1, tr.D2):
+        net.train()
+    B = args.batch
+    x3 = torch.rand((B, 3, 256, 256), generator=gen, device=dev) * 2 - 1
+    m3 = (torch.rand((B, 1, 256, 256), generator=gen, device=dev) < 0.5).float() * 2 - 1
+    y3 = torch.rand((B, 3, 256, 256), generator=gen, device=dev) * 2 - 1
+    tr.train_step(x3, m3, y3)
+    ms = timed(lambda: tr.train_step(x3, m3, y3), 3)
+    res[f"C3_train_step_bs{B}_fp32"] = {"images_per_s": round(B / (ms * 1e-3), 2), "ms_per_step": round(ms, 3),
+                                        "tflops": round(STEP_GFLOP_PER_IMG * B / (ms * 1e-3) / 1e3, 2),
+                                        "frac_fp32_mfma": round(STEP_GFLOP_PER_IMG * B / (ms * 1e-3) / 1e3
+                                                                / PEAK_TFLOPS["fp32"], 4)}
     return res
 
 

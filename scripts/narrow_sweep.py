@@ -1,4 +1,5 @@
-"""Time the narrow-N halo kernel under forced tile shapes {rows, 16-column blocks} (stc_conv_fwd_ex hook)."""
+"""Time the narrow-N kernels under forced tile shapes {rows, 16-column blocks (+16: the row-split
+narrow_halo_kernel instead of the K-split narrow_wk_kernel)} (stc_conv_fwd_ex hook)."""
 import ctypes
 import os
 import sys
@@ -16,9 +17,9 @@ CASES = [  # name, kind, B, grid H, W, cin, cout, out (nchw fp32 + tanh | nhwc b
     ("G out convT 128->1", L.CONVT_S2, 32, 128, 128, 128, 1, "nchw"),
     ("G out convT 128->3", L.CONVT_S2, 32, 128, 128, 128, 3, "nchw"),
     ("e1 dgrad convT 64->8", L.CONVT_S2, 32, 128, 128, 64, 8, "nhwc"),
-    ("D logits s1 512->1", L.CONV_S1, 32, 30, 30, 512, 1, "nhwc"),
+    ("D logits s1 512->1", L.CONV_S1, 32, 30, 30, 512, 1, "nhwc1"),
 ]
-SHAPES = [None, (8, 1), (8, 2), (16, 1), (16, 2), (32, 1)]
+SHAPES = [None, (8, 17), (8, 18), (16, 17), (8, 1), (8, 2), (16, 1), (4, 1), (4, 2)]
 ws = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
 for name, kind, B, gh, gw, cin, cout, out in CASES:
     if kind == L.CONVT_S2:
@@ -39,8 +40,8 @@ for name, kind, B, gh, gw, cin, cout, out in CASES:
     for sh in SHAPES:
         fp = (ctypes.c_int32 * 2)(*sh) if sh else None
         def call():  # noqa: E306
-            check(lib().stc_conv_fwd_ex(L.dtype_code(BF), kind, B, L.nhwc_view(x), cin, ptr(w), cout if out == "nchw" else npad,
-                                        yv, ptr(bias) if out == "nchw" else None, tanh, f32, None, 0, fp, ptr(ws),
+            check(lib().stc_conv_fwd_ex(L.dtype_code(BF), kind, B, L.nhwc_view(x), cin, ptr(w), cout if out != "nhwc" else npad,
+                                        yv, ptr(bias) if out != "nhwc" else None, tanh, f32, None, 0, fp, ptr(ws),
                                         ws.numel(), stream()), "stc_conv_fwd_ex")
         try:
             call()

@@ -14,6 +14,10 @@
 // MFMA, whose B fragment holds the weights of the (phase, tap) pairs that read that
 // neighbour (zeros elsewhere).  Long reductions (the 8192-deep logits layer) split the
 // channel chunks over blocks and reduce fp32 partials in a second pass.
+// Two block organisations: narrow_halo_kernel splits the tile's rows over the 4 waves (every wave holds
+// every B fragment), narrow_wk_kernel (the default) splits the K dimension over them (each fragment
+// loaded once per block), sums the waves' partials through LDS in a fixed order and stores the output
+// tile from LDS with row / pixel vector stores.
 #include "common.hpp"
 
 namespace stc {
@@ -232,6 +236,214 @@ __global__ void __launch_bounds__(256) narrow_halo_kernel(const HParams p) {
   }
 }
 
+// The same reduction with the K dimension split over the block's waves instead of the rows: wave w owns
+// column block j = w % NB and the 32-channel K-slices ks = w / NB + (4 / NB) t of the block's chunks, for
+// every row of the tile.  Each B fragment is then loaded from L2 once per block -- in the row-split form
+// above every wave loaded all of them, 3/4 of the block's L2 -> CU traffic for the N <= 16 layers.  All of
+// the block's chunks are staged at once (one DMA wait, no ring); the partial sums of the waves of K group
+// > 0 go through LDS (the A tile's space, after a barrier) to the K-group-0 wave of their column block,
+// which adds them in wave order (deterministic) and stores.  3 waves per SIMD (<= 168 VGPRs): the LDS of
+// 3 blocks per CU.
+template <int GEOM, int NB, int TY, int TXB>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) narrow_wk_kernel(const HParams p) {
+  constexpr int TX = 16 * TXB;
+  constexpr int HALO = GEOM == 0 ? 2 : 3;
+  constexpr int RY = TY + HALO, RX = TX + HALO;
+  constexpr int NPIX = RY * RX;
+  constexpr int PIECES = (NPIX + 7) / 8;  // 1 KiB DMA pieces per chunk image
+  constexpr int CSTRIDE = PIECES * 1024;
+  constexpr int NBR = GEOM == 0 ? 9 : 16;
+  constexpr int KG = 4 / NB;  // waves per column block
+  static_assert(NB == 1 || NB == 2, "NB");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = wave % NB, kg = wave / NB;
+  const int img = blockIdx.x / p.tiles_per_img, tix = blockIdx.x % p.tiles_per_img;
+  const int y0 = (tix / p.tiles_x) * TY, x0 = (tix % p.tiles_x) * TX;
+  const int split = blockIdx.y;
+  const int nchunks = p.cin / 64;
+  const int cbeg = split * p.chunks_per_split;
+  const int nch = min(nchunks, cbeg + p.chunks_per_split) - cbeg;
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, (short)0, (int)p.a_bytes, 0x00020000);
+  const unsigned OOBV = 0x80000000u;
+  const int abase = img * p.a_bs + p.a_co;
+  const int schunk = (lane & 7) ^ (lane >> 3);
+  // every chunk image of the block: piece q = chunk * PIECES + pc, wave-strided
+  for (int q = wave; q < nch * PIECES; q += 4) {
+    const int c = q / PIECES, pc = q - c * PIECES;
+    const int pix = pc * 8 + (lane >> 3);
+    const int py = pix / RX, px = pix - py * RX;
+    const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+    const bool ok = pix < NPIX && (unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW;
+    const unsigned off = (((unsigned)abase + (unsigned)iy * (unsigned)p.a_rs + (unsigned)ix * (unsigned)p.a_ps +
+                           (unsigned)((cbeg + c) * 64 + schunk * 8)) * 2u) | (ok ? 0u : OOBV);
+    hdma16(ra, smem + c * CSTRIDE + pc * 1024, off);
+  }
+
+  const uint4* frag = reinterpret_cast<const uint4*>(p.frag);
+  floatx4 acc[TY][TXB];
+#pragma unroll
+  for (int r = 0; r < TY; ++r)
+#pragma unroll
+    for (int cx = 0; cx < TXB; ++cx) acc[r][cx] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int gx = lane & 15;
+  const int KS = 2 * nch;
+  bool first = true;
+  for (int ks = kg; ks < KS || first; ks += KG) {
+    const bool have = ks < KS;
+    const int ch = cbeg + (ks >> 1), kk = ks & 1;
+    bf16x8_h bfr[NBR];
+    if (have) {
+#pragma unroll
+      for (int nb = 0; nb < NBR; ++nb)
+        bfr[nb] = __builtin_bit_cast(bf16x8_h, frag[((long long)((ch * 2 + kk) * NBR + nb) * NB + j) * 64 + lane]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (first) {  // the chunk images (every wave's pieces) have landed
+      __builtin_amdgcn_s_barrier();
+      first = false;
+    }
+    if (!have) break;
+    const char* sT = smem + (ks >> 1) * CSTRIDE;
+    const int cslot = kk * 4 + (lane >> 4);
+    // pixel pix = c + gx (c a compile-time offset per (row, neighbour, column block)) sits at byte
+    // c*128 + lofs[c & 7]: eight per-lane bases, the rest an immediate offset of the read
+    int lofs[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) lofs[m] = gx * 128 + ((cslot ^ ((m + gx) & 7)) * 16);
+#pragma unroll
+    for (int nb = 0; nb < NBR; ++nb) {
+      const int dy = GEOM == 0 ? nb / 3 - 1 : nb / 4 - 1;
+      const int dx = GEOM == 0 ? nb % 3 - 1 : nb % 4 - 1;
+#pragma unroll
+      for (int r = 0; r < TY; ++r)
+#pragma unroll
+        for (int cx = 0; cx < TXB; ++cx) {
+          const int c = (r + dy + 1) * RX + 16 * cx + dx + 1;
+          const bf16x8_h af = *reinterpret_cast<const bf16x8_h*>(sT + lofs[c & 7] + c * 128);
+          acc[r][cx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[nb], acc[r][cx], 0, 0, 0);
+        }
+      // one neighbour's reads at a time: hoisting all TY*TXB*NBR fragment reads spills
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // ---- partial sums through LDS: red[kg][j][r][cx][lane]; wave (j, kg) then sums rows
+  // [kg*RPW, (kg+1)*RPW) of column block j over the K groups in order (deterministic)
+  constexpr int RPW = TY / KG;
+  __syncthreads();  // every wave is done with the chunk images
+  floatx4* red = reinterpret_cast<floatx4*>(smem);
+#pragma unroll
+  for (int r = 0; r < TY; ++r)
+#pragma unroll
+    for (int cx = 0; cx < TXB; ++cx) red[(((kg * NB + j) * TY + r) * TXB + cx) * 64 + lane] = acc[r][cx];
+  __syncthreads();
+  floatx4 o[RPW][TXB];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+    for (int cx = 0; cx < TXB; ++cx) o[rr][cx] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int cx = 0; cx < TXB; ++cx) {
+        const floatx4 v = red[(((g * NB + j) * TY + kg * RPW + rr) * TXB + cx) * 64 + lane];
+        o[rr][cx][0] += v[0]; o[rr][cx][1] += v[1]; o[rr][cx][2] += v[2]; o[rr][cx][3] += v[3];
+      }
+
+  // ---- epilogue: o[rr][cx][e] = grid point (y0 + kg*RPW + rr, x0 + 16 cx + 4*(lane>>4) + e), column 16j + (lane&15)
+  const int np = 16 * j + (lane & 15);
+  const bool col_ok = np < p.NP;
+  int ph = 0, n = np;
+  if (GEOM == 0) { ph = np / p.N; n = np - ph * p.N; }
+  if (p.nsplit > 1) {  // fp32 partials of this channel-chunk split, summed by narrow_reduce_kernel
+    if (!col_ok) return;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int gy = y0 + kg * RPW + rr;
+      if (gy >= p.GH) break;
+#pragma unroll
+      for (int cx = 0; cx < TXB; ++cx)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int gxx = x0 + 16 * cx + 4 * (lane >> 4) + e;
+          if (gxx >= p.GW) continue;
+          const long long m = ((long long)img * p.GH + gy) * p.GW + gxx;
+          p.ws[((long long)split * p.Mtot + m) * p.NP + np] = o[rr][cx][e];
+        }
+    }
+    return;
+  }
+  // the block's output tile staged in LDS as [oy][ox][n] (behind the partials),
+  // then written with whole-row (NCHW fp32) or whole-pixel (NHWC bf16, 8 channels) vector stores
+  constexpr int SC = GEOM == 0 ? 2 : 1;  // output pixels per grid point per axis
+  constexpr int OYL = SC * TY, OXL = SC * TX;
+  float* stg = reinterpret_cast<float*>(smem + (size_t)4 * TY * TXB * 1024);
+  const int N = p.N;
+  if (col_ok) {
+    const float bz = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+      for (int cx = 0; cx < TXB; ++cx)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = o[rr][cx][e] + bz;
+          if (p.tanh_) v = tanhf(v);
+          const int ly = kg * RPW + rr, lx = 16 * cx + 4 * (lane >> 4) + e;
+          const int oyl = GEOM == 0 ? 2 * ly + (ph >> 1) : ly, oxl = GEOM == 0 ? 2 * lx + (ph & 1) : lx;
+          stg[(oyl * OXL + oxl) * N + n] = v;
+        }
+  }
+  __syncthreads();
+  const int OH = SC * p.GH, OW = SC * p.GW;
+  const int oy0 = SC * y0, ox0 = SC * x0;
+  const long long cbase = (long long)img * p.c_bs + (long long)p.c_co * p.c_cs;
+  const bool f32_rows = p.out_f32 && p.c_ps == 1 && ((p.c_rs | p.c_cs | (int)(p.c_bs & 3) | p.c_co) & 3) == 0;
+  const bool bf_pix = !p.out_f32 && N == 8 && p.c_cs == 1 && ((p.c_ps | p.c_rs | (int)(p.c_bs & 7) | p.c_co) & 7) == 0;
+  if (f32_rows) {
+    // (n, oy) rows of OXL floats: one float4 per thread-iteration
+    for (int t = tid; t < N * OYL * (OXL / 4); t += 256) {
+      const int xq = t % (OXL / 4), rest = t / (OXL / 4);
+      const int oyl = rest % OYL, nn = rest / OYL;
+      const int oy = oy0 + oyl, ox = ox0 + 4 * xq;
+      if (oy >= OH || ox >= OW) continue;
+      const float* sp = stg + (oyl * OXL + 4 * xq) * N + nn;
+      float* dst = reinterpret_cast<float*>(p.c) + cbase + (long long)oy * p.c_rs + ox + (long long)nn * p.c_cs;
+      if (ox + 4 <= OW) {
+        *reinterpret_cast<float4*>(dst) = make_float4(sp[0], sp[N], sp[2 * N], sp[3 * N]);
+      } else {
+        for (int i = 0; i < OW - ox; ++i) dst[i] = sp[i * N];
+      }
+    }
+  } else if (bf_pix) {
+    // one pixel = 8 channels = one 16-byte store
+    for (int t = tid; t < OYL * OXL; t += 256) {
+      const int oxl = t % OXL, oyl = t / OXL;
+      const int oy = oy0 + oyl, ox = ox0 + oxl;
+      if (oy >= OH || ox >= OW) continue;
+      const float* sp = stg + t * 8;
+      uint4 u;
+      u.x = pack_bf16x2(sp[0], sp[1]); u.y = pack_bf16x2(sp[2], sp[3]);
+      u.z = pack_bf16x2(sp[4], sp[5]); u.w = pack_bf16x2(sp[6], sp[7]);
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + cbase + (long long)oy * p.c_rs + (long long)ox * p.c_ps) = u;
+    }
+  } else {
+    for (int t = tid; t < OYL * OXL * N; t += 256) {
+      const int nn = t % N, pix = t / N;
+      const int oxl = pix % OXL, oyl = pix / OXL;
+      const int oy = oy0 + oyl, ox = ox0 + oxl;
+      if (oy >= OH || ox >= OW) continue;
+      store_out(p, cbase + (long long)oy * p.c_rs + (long long)ox * p.c_ps + (long long)nn * p.c_cs, stg[t]);
+    }
+  }
+}
+
 // split-K combine: out = epi(sum_s ws[s][m][n'])
 template <int GEOM>
 __global__ void narrow_reduce_kernel(const HParams p, int B) {
@@ -263,20 +475,43 @@ static size_t halo_lds(int geom, int ty, int txb, int nstage) {
   return (size_t)nstage * (size_t)((npix + 7) / 8) * 1024;
 }
 
-// Narrow plan: {ty, txb, nsplit}.  Taller / wider tiles reuse each register-held B fragment over more
-// MFMAs; the split over channel chunks keeps >= 1024 blocks on the long reductions.
+// K-split kernel LDS: all of the block's chunk images, or the partials + staged output tile if larger
+static size_t wk_lds(int geom, int ty, int txb, int n_out, int nch) {
+  const int halo = geom == 0 ? 2 : 3;
+  const size_t img = (size_t)(((ty + halo) * (16 * txb + halo) + 7) / 8) * 1024;
+  const int sc = geom == 0 ? 2 : 1;
+  const size_t red = (size_t)4 * ty * txb * 1024;                         // every wave's partials
+  const size_t stage = (size_t)(sc * ty) * (sc * 16 * txb) * n_out * 4;  // the output tile, fp32
+  return std::max(img * (size_t)nch, red + stage);
+}
+
+// Narrow plan: {ty, txb, nsplit, kernel}.  Taller / wider tiles reuse each register-held B fragment over
+// more MFMAs; the split over channel chunks keeps >= 1024 blocks on the long reductions.  Kernel 1 (default):
+// narrow_wk_kernel, whose block stages all its chunks at once -- the split also keeps that under 56 KiB
+// (3 blocks per CU).  force = {ty, txb (+16: the row-split narrow_halo_kernel)}.
 static void narrow_plan(int geom, int B, int GH, int GW, int cin, int np_cols, const int32_t* force, int* ty,
-                        int* txb, int* nsplit) {
-  *ty = 8;
-  *txb = geom == 0 && np_cols > 16 ? 2 : 1;  // two column blocks per B fragment: -11 % on the N = 8 ConvT
+                        int* txb, int* nsplit, int* kern) {
+  // K-split kernel: 4 x 16 tiles (scripts/narrow_sweep.py, round 3: G output ConvT 128->1|3 41.6|43.7 us,
+  // N = 8 input gradient 33.6 us, logits 21.1 us vs 60.7|60.3, 60.4, 24.7 us for the best row-split tiles)
+  *ty = 4;
+  *txb = 1;
+  *kern = 1;
   if (force && force[0] > 0) {
     *ty = force[0];
-    *txb = force[1] > 0 ? force[1] : 1;
+    *txb = (force[1] & 15) > 0 ? (force[1] & 15) : 1;
+    if (force[1] & 16) *kern = 0;
+  } else if (force && (force[1] & 16)) {  // the row-split kernel at its own default tile
+    *kern = 0;
+    *ty = 8;
+    *txb = geom == 0 && np_cols > 16 ? 2 : 1;  // two column blocks per B fragment: -11 % on the N = 8 ConvT
   }
   const int nchunks = cin / 64;
+  const int n_out = geom == 0 ? np_cols / 4 : np_cols;
   const long long blocks = (long long)B * cdiv(GH, *ty) * cdiv(GW, 16 * *txb);
   int ns = 1;
   while (blocks * ns < 1024 && ns * 2 <= nchunks) ns *= 2;
+  if (*kern == 1)
+    while (wk_lds(geom, *ty, *txb, n_out, cdiv(nchunks, ns)) > 56 * 1024 && ns * 2 <= nchunks) ns *= 2;
   *nsplit = ns;
 }
 
@@ -296,9 +531,9 @@ bool bf16_narrow_eligible(int kind, int Cin, int Cout) {
 
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout) {
   const int geom = kind == STC_CONVT_S2 ? 0 : 1;
-  int ty, txb, ns;
+  int ty, txb, ns, kern;
   const int np = geom == 0 ? 4 * Cout : Cout;
-  narrow_plan(geom, B, GH, GW, Cin, np, nullptr, &ty, &txb, &ns);
+  narrow_plan(geom, B, GH, GW, Cin, np, nullptr, &ty, &txb, &ns, &kern);
   return (ns <= 1 ? 0 : (int64_t)ns * B * GH * GW * np * 4) + narrow_frag_bytes(geom, Cin, Cout);
 }
 
@@ -323,8 +558,8 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
   p.c = (char*)y.p; p.c_bs = y.bs; p.c_rs = y.rs; p.c_ps = y.ps; p.c_co = y.co; p.c_cs = y.cs;
   p.bias = bias; p.tanh_ = epi_tanh; p.out_f32 = out_f32;
   p.Mtot = (long long)B * p.GH * p.GW;
-  int ty, txb, ns;
-  narrow_plan(geom, B, p.GH, p.GW, Cin, p.NP, force, &ty, &txb, &ns);
+  int ty, txb, ns, kern;
+  narrow_plan(geom, B, p.GH, p.GW, Cin, p.NP, force, &ty, &txb, &ns, &kern);
   p.tiles_x = cdiv(p.GW, 16 * txb);
   p.tiles_per_img = p.tiles_x * cdiv(p.GH, ty);
   const int nchunks = Cin / 64;
@@ -349,9 +584,28 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
     STC_CHECK_LAUNCH();
   }
   dim3 grid((unsigned)(B * p.tiles_per_img), (unsigned)p.nsplit);
-  const size_t lds = halo_lds(geom, ty, txb, p.chunks_per_split > 1 ? 2 : 1);
+  const size_t lds = kern == 1 ? wk_lds(geom, ty, txb, Cout, p.chunks_per_split)
+                               : halo_lds(geom, ty, txb, p.chunks_per_split > 1 ? 2 : 1);
   STC_REQUIRE(lds <= 160 * 1024, "narrow bf16: tile %dx%d needs %zu B of LDS", ty, 16 * txb, lds);
   main_timer_begin(st);
+  if (kern == 1) {
+#define STC_NW(G_, NB_, TY_, TXB_) hipLaunchKernelGGL((narrow_wk_kernel<G_, NB_, TY_, TXB_>), grid, dim3(256), lds, st, p)
+#define STC_NW_T(G_, NB_)                                                                  \
+  if (ty == 8 && txb == 1) STC_NW(G_, NB_, 8, 1);                                          \
+  else if (ty == 8 && txb == 2) STC_NW(G_, NB_, 8, 2);                                     \
+  else if (ty == 16 && txb == 1) STC_NW(G_, NB_, 16, 1);                                   \
+  else if (ty == 4 && txb == 1) STC_NW(G_, NB_, 4, 1);                                     \
+  else if (ty == 4 && txb == 2) STC_NW(G_, NB_, 4, 2);                                     \
+  else return fail(-1, "narrow bf16: no kernel for a %dx%d tile", ty, 16 * txb);
+    if (geom == 0) {
+      if (p.NP <= 16) { STC_NW_T(0, 1) }
+      else { STC_NW_T(0, 2) }
+    } else {
+      STC_NW_T(1, 1)
+    }
+#undef STC_NW_T
+#undef STC_NW
+  } else {
 #define STC_NH(G_, NB_, TY_, TXB_) hipLaunchKernelGGL((narrow_halo_kernel<G_, NB_, TY_, TXB_>), grid, dim3(256), lds, st, p)
 #define STC_NH_T(G_, NB_)                                                                  \
   if (ty == 8 && txb == 1) STC_NH(G_, NB_, 8, 1);                                          \
@@ -360,14 +614,15 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
   else if (ty == 16 && txb == 2) STC_NH(G_, NB_, 16, 2);                                   \
   else if (ty == 32 && txb == 1) STC_NH(G_, NB_, 32, 1);                                   \
   else return fail(-1, "narrow bf16: no kernel for a %dx%d tile", ty, 16 * txb);
-  if (geom == 0) {
-    if (p.NP <= 16) { STC_NH_T(0, 1) }
-    else { STC_NH_T(0, 2) }
-  } else {
-    STC_NH_T(1, 1)
-  }
+    if (geom == 0) {
+      if (p.NP <= 16) { STC_NH_T(0, 1) }
+      else { STC_NH_T(0, 2) }
+    } else {
+      STC_NH_T(1, 1)
+    }
 #undef STC_NH_T
 #undef STC_NH
+  }
   main_timer_end(st);
   STC_CHECK_LAUNCH();
   if (p.nsplit > 1) {
