@@ -1,4 +1,5 @@
-"""Which ATen ops still run inside a train step (names, shapes, counts) -- torch.profiler, CPU side."""
+"""Which ATen ops still run inside a train step (names, shapes, counts, and the trainer source line that
+issued them) -- torch.profiler, CPU side."""
 import os
 import sys
 import types
@@ -23,7 +24,7 @@ y = torch.rand((B, 3, 256, 256), device=dev) * 2 - 1
 for _ in range(3):
     tr.train_step(x, m, y)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU], record_shapes=True) as prof:
+with profile(activities=[ProfilerActivity.CPU], record_shapes=True, with_stack=True) as prof:
     tr.train_step(x, m, y)
     torch.cuda.synchronize()
 c = Counter()
@@ -31,6 +32,7 @@ for e in prof.events():
     if e.name in ("aten::add_", "aten::add", "aten::fill_", "aten::copy_", "aten::mul", "aten::zero_", "aten::zeros",
                   "aten::ones_like", "aten::mul_", "aten::sub", "aten::neg", "aten::div", "aten::clone",
                   "aten::contiguous", "aten::_to_copy", "aten::sum", "aten::mean", "aten::rsub", "aten::expand"):
-        c[(e.name, str(e.input_shapes)[:90])] += 1
-for (n, s), k in sorted(c.items(), key=lambda kv: -kv[1]):
-    print(f"{k:4d} {n:18s} {s}")
+        site = next((f for f in (e.stack or []) if "stcgan_amd" in f or "bench" in f), "?")
+        c[(e.name, str(e.input_shapes)[:70], site.split("repo/")[-1][:90])] += 1
+for (n, s, site), k in sorted(c.items(), key=lambda kv: -kv[1]):
+    print(f"{k:4d} {n:16s} {s:70s} {site}")

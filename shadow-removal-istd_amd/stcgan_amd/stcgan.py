@@ -88,13 +88,15 @@ class STCGAN(object):
         self.decay_D = torch.optim.lr_scheduler.ReduceLROnPlateau(self.optim_D, cooldown=10, min_lr=1e-7, factor=0.8)
         # each network's gradients live in one flat buffer (parallel.FlatGrads), cut into buckets that the
         # engine reports complete while the backward runs (parallel.BucketExchange): with data parallelism each
-        # bucket is averaged over the ranks (RCCL) right then, and the optimiser updates it right after
-        # (optim.Adam.overlap: the update of the deep layers runs under the backward of the shallow ones)
+        # bucket is averaged over the ranks (RCCL) right then.  overlap_optim: the optimiser also updates each
+        # bucket right after (optim.Adam.overlap) -- bit-identical, but off by default: the step is GPU-bound,
+        # and the updates' HBM traffic only moved time into the backward's kernels (round-3 A/B, scripts/
+        # ab_overlap.py: 13.22 vs 13.05 ms/step)
         world = parallel.world()
         self.bucket_mb = float(getattr(args, "bucket_mb", 32 if world > 1 else 8))
         for net in (self.G1, self.G2, self.D1, self.D2):
             net.grad_exchange = parallel.BucketExchange(parallel.flat_grads(net), self.bucket_mb)
-        self.overlap_optim = bool(getattr(args, "overlap_optim", True))
+        self.overlap_optim = bool(getattr(args, "overlap_optim", False))
         if self.overlap_optim:
             self.optim_G.overlap([self.G1.grad_exchange, self.G2.grad_exchange])
             self.optim_D.overlap([self.D1.grad_exchange, self.D2.grad_exchange])
