@@ -64,7 +64,11 @@ if args.ab_attr:
 for rep in range(args.repeat):
     if attr:
         v = attr[1][rep % len(attr[1])]
-        setattr(tr, attr[0], type(getattr(tr, attr[0]))(v))
+        setter = getattr(tr, "set_" + attr[0], None)
+        if setter is not None:
+            setter(v)
+        else:
+            setattr(tr, attr[0], type(getattr(tr, attr[0]))(v))
         args.wgrad_overlap = f"{attr[0]}={v}"
         for _ in range(2):
             tr.train_step(x, m, y)

@@ -98,6 +98,9 @@ constexpr unsigned OOB = 0x80000000u;
 #ifndef STC_IGEMM_INTERLEAVE
 #define STC_IGEMM_INTERLEAVE 0
 #endif
+#ifndef STC_SETPRIO
+#define STC_SETPRIO 0
+#endif
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)lds_dst, 16, voff, 0, 0, 0);
@@ -277,10 +280,16 @@ igemm_bf16_kernel(const GParams p) {
       for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + i * 16 * RB + rd_off[kk]);
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sB + j * 16 * RB + rd_off[kk]);
+#if STC_SETPRIO
+      __builtin_amdgcn_s_setprio(1);  // (guide T5: the MFMA cluster at raised wave priority)
+#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+#if STC_SETPRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
   };
 

@@ -18,6 +18,10 @@
 
 #include "common.hpp"
 
+#ifndef STC_SETPRIO
+#define STC_SETPRIO 0
+#endif
+
 namespace stc {
 
 struct WbParams {
@@ -328,10 +332,16 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
         const w4i16 v8[2] = {lo, hi};
         fb[j] = __builtin_bit_cast(wbf16x8, v8);
       }
+#if STC_SETPRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+#if STC_SETPRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
   };
 

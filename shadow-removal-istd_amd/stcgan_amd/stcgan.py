@@ -96,10 +96,7 @@ class STCGAN(object):
         self.bucket_mb = float(getattr(args, "bucket_mb", 32 if world > 1 else 8))
         for net in (self.G1, self.G2, self.D1, self.D2):
             net.grad_exchange = parallel.BucketExchange(parallel.flat_grads(net), self.bucket_mb)
-        self.overlap_optim = bool(getattr(args, "overlap_optim", False))
-        if self.overlap_optim:
-            self.optim_G.overlap([self.G1.grad_exchange, self.G2.grad_exchange])
-            self.optim_D.overlap([self.D1.grad_exchange, self.D2.grad_exchange])
+        self.set_overlap_optim(bool(getattr(args, "overlap_optim", False)))
         # discriminators on side HIP streams (train_step / _lanes); off for a strictly serial step
         self.streams = bool(getattr(args, "streams", True))
         self.lane_carry = bool(getattr(args, "lane_carry", True))
@@ -132,6 +129,12 @@ class STCGAN(object):
             self.valid_interval = getattr(args, "valid_every", 10)
         if "infer" in tasks:
             self.inferd_dir = getattr(args, "infered", None)
+
+    def set_overlap_optim(self, on):
+        """Update each gradient bucket as the backward completes it (optim.Adam.overlap) or after the backward."""
+        self.overlap_optim = bool(on)
+        self.optim_G.overlap([self.G1.grad_exchange, self.G2.grad_exchange], on=self.overlap_optim)
+        self.optim_D.overlap([self.D1.grad_exchange, self.D2.grad_exchange], on=self.overlap_optim)
 
     @staticmethod
     def _device_of(args):

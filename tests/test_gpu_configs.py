@@ -315,9 +315,11 @@ def test_c3_bf16_train_step_ngf64_vs_bf16_oracle(loss_type):
             fm2, fv2 = fopt2[name].state[fidx2[id(pf2)]]
             if loss_type != "normal" and name.startswith("D") and k == f"model.{len(net.model) - 1}.bias":
                 # the relativistic objectives are invariant to one shift of all logits: this gradient is
-                # analytically 0 (both sides hold rounding residue, no relative error to speak of)
+                # analytically 0 (both sides hold the residue of a sum of ~3e4 bf16-rounded logit gradients --
+                # measured <= 0.5 % of the network's largest gradient element -- no relative error to speak of;
+                # a missing or doubled loss term would make it O(1) of that scale)
                 scale = max(float(q.grad.abs().max()) for q in net.parameters())
-                check(float(p.grad.abs().max()) <= 1e-3 * scale and float(pr.grad.abs().max()) <= 1e-3 * scale,
+                check(float(p.grad.abs().max()) <= 2e-2 * scale and float(pr.grad.abs().max()) <= 2e-2 * scale,
                       (name, k, "shift-invariant bias gradient not ~0", float(p.grad.abs().max()), scale))
                 continue
             for what, a_, b_, c_, c2_ in (("grad", p.grad, pr.grad, pf.grad, pf2.grad),
