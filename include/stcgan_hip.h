@@ -132,6 +132,43 @@ int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin, const void
                     const stc_bnb_fuse* bnb, float* part2, int nchunks,
                     void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ---- BatchNorm finalize fused into the producing conv (no finalize launch on the chain) ----------
+ * Replaces, per BatchNorm2d of STCGAN/networks.py:107,109,170,179 (train mode), the pair
+ * stc_conv_fwd_ex + stc_bn_finalize (forward) and the dbeta/dgamma reduction of stc_bn_bwd_apply
+ * (backward).  On the bf16 LDS-DMA path the conv's last-arriving blocks (or those of its split-K
+ * reduction) merge the chunk partials in a fixed order (two levels: chunk groups, then groups) and
+ * write the results; other paths run the separate kernels with the same semantics.
+ *   stc_conv_fwd_bnfin: conv + statistics + mean/rstd/scale/shift + running-statistics update
+ *                       (stc_bn_finalize's outputs), stats_part as for stc_conv_fwd_ex.
+ *   stc_conv_bwd_bnfin: stc_conv_bwd_bn + dbeta = sum dn, dgamma = sum dn*xhat into fin->dbeta/dgamma;
+ *                       then call stc_bn_bwd_apply with part2 = NULL and nchunks = 0 (it reads the
+ *                       finished dgamma/dbeta).
+ * counters: uint32 [stc_bn_fin_counters()], zeroed once by the caller; every call leaves them zero,
+ * so calls that share a counter buffer must be ordered on one stream.  scratch: float [64*C*4].   */
+typedef struct {
+  void* counters;
+  float* scratch;
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  int64_t* num_batches_tracked;
+  float momentum, eps;
+  float* mean;
+  float* rstd;
+  float* scale;
+  float* shift;
+  float* dgamma;
+  float* dbeta;
+} stc_bn_fin;
+int stc_bn_fin_counters(void);
+int stc_conv_fwd_bnfin(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
+                       stc_view y, const float* bias, float* stats_part, int stats_chunks, const stc_bn_fin* fin,
+                       const int32_t* force_plan, void* workspace, int64_t workspace_bytes, void* stream);
+int stc_conv_bwd_bnfin(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout, stc_view out,
+                       const stc_bnb_fuse* bnb, float* part2, int nchunks, const stc_bn_fin* fin,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---- weight gradient ---------------------------------------------------------
  * dW[r][ci][kh][kw] = sum_{b,oy,ox} D[b,oy,ox,r] * G[b, oy*s+kh-1, ox*s+kw-1, ci]
  *   Conv2d s2/s1 : D = dy (grid = output), G = x (input), s = stride

@@ -10,6 +10,7 @@
 // input (n = x*scale + shift), reduced to sum(dn), sum(dn*xhat), then applied.
 // All reductions are fixed-order => bitwise reproducible.
 #include "common.hpp"
+#include "bnfin.hpp"
 
 namespace stc {
 
@@ -156,24 +157,6 @@ __device__ __forceinline__ double block_sum256(double v, double* sh) {
   const double r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
   __syncthreads();
   return r;
-}
-
-// mean / rstd / affine table / running statistics of channel c from the merged N, mean, M2
-__device__ __forceinline__ void bn_finalize_store(int c, double N, double mu, double M2, const float* gamma,
-                                                  const float* beta, float* rmean, float* rvar, long long* nbt,
-                                                  float momentum, float eps, float* mean_o, float* rstd_o,
-                                                  float* scale, float* shift) {
-  const double var = N > 0 ? M2 / N : 0.0;
-  const float rs = (float)(1.0 / sqrt(var + (double)eps));
-  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  if (mean_o) mean_o[c] = (float)mu;
-  if (rstd_o) rstd_o[c] = rs;
-  const float sc = g * rs;
-  scale[c] = sc;
-  shift[c] = bt - (float)mu * sc;
-  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
-  if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(N > 1 ? M2 / (N - 1) : var);
-  if (nbt && c == 0) nbt[0] += 1;
 }
 
 __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int nchunks, int C,
@@ -898,7 +881,10 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
               "stc_bn_bwd_apply: bad C=%d / views", C);
   hipStream_t st = (hipStream_t)stream;
   GradIn gi = mkgrad(g1, slope1, g2, slope2);
-  if (mean) {
+  if (mean && part2 == nullptr && nchunks == 0) {
+    // dgamma / dbeta already final (stc_conv_bwd_bnfin)
+    STC_REQUIRE(dgamma && dbeta && gamma && rstd && scale && shift, "stc_bn_bwd_apply: missing BN tensors");
+  } else if (mean) {
     STC_REQUIRE(part2 && dgamma && dbeta && gamma && rstd && scale && shift, "stc_bn_bwd_apply: missing BN tensors");
     if (nchunks <= 256)
       hipLaunchKernelGGL(bn_bwd_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part2, nchunks, C, dgamma, dbeta);
@@ -920,3 +906,20 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
   STC_CHECK_LAUNCH();
   return 0;
 }
+
+namespace stc {
+// The finalize of stc_conv_fwd_bnfin / stc_conv_bwd_bnfin as its own launch (paths whose producer has no
+// in-kernel finalize): the same merges as stc_bn_finalize / stc_bn_bwd_apply's reduction.
+int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st) {
+  if (!sums)
+    return stc_bn_finalize(part, nchunks, C, f.gamma, f.beta, f.rmean, f.rvar, (int64_t*)f.nbt, f.momentum, f.eps,
+                           f.mean_o, f.rstd_o, f.scale, f.shift, st);
+  STC_REQUIRE(f.dgamma && f.dbeta, "bn finalize: dgamma/dbeta required");
+  if (nchunks <= 256)
+    hipLaunchKernelGGL(bn_bwd_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nchunks, C, f.dgamma, f.dbeta);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, nchunks, C, f.dgamma, f.dbeta);
+  STC_CHECK_LAUNCH();
+  return 0;
+}
+}  // namespace stc

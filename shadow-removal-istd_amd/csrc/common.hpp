@@ -17,6 +17,28 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 typedef short shortx4 __attribute__((ext_vector_type(4)));
 
+// Diagnostic builds (scripts/diag_gemm.sh; never the shipped library): STC_EXP_NODMA drops the
+// LDS-DMA operand loads, STC_EXP_NOMFMA replaces each MFMA by one VALU add that still consumes its
+// fragments, STC_EXP_NOEPI ends the GEMM kernels after the K loop -- what each part of a tile costs.
+#ifndef STC_EXP_NODMA
+#define STC_EXP_NODMA 0
+#endif
+#ifndef STC_EXP_NOMFMA
+#define STC_EXP_NOMFMA 0
+#endif
+#ifndef STC_EXP_NOEPI
+#define STC_EXP_NOEPI 0
+#endif
+typedef __bf16 stc_bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ floatx4 exp_mfma(stc_bf16x8 a, stc_bf16x8 b, floatx4 c) {
+#if STC_EXP_NOMFMA
+  c[0] += (float)a[0] * (float)b[0];
+  return c;
+#else
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
 // ---------------------------------------------------------------- errors
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);

@@ -17,6 +17,7 @@
 //     squares, in fp32 from the accumulators) -> part[tile][n] = {count, 0, M2, mean},
 //     the format stc_bn_finalize merges (Chan's parallel variance).
 #include "common.hpp"
+#include "bnfin.hpp"
 
 namespace stc {
 
@@ -58,6 +59,10 @@ struct GParams {
   const float *bsc, *bsh, *bmu, *brs;
   float bs_self, bs_other;
   int bC, bch_off;
+  // BatchNorm finalize in this launch (bnfin.hpp): statistics -> tables (stats) or the backward sums
+  // (part2) -> dbeta/dgamma, by the last-arriving blocks; stat_chunks = the chunk count of stats/part2
+  int fin_on, stat_chunks;
+  BnFin fin;
 };
 
 // {dn, dn*xhat} of 8 consecutive BN channels at one pixel (v: this conv's 8 output values)
@@ -103,7 +108,9 @@ constexpr unsigned OOB = 0x80000000u;
 #endif
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, unsigned voff) {
+#if !STC_EXP_NODMA  // diagnostic builds only (common.hpp)
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)lds_dst, 16, voff, 0, 0, 0);
+#endif
 }
 
 // LDS swizzle of a K-row image: BK = 64 -> 128-B rows, chunk ^ (row & 7); BK = 32 -> 64-B rows,
@@ -143,19 +150,23 @@ __device__ __forceinline__ unsigned tap_spread(unsigned r, int lg) {
   return (r & 1u) | (((r >> 1) & 1u) << (1 << lg)) | (((r >> 2) & 1u) << (2 << lg)) | (((r >> 3) & 1u) << (3 << lg));
 }
 
-template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB>
-__global__ void __launch_bounds__(64 * WM * WN)
+// LD > 0: LD extra "loader" waves issue every LDS-DMA piece and the WM*WN compute waves only read
+// fragments and issue MFMAs (one barrier per K-step; the loaders run NST-1 steps ahead), so the DMA
+// issue never sits in a compute wave's instruction stream.
+template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB, int LD = 0>
+__global__ void __launch_bounds__(64 * (WM * WN + LD))
 igemm_bf16_kernel(const GParams p) {
   constexpr int NW = WM * WN;
+  constexpr int NL = LD > 0 ? LD : NW;   // waves that issue the DMA
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int RB = BK * 2;             // bytes per LDS row (one GEMM row's K-step)
   constexpr int CH = BK / 8;             // 16-byte chunks per row
   constexpr int RPP = 1024 / RB;         // rows per 1 KiB DMA piece
-  constexpr int AG = BM / (RPP * NW), BG = BN / (RPP * NW);  // pieces per wave per K-step
+  constexpr int AG = BM / (RPP * NL), BG = BN / (RPP * NL);  // pieces per loading wave per K-step
   constexpr int STAGE = (BM + BN) * RB;
   constexpr int KK = BK / 32;            // 16x16x32 MFMA sub-steps per K-step
-  static_assert(AG * RPP * NW == BM && BG * RPP * NW == BN, "tile rows must split into whole pieces per wave");
+  static_assert(AG * RPP * NL == BM && BG * RPP * NL == BN, "tile rows must split into whole pieces per wave");
   static_assert(FM >= 1 && FN >= 1, "wave tile >= 16x16");
   static_assert(NST >= 2 && NST <= 8, "2..8-stage ring (wait_ahead covers up to 6 steps ahead)");
   static_assert(BK == 64 || BK == 32, "BK");
@@ -164,6 +175,7 @@ igemm_bf16_kernel(const GParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
+  const int lw = LD > 0 ? wave - NW : wave;  // index among the loading waves
 
   const int nwg = p.mtiles * p.ntiles;
   int bid = blockIdx.x;
@@ -197,7 +209,7 @@ igemm_bf16_kernel(const GParams p) {
   unsigned a_off0[AG], a_inv[AG];
 #pragma unroll
   for (int g = 0; g < AG; ++g) {
-    const int m = m0 + (wave * AG + g) * RPP + prow;
+    const int m = m0 + (lw * AG + g) * RPP + prow;
     const int mm = m < p.M ? m : 0;
     const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
     const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
@@ -209,7 +221,7 @@ igemm_bf16_kernel(const GParams p) {
   unsigned b_off[BG];
 #pragma unroll
   for (int g = 0; g < BG; ++g) {
-    const int n = n0 + (wave * BG + g) * RPP + prow;
+    const int n = n0 + (lw * BG + g) * RPP + prow;
     b_off[g] = n < p.N ? (unsigned)(ph * p.b_phase_stride + n * p.K) : OOB;
   }
   const int tw_mask = ntap1 - 1;
@@ -235,11 +247,11 @@ igemm_bf16_kernel(const GParams p) {
     char* sB = sA + BM * RB;
     if (g < AG) {
       const unsigned pen = (((a_inv[g] >> (st_tcur & 31)) & 1u) << 31) | st_kpen;
-      dma16(ra, sA + (wave * AG + g) * 1024, ((a_off0[g] + st_delta) * 2u) | pen);
+      dma16(ra, sA + (lw * AG + g) * 1024, ((a_off0[g] + st_delta) * 2u) | pen);
     } else {
       const int h = g - AG;
       const unsigned off = ((b_off[h] + (unsigned)(kcur)) * 2u) | st_kpen | (b_off[h] & OOB);
-      dma16(rb, sB + (wave * BG + h) * 1024, off);
+      dma16(rb, sB + (lw * BG + h) * 1024, off);
     }
   };
   auto advance = [&]() {  // to the next K-step
@@ -286,7 +298,7 @@ igemm_bf16_kernel(const GParams p) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = exp_mfma(fa[i], fb[j], acc[i][j]);
 #if STC_SETPRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
@@ -309,7 +321,7 @@ igemm_bf16_kernel(const GParams p) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = exp_mfma(fa[i], fb[j], acc[i][j]);
         const int slot = kk * FM + i;
         if (dma && slot < AG + BG) {
           piece(nstage, slot);
@@ -325,7 +337,28 @@ igemm_bf16_kernel(const GParams p) {
     }
   };
 
-  if constexpr (NST == 2 && STC_IGEMM_INTERLEAVE) {
+  if constexpr (LD > 0) {
+    constexpr int P = AG + BG;
+    if (wave >= NW) {  // loader: steps 0 .. NST-2 ahead, then one refill per K-step
+#pragma unroll
+      for (int i = 0; i < NST - 1; ++i)
+        if (i < nsteps) issue(i);
+      int nxt = NST - 1;
+      for (int s = 0; s < nsteps; ++s) {
+        wait_ahead<P>(min(NST - 2, nsteps - 1 - s));  // this wave's pieces of step s have landed
+        __builtin_amdgcn_s_barrier();                 // ... and every loader's; step s - 1 is read
+        if (s + NST - 1 < nsteps) issue(nxt);         // into the stage step s - 1 used
+        nxt = nxt == NST - 1 ? 0 : nxt + 1;
+      }
+      return;  // (a terminated wave no longer counts at the epilogue's barriers)
+    }
+    int cur = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      __builtin_amdgcn_s_barrier();
+      compute(cur);
+      cur = cur == NST - 1 ? 0 : cur + 1;
+    }
+  } else if constexpr (NST == 2 && STC_IGEMM_INTERLEAVE) {
     if (nsteps > 0) issue(0);
     for (int s = 0; s < nsteps; ++s) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -364,6 +397,17 @@ igemm_bf16_kernel(const GParams p) {
     }
   }
 
+#if STC_EXP_NOEPI
+  {
+    float s_ = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) s_ += acc[i][j][0] + acc[i][j][3];
+    if (s_ == 1.2345f) p.ws[threadIdx.x] = s_;
+    return;
+  }
+#endif
   // ---------------------------------------------------------------- epilogue
   // accumulator element (i, j, r): row wm*TM + 16i + 4*(lane>>4) + r, column wn*TN + 16j + (lane&15)
   const int rq = 4 * (lane >> 4), cl = lane & 15;
@@ -464,7 +508,7 @@ igemm_bf16_kernel(const GParams p) {
         m2 += m2w + dl * dl * (cnt * nw / nt);
         cnt = nt;
       }
-      *reinterpret_cast<float4*>(p.stats + (tile * p.N + n) * 4) = make_float4(cnt, 0.f, m2, mean);
+      wt_store4(p.stats + (tile * p.N + n) * 4, make_float4(cnt, 0.f, m2, mean));  // (read in-launch: bnfin.hpp)
     }
     __syncthreads();
   }
@@ -524,6 +568,9 @@ igemm_bf16_kernel(const GParams p) {
           if (++y == p.GH) { y = 0; ++b; }
         }
       }
+      if (p.fin_on && p.stats)
+        bnfin_arrive_stats(p.fin, p.stats, p.stat_chunks, p.N, ph * p.mtiles + mt, n0, min(n0 + BN, p.N), nt, p.ntiles,
+                           smem);
       return;
     }
     // fused BatchNorm-backward reduction: {sum dn, sum dn*xhat} of this thread's 8-channel chunk
@@ -598,8 +645,14 @@ igemm_bf16_kernel(const GParams p) {
         const long long tile = (long long)ph * p.mtiles + mt;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          *reinterpret_cast<float2*>(p.part2 + (tile * p.bC + ch0 + e) * 2) = make_float2(ta[e], tb[e]);
+          wt_store2(p.part2 + (tile * p.bC + ch0 + e) * 2, ta[e], tb[e]);
       }
+    }
+    if (p.fin_on) {
+      // this block's BN channels: [n0, n0 + BN) - bch_off, clipped to [0, bC) (uniform over the blocks of nt)
+      const int lo = max(n0 - p.bch_off, 0), hi = min(min(n0 + BN, p.N) - p.bch_off, p.bC);
+      if (lo < hi)
+        bnfin_arrive_sums(p.fin, p.part2, p.stat_chunks, p.bC, ph * p.mtiles + mt, lo, hi, nt, p.ntiles, smem);
     }
     return;
   }
@@ -733,9 +786,11 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        *reinterpret_cast<float2*>(p.part2 + ((long long)blockIdx.x * p.bC + bnch + e) * 2) = make_float2(ta[e], tb[e]);
+        wt_store2(p.part2 + ((long long)blockIdx.x * p.bC + bnch + e) * 2, ta[e], tb[e]);
     }
   }
+  __shared__ double fin_red[2 * 256 + 1];  // (bnfin.hpp LDS: 2 doubles per thread + the ticket flag)
+  if (p.part2 && p.fin_on) bnfin_arrive_sums(p.fin, p.part2, p.stat_chunks, p.bC, blockIdx.x, 0, p.bC, 0, 1, fin_red);
   if (!p.stats) return;
   __shared__ float red[2][256][8];
   __shared__ float rcnt[256];
@@ -755,8 +810,9 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      *reinterpret_cast<float4*>(p.stats + ((long long)blockIdx.x * p.N + n + e) * 4) = make_float4(nn, a1[e], a2[e], sh[e]);
+      wt_store4(p.stats + ((long long)blockIdx.x * p.N + n + e) * 4, make_float4(nn, a1[e], a2[e], sh[e]));
   }
+  if (p.fin_on) bnfin_arrive_stats(p.fin, p.stats, p.stat_chunks, p.N, blockIdx.x, 0, p.N, 0, 1, fin_red);
 }
 
 // The same reduction for few rows over many splits (the deep 1x1 - 4x4 layers): one wave per (row,
@@ -863,7 +919,13 @@ static const TileCfg kTiles[] = {
     {128, 64, 4, 2, 2, 64},   // 26: 8 waves of 32x32
     {256, 128, 4, 4, 2, 64},  // 27: 16 waves of 64x32
     {128, 256, 4, 4, 2, 64},  // 28: 16 waves of 32x64
+    {128, 128, 2, 2, 4, 64},  // 29: + 4 loader waves (LD), 4 stages
+    {128, 128, 2, 2, 3, 64},  // 30: + 4 loader waves, 3 stages
+    {256, 128, 4, 2, 3, 64},  // 31: + 4 loader waves, 3 stages (8 compute waves)
+    {128, 64, 2, 2, 4, 64},   // 32: + 4 loader waves, 4 stages
 };
+// configurations whose blocks carry 4 loader waves besides the WM*WN compute waves
+static inline int tile_loaders(int cfg) { return cfg >= 29 ? 4 : 0; }
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
 static size_t bf16_lds_bytes(int cfg) {
@@ -988,10 +1050,25 @@ int bf16_igemm_query(int M, int N, int K, int nphase, const int32_t* force, int6
 }
 
 // p: filled by the caller (geometry, operands, output); returns 0 or error.
+int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st);
+
 int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_bytes, float* stats, int stats_chunks,
-                      hipStream_t st) {
+                      hipStream_t st, const BnFin* fin) {
   Bf16Problem pr = bf16_problem(p.M, p.N, p.K, p.nphase, force, p.vec_out != 0);
   const BPlan& pl = pr.pl;
+  p.fin_on = 0;
+  p.stat_chunks = pr.stats_chunks;
+  bool fin_after = false;  // the wide split-K reduction has no in-kernel finalize: a separate launch
+  if (fin) {
+    STC_REQUIRE(stats || p.part2, "bf16 igemm: finalize without statistics");
+    p.fin = *fin;
+    bnfin_groups(pr.stats_chunks, &p.fin.gs, &p.fin.ngroups);
+    const int nct = pl.ksplit > 1 ? 1 : pl.ntiles;
+    STC_REQUIRE(p.fin.ngroups <= BNFIN_MAXG && p.fin.ngroups * nct <= BNFIN_L1 && nct <= BNFIN_L2,
+                "bf16 igemm: finalize grouping %d x %d out of range", p.fin.ngroups, nct);
+    fin_after = pl.ksplit > 1 && pr.wide;
+    p.fin_on = fin_after ? 0 : 1;
+  }
   p.ksplit = pl.ksplit; p.kchunk = pl.kchunk; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles;
   p.stats = nullptr;
   p.ws = nullptr;
@@ -1014,6 +1091,13 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
       hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, true>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
     else                                                                                                    \
       hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, false>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
+    break;
+#define STC_BL(I, BM_, BN_, WM_, WN_, NST_, BK_)                                                            \
+  case I:                                                                                                   \
+    if (p.part2)                                                                                            \
+      hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, true, 4>), grid, dim3(64 * (WM_ * WN_ + 4)), lds, st, p); \
+    else                                                                                                    \
+      hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, false, 4>), grid, dim3(64 * (WM_ * WN_ + 4)), lds, st, p); \
     break;
   main_timer_begin(st);
   switch (pl.cfg) {
@@ -1046,10 +1130,15 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     STC_B(26, 128, 64, 4, 2, 2, 64)
     STC_B(27, 256, 128, 4, 4, 2, 64)
     STC_B(28, 128, 256, 4, 4, 2, 64)
+    STC_BL(29, 128, 128, 2, 2, 4, 64)
+    STC_BL(30, 128, 128, 2, 2, 3, 64)
+    STC_BL(31, 256, 128, 4, 2, 3, 64)
+    STC_BL(32, 128, 64, 2, 2, 4, 64)
     default:
       return fail(-1, "bf16 igemm: bad tile config %d", pl.cfg);
   }
 #undef STC_B
+#undef STC_BL
   main_timer_end(st);
   STC_CHECK_LAUNCH();
   if (pl.ksplit > 1) {
@@ -1065,6 +1154,11 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
       hipLaunchKernelGGL(splitk_reduce_stats_kernel, dim3(blocks), dim3(256), 0, st, p, pr.reduce_rows);
     }
     STC_CHECK_LAUNCH();
+  }
+  if (fin_after) {
+    const bool sums = p.part2 != nullptr;
+    const int rc = bnfin_fallback(p.fin, sums ? p.part2 : stats, pr.stats_chunks, sums ? p.bC : p.N, sums, st);
+    if (rc) return rc;
   }
   return 0;
 }
@@ -1102,7 +1196,7 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
 int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
-                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr) {
+                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr) {
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   GParams p{};
@@ -1146,7 +1240,7 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
     p.bs_self = bnb->slope_self; p.bs_other = bnb->slope_other;
     p.bC = bnb->C; p.bch_off = bnb->ch_off;
   }
-  return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st);
+  return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st, fin);
 }
 
 }  // namespace stc

@@ -342,9 +342,56 @@ __global__ void __launch_bounds__(256) wgrad_reduce_wide_kernel(const float* __r
   if (lane == 0) *reinterpret_cast<float4*>(dW + ((long long)r * Cg_out + ci) * 16 + 4 * g) = acc;
 }
 
+// The same fixed-order sum with more bytes in flight (the kernel above keeps 8 four-byte loads per
+// thread outstanding and was latency-bound at ~17 us for 64 slabs of 512 KB): a block = one row r x
+// 64 channels x 16 taps, a thread = (tap, 4 channels) reading one 16-byte vector per slab, 8 slabs
+// loaded before they are added (in split order, so the result is bit-identical), then the tile is
+// transposed through LDS into dW[r][ci][tap] and stored as contiguous 16-byte rows.
+// Needs Cg % 4 == 0 and Cg_out >= 64.
+__global__ void __launch_bounds__(256) wgrad_reduce_v4_kernel(const float* __restrict__ ws, int nsplit, int R, int Cg,
+                                                              int Cg_out, float* __restrict__ dW) {
+  __shared__ float tile[64 * 17];
+  const int tid = threadIdx.x;
+  const int r = blockIdx.x / ((Cg_out + 63) >> 6);
+  const int c0 = (blockIdx.x - r * ((Cg_out + 63) >> 6)) * 64;
+  const int tap = tid >> 4, c4 = tid & 15;
+  const int ci = c0 + 4 * c4;
+  const long long Ncol = 16LL * Cg;
+  const long long slab = (long long)R * Ncol;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ci < Cg) {
+    const float* src = ws + (long long)r * Ncol + (long long)tap * Cg + ci;
+    int sp = 0;
+    for (; sp + 8 <= nsplit; sp += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (long long)(sp + u) * slab);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+    }
+    for (; sp < nsplit; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (long long)sp * slab);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  tile[(4 * c4 + 0) * 17 + tap] = acc.x;
+  tile[(4 * c4 + 1) * 17 + tap] = acc.y;
+  tile[(4 * c4 + 2) * 17 + tap] = acc.z;
+  tile[(4 * c4 + 3) * 17 + tap] = acc.w;
+  __syncthreads();
+  const int cl = tid >> 2, t4 = (tid & 3) * 4;
+  if (c0 + cl < Cg_out) {
+    const float* q = tile + cl * 17 + t4;
+    *reinterpret_cast<float4*>(dW + ((long long)r * Cg_out + c0 + cl) * 16 + t4) = make_float4(q[0], q[1], q[2], q[3]);
+  }
+}
+
 void wgrad_reduce_launch(const float* ws, int nsplit, int R, int Cg, int Cg_out, float* dW, hipStream_t st) {
   const long long units = (long long)R * Cg_out * 4;
-  if (units < 8192 && nsplit >= 16)
+  if (Cg % 4 == 0 && Cg_out >= 64 && !(units < 8192 && nsplit >= 16))
+    hipLaunchKernelGGL(wgrad_reduce_v4_kernel, dim3((unsigned)(R * ((Cg_out + 63) / 64))), dim3(256), 0, st, ws, nsplit,
+                       R, Cg, Cg_out, dW);
+  else if (units < 8192 && nsplit >= 16)
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, st, ws, nsplit, R, Cg,
                        Cg_out, dW);
   else

@@ -50,7 +50,9 @@ typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
 using wlds_ptr = __attribute__((address_space(3))) void*;
 
 __device__ __forceinline__ void wdma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, unsigned voff) {
+#if !STC_EXP_NODMA  // diagnostic builds only (common.hpp)
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (wlds_ptr)lds_dst, 16, voff, 0, 0, 0);
+#endif
 }
 __device__ __forceinline__ w4i16 wtr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) w4i16*)(p));
@@ -87,9 +89,12 @@ constexpr int WB_BK = 64;
 // D (plain pixel-major channels r) or Gcol (im2col columns tap*Cg + ci).  SWAP = false: rows = D
 // (r), columns = Gcol; SWAP = true (R <= 16): rows = Gcol, columns = D, so the tiny R dimension
 // becomes a 16-wide MFMA N tile instead of wasting 7/8 of a 128-row tile.
-template <int BM, int BN, int WM, int WN, bool SWAP, bool FAST>
-__global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams p) {
+// LD > 0: LD loader waves issue every LDS-DMA piece into an NST-stage ring, NST-1 steps ahead, and the
+// WM*WN compute waves only read fragments and issue MFMAs (one barrier per step).
+template <int BM, int BN, int WM, int WN, bool SWAP, bool FAST, int LD = 0, int NST = 2>
+__global__ void __launch_bounds__(64 * (WM * WN + LD)) wgrad_bf16_kernel(const WbParams p) {
   constexpr int NW = WM * WN;
+  constexpr int NL = LD > 0 ? LD : NW;                 // waves that issue the DMA
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int CHA = BM / 8, CHB = BN / 8;            // 16-byte chunks per pixel row
@@ -97,11 +102,13 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
   constexpr int PA = WB_BK * ROWA / 1024, PB = WB_BK * ROWB / 1024;  // 1 KiB DMA pieces per step
   constexpr int TILEA = WB_BK * ROWA, TILEB = WB_BK * ROWB;
   constexpr int STAGE = TILEA + TILEB;
-  constexpr int IA = (PA + NW - 1) / NW, IB = (PB + NW - 1) / NW;
+  constexpr int IA = (PA + NL - 1) / NL, IB = (PB + NL - 1) / NL;
+  static_assert(LD == 0 || NST >= 3, "the loader ring runs at least two steps ahead");
   static_assert(FM >= 1 && FN >= 1 && PA >= 1 && PB >= 1, "tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
+  const int lw = LD > 0 ? wave - NW : wave;  // index among the loading waves
   // XCD-aware order over (split, tile): workgroups go round-robin to the 8 XCDs by linear id, so
   // remap the linear id to give every XCD a contiguous run of (split-major) work -- the tiles of one
   // pixel split then share their D / G rows in that XCD's L2 instead of every XCD streaming all splits.
@@ -152,9 +159,9 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
   };
   Role ra_[IA], rb_[IB];
 #pragma unroll
-  for (int i = 0; i < IA; ++i) ra_[i] = role(SWAP, CHA, wave + NW * i, a0);
+  for (int i = 0; i < IA; ++i) ra_[i] = role(SWAP, CHA, lw + NL * i, a0);
 #pragma unroll
-  for (int i = 0; i < IB; ++i) rb_[i] = role(!SWAP, CHB, wave + NW * i, b0);
+  for (int i = 0; i < IB; ++i) rb_[i] = role(!SWAP, CHB, lw + NL * i, b0);
 
   struct Pix {
     int b, oy, ox;
@@ -216,9 +223,9 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
   Lc la_[IA], lb_[IB];
   if constexpr (FAST) {
 #pragma unroll
-    for (int i = 0; i < IA; ++i) la_[i] = lane_const(SWAP, ra_[i], 64 / CHA, wave + NW * i);
+    for (int i = 0; i < IA; ++i) la_[i] = lane_const(SWAP, ra_[i], 64 / CHA, lw + NL * i);
 #pragma unroll
-    for (int i = 0; i < IB; ++i) lb_[i] = lane_const(!SWAP, rb_[i], 64 / CHB, wave + NW * i);
+    for (int i = 0; i < IB; ++i) lb_[i] = lane_const(!SWAP, rb_[i], 64 / CHB, lw + NL * i);
   }
   // scalar step base (sb0, soy0, sox0) of pixel pbeg, advanced by 64 pixels per issued step
   int sb0 = 0, soy0 = 0, sox0 = 0;
@@ -254,12 +261,12 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
       const unsigned sg = (unsigned)sb0 * (unsigned)p.g_bs + (unsigned)sy * (unsigned)p.g_rs + (unsigned)sx * (unsigned)p.g_ps;
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
-        const int pc = wave + NW * i;
+        const int pc = lw + NL * i;
         if (pc < PA) fast_piece(SWAP, 64 / CHA, la_[i], SWAP ? sg : sd, sy, sx, tail, pc, sA);
       }
 #pragma unroll
       for (int i = 0; i < IB; ++i) {
-        const int pc = wave + NW * i;
+        const int pc = lw + NL * i;
         if (pc < PB) fast_piece(!SWAP, 64 / CHB, lb_[i], SWAP ? sd : sg, sy, sx, tail, pc, sB);
       }
       // advance the base by one step (64 pixels)
@@ -275,7 +282,7 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
     } else if constexpr (CHA == CHB && IA == IB) {  // A and B pieces cover the same pixel rows
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
-        const int pc = wave + NW * i;
+        const int pc = lw + NL * i;
         if (pc < PA) {
           const Pix px = pixel(64 / CHA, pc, s);
           dma_piece(SWAP, ra_[i], px, pc, sA);
@@ -285,12 +292,12 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
     } else {
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
-        const int pc = wave + NW * i;
+        const int pc = lw + NL * i;
         if (pc < PA) dma_piece(SWAP, ra_[i], pixel(64 / CHA, pc, s), pc, sA);
       }
 #pragma unroll
       for (int i = 0; i < IB; ++i) {
-        const int pc = wave + NW * i;
+        const int pc = lw + NL * i;
         if (pc < PB) dma_piece(!SWAP, rb_[i], pixel(64 / CHB, pc, s), pc, sB);
       }
     }
@@ -338,21 +345,59 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = exp_mfma(fa[i], fb[j], acc[i][j]);
 #if STC_SETPRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
     }
   };
 
-  if (nsteps > 0) issue(0, 0);
-  for (int s = 0; s < nsteps; ++s) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
-    compute(s & 1);
+  if constexpr (LD > 0) {
+    constexpr int P = IA + IB;  // pieces per loader wave per step (every wave issues all of its slots)
+    static_assert(IA * NL == PA && IB * NL == PB, "loader pieces split evenly");
+    if (wave >= NW) {  // loader: steps 0 .. NST-2 ahead, then one refill per step
+#pragma unroll
+      for (int i = 0; i < NST - 1; ++i)
+        if (i < nsteps) issue(i, i);
+      int nxt = NST - 1;
+      for (int s = 0; s < nsteps; ++s) {
+        const int ahead = min(NST - 2, nsteps - 1 - s);  // steps issued beyond s that may stay in flight
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (s + NST - 1 < nsteps) issue(s + NST - 1, nxt);  // into the stage step s - 1 used
+        nxt = nxt == NST - 1 ? 0 : nxt + 1;
+      }
+      return;  // (a terminated wave no longer counts at barriers)
+    }
+    int cur = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      __builtin_amdgcn_s_barrier();
+      compute(cur);
+      cur = cur == NST - 1 ? 0 : cur + 1;
+    }
+  } else {
+    if (nsteps > 0) issue(0, 0);
+    for (int s = 0; s < nsteps; ++s) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (s + 1 < nsteps) issue(s + 1, (s + 1) & 1);
+      compute(s & 1);
+    }
   }
 
+#if STC_EXP_NOEPI
+  {
+    float s_ = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) s_ += acc[i][j][0] + acc[i][j][3];
+    if (s_ == 1.2345f) p.ws[threadIdx.x] = s_;
+    return;
+  }
+#endif
   // epilogue: acc[i][j][e] = C[a0 + wm*TM + 16i + 4*(lane>>4) + e][b0 + wn*TN + 16j + (lane&15)]
   // (row, column) = (r, n) or, swapped, (n, r); n = tap*Cg + ci goes to dW[r][ci][tap].
   const int rq = 4 * (lane >> 4), cl = lane & 15;
@@ -405,14 +450,17 @@ __global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams
 struct WbCfg {
   int BM, BN, waves;
   bool swap;
+  int stages = 2, loaders = 0;
 };
 constexpr WbCfg kWbCfg[] = {
-    {128, 128, 4, false},  // 0
-    {64, 128, 4, false},   // 1: R <= 64
-    {128, 16, 4, true},    // 2: R <= 16 (rows = im2col columns, columns = R)
-    {256, 256, 8, false},  // 3
-    {256, 128, 8, false},  // 4
-    {128, 256, 8, false},  // 5
+    {128, 128, 4, false},        // 0
+    {64, 128, 4, false},         // 1: R <= 64
+    {128, 16, 4, true},          // 2: R <= 16 (rows = im2col columns, columns = R)
+    {256, 256, 8, false},        // 3
+    {256, 128, 8, false},        // 4
+    {128, 256, 8, false},        // 5
+    {128, 128, 4, false, 4, 4},  // 6: + 4 loader waves, 4-stage ring
+    {128, 128, 4, false, 3, 4},  // 7: + 4 loader waves, 3-stage ring
 };
 constexpr int kNumWbCfg = sizeof(kWbCfg) / sizeof(kWbCfg[0]);
 
@@ -452,7 +500,7 @@ static WbPlan wb_plan(int P, int R, int Cg, const int32_t* force) {
   } else {
     // about 2 four-wave blocks (one eight-wave block; 4 of the short swapped tile) per CU, at least
     // 8 K-steps (512 pixels) per split
-    const long long target = c.waves == 8 ? 256 : (c.swap ? 1024 : 512);
+    const long long target = (c.waves == 8 || c.loaders) ? 256 : (c.swap ? 1024 : 512);
     while (tiles * ns < target && ns * 2 <= 256 && steps / (ns * 2) >= 8) ns *= 2;
   }
   pl.pchunk = cdiv(steps, ns) * WB_BK;
@@ -510,7 +558,7 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
   const WbPlan pl = wb_plan(p.P, R, Cg, force);
   p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.nsplit = pl.nsplit; p.pchunk = pl.pchunk;
   dim3 grid(pl.mtiles * pl.ntiles, 1, pl.nsplit);
-  const size_t lds = 2 * (size_t)WB_BK * (pl.BM + pl.BN) * 2;
+  const size_t lds = (size_t)kWbCfg[pl.cfg].stages * WB_BK * (pl.BM + pl.BN) * 2;
   if (!pl.slab) {
     p.dW = dW;
   } else {
@@ -531,7 +579,15 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
       hipLaunchKernelGGL((wgrad_bf16_kernel<256, 256, 2, 4, false, false>), grid, dim3(512), lds, st, p);
       break;
     case 4: STC_WB(256, 128, 4, 2, false, 512) break;
-    default: STC_WB(128, 256, 2, 4, false, 512) break;
+    case 5: STC_WB(128, 256, 2, 4, false, 512) break;
+    case 6:
+      if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false, true, 4, 4>), grid, dim3(512), lds, st, p);
+      else hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false, false, 4, 4>), grid, dim3(512), lds, st, p);
+      break;
+    default:
+      if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false, true, 4, 3>), grid, dim3(512), lds, st, p);
+      else hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false, false, 4, 3>), grid, dim3(512), lds, st, p);
+      break;
   }
 #undef STC_WB
   main_timer_end(st);

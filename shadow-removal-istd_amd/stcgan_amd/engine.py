@@ -202,11 +202,18 @@ def _pad2(S, k):
     return (2 * S[k + 1][0], 2 * S[k + 1][1])
 
 
+def _fin_bn(bn):
+    """The BatchNorm whose backward sums are finalized inside the input-gradient conv (None: separate kernel)."""
+    return bn if ops.FUSE_FINALIZE else None
+
+
 def _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev):
     """Conv whose output feeds a BatchNorm2d: returns ((2, cout) scale/shift table, (mean, rstd) or None).
     Train mode: the batch statistics come out of the conv itself (stc_conv_fwd_ex)."""
     t = torch.empty((2, cout), dtype=torch.float32, device=dev)
-    if train:
+    if train and ops.FUSE_FINALIZE:
+        st = ops.conv_stats_fin(kind, B, xv, cin, w, cout, yv, dt, bn, t[0], t[1])
+    elif train:
         part, nch = ops.conv_stats(kind, B, xv, cin, w, cout, yv, dt)
         st = ops.bn_finalize_part(part, nch, cout, bn, t[0], t[1])
     else:
@@ -342,7 +349,7 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
         ops.conv_bn_backward(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt,
                              bn_x=L.nhwc_view(rq[k + 1]), C=C, bn_state=(t[0], t[1], mean, rstd),
                              gamma=bn.weight, s_self=0.0, ch_off=C, dxv=L.nhwc_view(dq),
-                             dgamma=dest(bn.weight), dbeta=dest(bn.bias))
+                             dgamma=dest(bn.weight), dbeta=dest(bn.bias), bn=_fin_bn(bn))
         if need_w:
             W.done([plan.convT[k].weight], lane)
             W.done([bn.weight, bn.bias])
@@ -399,7 +406,7 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
             ops.conv_bn_backward(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt, bn_x=xv, C=cprev,
                                  bn_state=(t[0], t[1], mean, rstd), gamma=bn.weight, s_self=LRELU,
                                  g_other=g1, s_other=0.0, dxv=L.nhwc_view(dr), dgamma=dest(bn.weight),
-                                 dbeta=dest(bn.bias))
+                                 dbeta=dest(bn.bias), bn=_fin_bn(bn))
             if need_w:
                 W.done([plan.conv[k].weight], lane)
                 W.done([bn.weight, bn.bias])
@@ -585,7 +592,7 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, W):
                                  bn_state=(tabs[i][0], tabs[i][1], mean, rstd), gamma=bn.weight,
                                  s_self=LRELU, dxv=L.nhwc_view(gn),
                                  dgamma=W.dest(bn.weight) if need_w else None,
-                                 dbeta=W.dest(bn.bias) if need_w else None)
+                                 dbeta=W.dest(bn.bias) if need_w else None, bn=_fin_bn(bn))
             if need_w:
                 W.done(own, lane)
                 W.done([bn.weight, bn.bias])

@@ -135,7 +135,7 @@ def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
     return part, nch
 
 
-# bf16 LDS-DMA tile configurations (csrc/igemm_bf16.hip kTiles): cfg -> (BM, BN, WM, WN, stages, BK)
+# bf16 LDS-DMA tile configurations (csrc/igemm_bf16.hip kTiles): cfg -> (BM, BN, WM, WN, stages, BK[, loader waves])
 _BF16_TILES = [(128, 128, 2, 2, 2, 64), (256, 128, 2, 2, 2, 64), (128, 64, 2, 2, 2, 64), (256, 64, 4, 1, 2, 64),
                (64, 128, 1, 4, 2, 64), (64, 64, 2, 2, 2, 64), (256, 256, 2, 4, 2, 64), (128, 256, 2, 4, 2, 64),
                (128, 128, 2, 2, 3, 64), (128, 256, 2, 4, 3, 64), (64, 128, 1, 4, 3, 64), (128, 64, 2, 2, 3, 64),
@@ -143,7 +143,8 @@ _BF16_TILES = [(128, 128, 2, 2, 2, 64), (256, 128, 2, 2, 2, 64), (128, 64, 2, 2,
                (128, 256, 2, 4, 4, 32), (128, 128, 2, 2, 4, 32), (128, 64, 2, 2, 4, 32), (64, 64, 2, 2, 4, 32),
                (128, 128, 2, 2, 3, 32), (128, 128, 2, 2, 2, 32), (256, 128, 4, 2, 3, 32), (128, 64, 2, 2, 3, 32),
                (128, 128, 2, 4, 2, 64), (128, 128, 4, 2, 2, 64), (128, 64, 4, 2, 2, 64), (256, 128, 4, 4, 2, 64),
-               (128, 256, 4, 4, 2, 64)]
+               (128, 256, 4, 4, 2, 64), (128, 128, 2, 2, 4, 64, 4), (128, 128, 2, 2, 3, 64, 4),
+               (256, 128, 4, 2, 3, 64, 4), (128, 64, 2, 2, 4, 64, 4)]
 
 
 def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
@@ -159,7 +160,8 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
         return "narrow_tiled_kernel", True
     if cfg >= 0:
         t = _BF16_TILES[cfg]
-        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}, {str(bnb).lower()}>", ks == 1
+        ld = f", {t[6]}" if len(t) > 6 else ""  # loader waves
+        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}, {str(bnb).lower()}{ld}>", ks == 1
     tname = {torch.float32: "float", torch.bfloat16: "__hip_bfloat16"}[dt]
     return f"igemm_kernel<{tname}, {bm}, {bn}>", ks == 1
 
@@ -173,7 +175,7 @@ def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=False):
 
 
 def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state, gamma, s_self, ch_off=0,
-                     g_other=None, s_other=0.0, dxv=None, dgamma=None, dbeta=None):
+                     g_other=None, s_other=0.0, dxv=None, dgamma=None, dbeta=None, bn=None):
     """Input-gradient conv (output yv) whose output feeds a BatchNorm backward, with the BN
     reduction fused into the conv (stc_conv_bwd_bn), then the BN apply (stc_bn_bwd_apply):
     dx = BN-backward of dn = out*act'(n, s_self) [+ g_other*act'(n, s_other)].
@@ -191,22 +193,80 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
     timer = _timer
     if timer is not None:
         e0, e1 = _main_events()
-    rc = l.stc_conv_bwd_bn(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse), ptr(part),
-                           nch, ptr(ws), nb, stream())
+    dgamma = _out1(dgamma, C, dev)
+    dbeta = _out1(dbeta, C, dev)
+    if bn is not None:  # dbeta/dgamma finalized inside the conv launch (stc_conv_bwd_bnfin)
+        cnt, scr = _fin_state(bn, C, dev, "bwd")
+        fin = L.BnFin(cnt.data_ptr(), scr.data_ptr(), None, None, None, None, None, 0.0, 0.0, None, None, None, None,
+                      ptr(dgamma), ptr(dbeta))
+        rc = l.stc_conv_bwd_bnfin(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse),
+                                  ptr(part), nch, ctypes.byref(fin), ptr(ws), nb, stream())
+    else:
+        rc = l.stc_conv_bwd_bn(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse),
+                               ptr(part), nch, ptr(ws), nb, stream())
     if timer is not None:
         _disarm()
-    check(rc, "stc_conv_bwd_bn")
+    check(rc, "stc_conv_bwd_bnfin" if bn is not None else "stc_conv_bwd_bn")
     if timer is not None:
         _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=yv.cs == 1)
     # apply: g1 = the conv output at the BN channels over the BN extent
     g1 = L.View(yv.p, bn_x.H, bn_x.W, yv.bs, yv.rs, yv.ps, yv.co + ch_off, yv.cs, 0)
     g1._keep = yv
-    dgamma = _out1(dgamma, C, dev)
-    dbeta = _out1(dbeta, C, dev)
     check(l.stc_bn_bwd_apply(L.dtype_code(dt), B, bn_x, C, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), ptr(gamma),
                              g1, float(s_self), g_other if g_other is not None else L.NULL_VIEW, float(s_other),
-                             ptr(part), nch, dxv, ptr(dgamma), ptr(dbeta), stream()), "stc_bn_bwd_apply")
+                             None if bn is not None else ptr(part), 0 if bn is not None else nch, dxv, ptr(dgamma),
+                             ptr(dbeta), stream()), "stc_bn_bwd_apply")
     return dgamma, dbeta
+
+
+# BatchNorm finalize fused into the producing conv (stc_conv_fwd_bnfin / stc_conv_bwd_bnfin); STC_BNFIN=0 runs
+# the separate finalize kernels (default until the A/B favours the fused form)
+FUSE_FINALIZE = os.environ.get("STC_BNFIN", "0") != "0"
+
+
+def _fin_state(bn, C, dev, which):
+    """Per-BatchNorm (module, device, forward/backward) counters and level-2 scratch of the finalize fused
+    into the producing conv (stc_bn_fin): the counters are zeroed once here and left zero by every call."""
+    key = (str(dev), which)
+    states = bn.__dict__.setdefault("_stc_fin", {})
+    st = states.get(key)
+    if st is None or st[1].numel() < 64 * C * 4:
+        st = (torch.zeros(lib().stc_bn_fin_counters(), dtype=torch.int32, device=dev),
+              torch.empty(64 * C * 4, dtype=torch.float32, device=dev))
+        states[key] = st
+    return st
+
+
+def conv_stats_fin(kind, B, xv, cin, w_packed, cout, yv, dt, bn, scale_out, shift_out, bias=None, force=None):
+    """Conv forward + its BatchNorm's batch statistics, finalized inside the conv launch
+    (stc_conv_fwd_bnfin: the producer's last-arriving blocks merge the partials and write the tables and the
+    running statistics -- no separate finalize kernel).  Returns (mean, rstd)."""
+    dev = w_packed.device
+    gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
+    if force is None and FORCE_CONV:
+        force = FORCE_CONV.get((kind, B, gh, gw, cin, cout))
+    nbytes, nch, plan = conv_query(kind, B, gh, gw, cin, cout, dt, force=force)
+    ws, nb = _ws(nbytes, dev)
+    part = torch.empty((nch, cout, 4), dtype=torch.float32, device=dev)
+    mean = torch.empty(cout, dtype=torch.float32, device=dev)
+    rstd = torch.empty(cout, dtype=torch.float32, device=dev)
+    cnt, scr = _fin_state(bn, cout, dev, "fwd")
+    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+    fin = L.BnFin(cnt.data_ptr(), scr.data_ptr(), ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
+                  ptr(bn.running_var), ptr(bn.num_batches_tracked), float(mom), float(bn.eps), ptr(mean), ptr(rstd),
+                  ptr(scale_out), ptr(shift_out), None, None)
+    fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
+    timer = _timer
+    if timer is not None:
+        e0, e1 = _main_events()
+    rc = lib().stc_conv_fwd_bnfin(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ptr(bias), ptr(part),
+                                  nch, ctypes.byref(fin), fp, ptr(ws), nb, stream())
+    if timer is not None:
+        _disarm()
+    check(rc, "stc_conv_fwd_bnfin")
+    if timer is not None:
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+    return mean, rstd
 
 
 def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True):
