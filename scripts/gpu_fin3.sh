@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/fin3
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread \
+STC_BNFIN=1 timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread \
   -k "streams or c3 or model or dist or extras or bn" > $O/suite.log 2>&1
 rc=$?
 echo "suite rc=$rc" >> $O/suite.log

@@ -19,7 +19,7 @@ from stcgan_amd import ops  # noqa: E402
 from stcgan_amd.stcgan import STCGAN  # noqa: E402
 
 BF = torch.bfloat16
-CFGS = range(6)
+CFGS = range(8)
 SPLITS = tuple(int(v) for v in os.environ.get("WG_SPLITS", "0,1,2,4,8,16,32,64").split(","))
 MIN_P = int(os.environ.get("WG_MIN_P", "0"))
 WG_CFGS = os.environ.get("WG_CFGS")
@@ -31,11 +31,12 @@ def record():
     probs = {}
     orig = ops.wgrad
 
-    def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None):
-        if dt == BF and dpro is None and gpro is None and dslope is None and gslope is None:
+    def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None,
+              **kw):
+        if dt == BF and dpro is None and gpro is None and dslope is None and gslope is None and not kw.get("rows"):
             k = (B, stride, Dv.H, Dv.W, Gv.H, Gv.W, R, Cg, Cg_out)
             probs[k] = probs.get(k, 0) + 1
-        return orig(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro, dslope, gpro, gslope, device)
+        return orig(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro, dslope, gpro, gslope, device, **kw)
 
     ops.wgrad = wgrad
     a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5, beta2=0.999,

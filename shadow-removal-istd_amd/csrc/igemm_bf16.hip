@@ -16,6 +16,8 @@
 //     statistics of the tile fused in (two-pass: tile mean, then centred sum of
 //     squares, in fp32 from the accumulators) -> part[tile][n] = {count, 0, M2, mean},
 //     the format stc_bn_finalize merges (Chan's parallel variance).
+#include <cstdlib>
+
 #include "common.hpp"
 #include "bnfin.hpp"
 
@@ -949,14 +951,29 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
     ks = force_ks > 0 ? force_ks : 1;
   } else {
     int order[5], no = 0;
-    if (N >= 256) {
-      if ((long long)M * nphase >= 8192 && K >= 8192) {  // long reductions: 8-wave 128x256 (s1 dgrad)
+    // The loader-wave tiles 29 / 31 win these layers in isolation (profiles/r03/diag/loader_tiles_conv.log,
+    // up to 20 %) but lose 0.36 ms per train step in situ: one of their blocks fills a CU's LDS, so the
+    // side streams' kernels cannot share it.  STC_PLAN_R3=1 selects them (A/B).
+    static const bool r3 = getenv("STC_PLAN_R3") != nullptr;
+    if (!r3 && N >= 256) {
+      if ((long long)M * nphase >= 8192 && K >= 8192) {
         order[0] = 6; order[1] = 7; order[2] = 0; order[3] = 4; order[4] = 5; no = 5;
       } else if ((long long)M * nphase >= 8192) { order[0] = 6; order[1] = 0; order[2] = 4; order[3] = 5; }
       else { order[0] = 0; order[1] = 4; order[2] = 12; order[3] = 5; }
       if (no == 0) no = 4;
-    } else if (N >= 128) {
+    } else if (!r3 && N >= 128) {
       order[0] = 0; order[1] = 4; order[2] = 5; no = 3;
+    } else if (N >= 256) {
+      if ((long long)M * nphase >= 8192 && K >= 8192) {  // long reductions: 8-wave 128x256 (s1 dgrad)
+        order[0] = 6; order[1] = 7; order[2] = 0; order[3] = 4; order[4] = 5; no = 5;
+      } else if ((long long)M * nphase >= 16384) { order[0] = 31; order[1] = 6; order[2] = 0; order[3] = 4; order[4] = 5; no = 5; }
+      else if (nphase == 1 && M >= 2048 && M < 8192 && K >= 4096) {  // e5: 128x128 + loaders, 4-way split-K
+        order[0] = 29; no = 1;
+      } else { order[0] = 29; order[1] = 0; order[2] = 4; order[3] = 12; order[4] = 5; no = 5; }
+      if (no == 0) no = 4;
+    } else if (N >= 128) {
+      if (K >= 2048 && (long long)M * nphase >= 65536) { order[0] = 31; order[1] = 0; order[2] = 4; order[3] = 5; no = 4; }
+      else { order[0] = 0; order[1] = 4; order[2] = 5; no = 3; }
     } else if (K <= 128) {  // first layers (Cin = 8): 3-stage BK = 32, 3-4 blocks per CU
       order[0] = 23; order[1] = 2; order[2] = 5; no = 3;
     } else if (K <= 512) {  // (Cin = 128 ConvT-geometry dgrads: the 3-stage BK = 32 128x64 tile, -9 %)
@@ -968,7 +985,7 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
       if (k > 1 && (ksteps / k < 8 || !allow_split)) break;
       for (int i = 0; i < no; ++i) {
         const int c = order[i];
-        const long long need = (c == 6 || c == 7 || c == 9) ? 240 : 400;
+        const long long need = (c == 6 || c == 7 || c == 9 || tile_loaders(c)) ? 240 : 400;
         if (tiles(c) * k >= need) { cfg = c; ks = k; break; }
       }
     }
@@ -1066,7 +1083,10 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     const int nct = pl.ksplit > 1 ? 1 : pl.ntiles;
     STC_REQUIRE(p.fin.ngroups <= BNFIN_MAXG && p.fin.ngroups * nct <= BNFIN_L1 && nct <= BNFIN_L2,
                 "bf16 igemm: finalize grouping %d x %d out of range", p.fin.ngroups, nct);
-    fin_after = pl.ksplit > 1 && pr.wide;
+    // In-launch only behind the split-K reduction (a short grid): in the main GEMM every block would have to
+    // drain its output stores before its ticket, holding its CU slot one store latency longer per round of
+    // blocks -- measured +1 ms per train step against the separate finalize launch.
+    fin_after = !(pl.ksplit > 1 && !pr.wide);
     p.fin_on = fin_after ? 0 : 1;
   }
   p.ksplit = pl.ksplit; p.kchunk = pl.kchunk; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles;

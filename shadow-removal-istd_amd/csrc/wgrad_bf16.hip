@@ -15,6 +15,7 @@
 // step s+1 under the MFMAs of step s).  The pixel range is split over blockIdx.z into fp32 slabs
 // that wgrad_reduce_launch sums in a fixed order; a single split writes torch layout directly.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -485,7 +486,9 @@ static WbPlan wb_plan(int P, int R, int Cg, const int32_t* force) {
     if (R <= 16) cfg = 2;
     else if (R <= 64) cfg = 1;
     else if (ncol >= 1024 && ((R >= 512 && P >= 16384) || (R >= 256 && P >= 65536))) cfg = 3;
-    else cfg = 0;
+    // 128x128 + 4 loader waves, 3-stage ring (96 KiB: a 64 KiB conv block still fits beside it): 5-13 % under
+    // cfg 0 in isolation, -0.16 ms per train step in situ (profiles/r03/diag/plan_ab.log); STC_WPLAN_R2=1: cfg 0
+    else cfg = getenv("STC_WPLAN_R2") ? 0 : 7;
   }
   const WbCfg& c = kWbCfg[cfg];
   pl.cfg = cfg;

@@ -75,7 +75,8 @@ CASES = [  # B, Cin, Cout, H(grid), W(grid)
     (2, 8, 64, 64, 64),      # Cin = 8: a K-step spans 8 taps
     (1, 256, 64, 7, 9),
 ]
-CFGS = [None] + [(c, 1) for c in range(20)] + [(0, 2), (5, 4), (8, 2), (12, 4), (14, 2), (17, 4)]
+CFGS = ([None] + [(c, 1) for c in range(20)] + [(0, 2), (5, 4), (8, 2), (12, 4), (14, 2), (17, 4)] +
+        [(c, 1) for c in (29, 30, 31, 32)] + [(29, 4), (31, 2)])  # loader-wave tiles
 
 
 @pytest.mark.parametrize("force", CFGS, ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
@@ -90,7 +91,7 @@ def test_conv_s2(case, force):
 
 
 @pytest.mark.parametrize("force", [None, (0, 1), (1, 1), (3, 1), (5, 2), (8, 1), (9, 1), (13, 1), (11, 2), (14, 1),
-                                   (15, 1), (16, 1), (17, 2), (18, 1), (19, 1)],
+                                   (15, 1), (16, 1), (17, 2), (18, 1), (19, 1), (29, 1), (30, 2), (31, 1), (32, 1)],
                          ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 def test_convT_s2(case, force):
@@ -303,6 +304,15 @@ WGRAD_FORCED = [  # (case, tile config, pixel splits): the 8-wave tiles on ragge
     (("conv", 1, 2, 512, 8, 17, 17), 0, 4),     # R = 8 on a 128-row tile
     (("conv", 2, 1, 16, 128, 128, 128), 0, 3),  # mode 1 with an odd split count
     (("conv", 2, 5, 16, 64, 8, 8), 0, 2),       # mode 3, split boundary inside the pixel range
+    # loader-wave tiles (4 DMA-only waves, 4- / 3-stage ring): every pixel mode, ragged, split / unsplit
+    (("conv", 2, 2, 64, 256, 32, 32), 6, 0),
+    (("conv", 2, 2, 64, 256, 32, 32), 7, 1),
+    (("conv", 2, 3, 32, 96, 10, 14), 6, 3),
+    (("conv", 2, 3, 32, 96, 10, 14), 7, 0),
+    (("convT", 2, 2, 128, 64, 16, 16), 7, 2),
+    (("conv", 2, 1, 16, 128, 128, 128), 6, 3),
+    (("conv", 2, 5, 16, 64, 8, 8), 7, 2),
+    (("conv", 1, 2, 512, 8, 17, 17), 6, 4),
 ]
 
 
