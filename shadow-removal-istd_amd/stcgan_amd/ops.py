@@ -160,8 +160,8 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
         return "narrow_tiled_kernel", True
     if cfg >= 0:
         t = _BF16_TILES[cfg]
-        ld = f", {t[6]}" if len(t) > 6 else ""  # loader waves
-        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}, {str(bnb).lower()}{ld}>", ks == 1
+        ld = t[6] if len(t) > 6 else 0  # loader waves
+        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}, {str(bnb).lower()}, {ld}>", ks == 1
     tname = {torch.float32: "float", torch.bfloat16: "__hip_bfloat16"}[dt]
     return f"igemm_kernel<{tname}, {bm}, {bn}>", ks == 1
 
@@ -286,7 +286,8 @@ def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True
 
 # bf16 weight-gradient tile configurations (csrc/wgrad_bf16.hip kWbCfg): cfg -> (BM, BN, WM, WN, swapped)
 _WB_TILES = [(128, 128, 2, 2, "false"), (64, 128, 1, 4, "false"), (128, 16, 4, 1, "true"), (256, 256, 2, 4, "false"),
-             (256, 128, 4, 2, "false"), (128, 256, 2, 4, "false")]
+             (256, 128, 4, 2, "false"), (128, 256, 2, 4, "false"), (128, 128, 2, 2, "false", 4, 4),
+             (128, 128, 2, 2, "false", 4, 3)]  # (BM, BN, WM, WN, swapped[, loader waves, stages])
 
 
 def wgrad_query(B, Hd, Wd, R, Cg, dt, force=None):
@@ -303,12 +304,13 @@ def _wgrad_kernel_name(plan, Hd, Wd):
     cfg = plan[0]
     if cfg < 0:
         return "wgrad_kernel"
-    bm, bn, wm, wn, sw = _WB_TILES[cfg]
+    bm, bn, wm, wn, sw = _WB_TILES[cfg][:5]
+    ld, nst = _WB_TILES[cfg][5:] if len(_WB_TILES[cfg]) > 5 else (0, 2)
     ghw = Hd * Wd
     pow2 = lambda v: v > 0 and (v & (v - 1)) == 0  # noqa: E731
     fast = Wd % 64 == 0 or (pow2(Wd) and ghw % 64 == 0) or (pow2(ghw) and pow2(Wd) and 64 % ghw == 0)
     fast = fast and cfg != 3  # the 256x256 tile keeps the general addressing (register budget)
-    return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}>"
+    return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}, {ld}, {nst}>"
 
 
 # The narrow-R VALU weight gradient (stc_conv_wgrad_rows) for the PatchGAN logits layer (~25 us vs ~75 us
