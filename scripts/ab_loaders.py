@@ -16,12 +16,12 @@ from stcgan_amd import ops  # noqa: E402
 
 B = 32
 PROBS = [  # (name, prob, plain cfg of the same tile for the bit-identity check, loader cfgs)
-    ("e2 conv_s2 64x64 64->128", (L.CONV_S2, B, 64, 64, 128, 128, 64, 64, 64, 128), 0, (29, 30, 31)),
-    ("e3 conv_s2 32x32 128->256", (L.CONV_S2, B, 32, 32, 64, 64, 32, 32, 128, 256), 0, (29, 30, 31)),
-    ("d4 convT 16x16 1024->256", (L.CONVT_S2, B, 16, 16, 16, 16, 32, 32, 1024, 256), 0, (29, 30, 31)),
-    ("d3 convT 32x32 512->128", (L.CONVT_S2, B, 32, 32, 32, 32, 64, 64, 512, 128), 0, (29, 30, 31)),
-    ("d2 convT 64x64 256->64", (L.CONVT_S2, B, 64, 64, 64, 64, 128, 128, 256, 64), 11, (32,)),
-    ("e4 conv_s2 16x16 256->512", (L.CONV_S2, B, 16, 16, 32, 32, 16, 16, 256, 512), 0, (29, 30, 31)),
+    ("e2 conv_s2 64x64 64->128", (L.CONV_S2, B, 64, 64, 128, 128, 64, 64, 64, 128), 0, (33, 29, 31)),
+    ("e3 conv_s2 32x32 128->256", (L.CONV_S2, B, 32, 32, 64, 64, 32, 32, 128, 256), 0, (33, 29, 31)),
+    ("d4 convT 16x16 1024->256", (L.CONVT_S2, B, 16, 16, 16, 16, 32, 32, 1024, 256), 0, (33, 29, 31)),
+    ("d3 convT 32x32 512->128", (L.CONVT_S2, B, 32, 32, 32, 32, 64, 64, 512, 128), 0, (33, 29, 31)),
+    ("d2 convT 64x64 256->64", (L.CONVT_S2, B, 64, 64, 64, 64, 128, 128, 256, 64), 11, (34, 32)),
+    ("e4 conv_s2 16x16 256->512", (L.CONV_S2, B, 16, 16, 32, 32, 16, 16, 256, 512), 0, (33, 29, 31)),
 ]
 
 

@@ -17,7 +17,7 @@ from stcgan_amd import ops  # noqa: E402
 from stcgan_amd.stcgan import STCGAN  # noqa: E402
 
 BF = torch.bfloat16
-NCFG = 33
+NCFG = 36
 
 
 def record():

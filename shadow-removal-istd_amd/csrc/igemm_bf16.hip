@@ -155,9 +155,8 @@ __device__ __forceinline__ unsigned tap_spread(unsigned r, int lg) {
 // LD > 0: LD extra "loader" waves issue every LDS-DMA piece and the WM*WN compute waves only read
 // fragments and issue MFMAs (one barrier per K-step; the loaders run NST-1 steps ahead), so the DMA
 // issue never sits in a compute wave's instruction stream.
-template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB, int LD = 0>
-__global__ void __launch_bounds__(64 * (WM * WN + LD))
-igemm_bf16_kernel(const GParams p) {
+template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB, int LD>
+__device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
   constexpr int NW = WM * WN;
   constexpr int NL = LD > 0 ? LD : NW;   // waves that issue the DMA
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -680,6 +679,18 @@ igemm_bf16_kernel(const GParams p) {
     }
 }
 
+template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB>
+__global__ void __launch_bounds__(64 * WM * WN) igemm_bf16_kernel(const GParams p) {
+  igemm_bf16_body<BM, BN, WM, WN, NST, BK, BNB, 0>(p);
+}
+
+// Loader-wave blocks (LD extra DMA-only waves): LD = 2 -> two 6-wave blocks per CU (3 waves per SIMD, the
+// register budget capped to fit), LD = 4 -> one 8-wave block (2 waves per SIMD).
+template <int BM, int BN, int WM, int WN, int NST, int BK, bool BNB, int LD>
+__global__ void __launch_bounds__(64 * (WM * WN + LD), (LD == 2 ? 3 : 2)) igemm_bf16_ld_kernel(const GParams p) {
+  igemm_bf16_body<BM, BN, WM, WN, NST, BK, BNB, LD>(p);
+}
+
 // Split-K reduction: out[row] = sum_s slab[s][row] (+bias, tanh) -> bf16 16-byte stores, with the
 // BatchNorm partial statistics of the block's rows (shift = the block's first row, Chan-mergeable).
 // Thread = 8 consecutive channels of one GEMM row; the block walks a contiguous row range.
@@ -925,9 +936,12 @@ static const TileCfg kTiles[] = {
     {128, 128, 2, 2, 3, 64},  // 30: + 4 loader waves, 3 stages
     {256, 128, 4, 2, 3, 64},  // 31: + 4 loader waves, 3 stages (8 compute waves)
     {128, 64, 2, 2, 4, 64},   // 32: + 4 loader waves, 4 stages
+    {128, 128, 2, 2, 2, 64},  // 33: + 2 loader waves, 2 stages (64 KiB: two blocks per CU, as config 0)
+    {128, 64, 2, 2, 2, 64},   // 34: + 2 loader waves, 2 stages
+    {128, 256, 2, 4, 2, 64},  // 35: + 2 loader waves, 2 stages
 };
-// configurations whose blocks carry 4 loader waves besides the WM*WN compute waves
-static inline int tile_loaders(int cfg) { return cfg >= 29 ? 4 : 0; }
+// loader waves of a configuration's blocks besides the WM*WN compute waves
+static inline int tile_loaders(int cfg) { return cfg >= 33 ? 2 : (cfg >= 29 ? 4 : 0); }
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
 static size_t bf16_lds_bytes(int cfg) {
@@ -1000,6 +1014,9 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
     }
   }
   if (!allow_split) ks = 1;
+  // A/B hook: the same tiles with 2 loader waves (bit-identical; STC_PLAN_LD2=1)
+  static const bool ld2 = getenv("STC_PLAN_LD2") != nullptr;
+  if (ld2 && force_cfg < 0) cfg = cfg == 0 ? 33 : cfg == 7 ? 35 : (cfg == 2 || cfg == 11) ? 34 : cfg;
   const TileCfg& t = kTiles[cfg];
   pl.cfg = cfg;
   pl.BM = t.BM;
@@ -1112,12 +1129,12 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     else                                                                                                    \
       hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, false>), grid, dim3(64 * WM_ * WN_), lds, st, p); \
     break;
-#define STC_BL(I, BM_, BN_, WM_, WN_, NST_, BK_)                                                            \
+#define STC_BL(I, BM_, BN_, WM_, WN_, NST_, BK_, LD_)                                                       \
   case I:                                                                                                   \
     if (p.part2)                                                                                            \
-      hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, true, 4>), grid, dim3(64 * (WM_ * WN_ + 4)), lds, st, p); \
+      hipLaunchKernelGGL((igemm_bf16_ld_kernel<BM_, BN_, WM_, WN_, NST_, BK_, true, LD_>), grid, dim3(64 * (WM_ * WN_ + LD_)), lds, st, p); \
     else                                                                                                    \
-      hipLaunchKernelGGL((igemm_bf16_kernel<BM_, BN_, WM_, WN_, NST_, BK_, false, 4>), grid, dim3(64 * (WM_ * WN_ + 4)), lds, st, p); \
+      hipLaunchKernelGGL((igemm_bf16_ld_kernel<BM_, BN_, WM_, WN_, NST_, BK_, false, LD_>), grid, dim3(64 * (WM_ * WN_ + LD_)), lds, st, p); \
     break;
   main_timer_begin(st);
   switch (pl.cfg) {
@@ -1150,10 +1167,13 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     STC_B(26, 128, 64, 4, 2, 2, 64)
     STC_B(27, 256, 128, 4, 4, 2, 64)
     STC_B(28, 128, 256, 4, 4, 2, 64)
-    STC_BL(29, 128, 128, 2, 2, 4, 64)
-    STC_BL(30, 128, 128, 2, 2, 3, 64)
-    STC_BL(31, 256, 128, 4, 2, 3, 64)
-    STC_BL(32, 128, 64, 2, 2, 4, 64)
+    STC_BL(29, 128, 128, 2, 2, 4, 64, 4)
+    STC_BL(30, 128, 128, 2, 2, 3, 64, 4)
+    STC_BL(31, 256, 128, 4, 2, 3, 64, 4)
+    STC_BL(32, 128, 64, 2, 2, 4, 64, 4)
+    STC_BL(33, 128, 128, 2, 2, 2, 64, 2)
+    STC_BL(34, 128, 64, 2, 2, 2, 64, 2)
+    STC_BL(35, 128, 256, 2, 4, 2, 64, 2)
     default:
       return fail(-1, "bf16 igemm: bad tile config %d", pl.cfg);
   }

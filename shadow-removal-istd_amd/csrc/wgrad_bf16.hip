@@ -92,8 +92,8 @@ constexpr int WB_BK = 64;
 // becomes a 16-wide MFMA N tile instead of wasting 7/8 of a 128-row tile.
 // LD > 0: LD loader waves issue every LDS-DMA piece into an NST-stage ring, NST-1 steps ahead, and the
 // WM*WN compute waves only read fragments and issue MFMAs (one barrier per step).
-template <int BM, int BN, int WM, int WN, bool SWAP, bool FAST, int LD = 0, int NST = 2>
-__global__ void __launch_bounds__(64 * (WM * WN + LD)) wgrad_bf16_kernel(const WbParams p) {
+template <int BM, int BN, int WM, int WN, bool SWAP, bool FAST, int LD, int NST>
+__device__ __forceinline__ void wgrad_bf16_body(const WbParams& p) {
   constexpr int NW = WM * WN;
   constexpr int NL = LD > 0 ? LD : NW;                 // waves that issue the DMA
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -446,6 +446,17 @@ __global__ void __launch_bounds__(64 * (WM * WN + LD)) wgrad_bf16_kernel(const W
   }
 }
 
+template <int BM, int BN, int WM, int WN, bool SWAP, bool FAST>
+__global__ void __launch_bounds__(64 * WM * WN) wgrad_bf16_kernel(const WbParams p) {
+  wgrad_bf16_body<BM, BN, WM, WN, SWAP, FAST, 0, 2>(p);
+}
+
+// loader-wave blocks (LD DMA-only waves, NST-stage ring), 2 waves per SIMD
+template <int BM, int BN, int WM, int WN, bool SWAP, bool FAST, int LD, int NST>
+__global__ void __launch_bounds__(64 * (WM * WN + LD), 2) wgrad_bf16_ld_kernel(const WbParams p) {
+  wgrad_bf16_body<BM, BN, WM, WN, SWAP, FAST, LD, NST>(p);
+}
+
 // ------------------------------------------------------------------------- host
 // Tile configurations: {BM (rows), BN (columns), waves, swapped}
 struct WbCfg {
@@ -584,12 +595,12 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
     case 4: STC_WB(256, 128, 4, 2, false, 512) break;
     case 5: STC_WB(128, 256, 2, 4, false, 512) break;
     case 6:
-      if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false, true, 4, 4>), grid, dim3(512), lds, st, p);
-      else hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false, false, 4, 4>), grid, dim3(512), lds, st, p);
+      if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_ld_kernel<128, 128, 2, 2, false, true, 4, 4>), grid, dim3(512), lds, st, p);
+      else hipLaunchKernelGGL((wgrad_bf16_ld_kernel<128, 128, 2, 2, false, false, 4, 4>), grid, dim3(512), lds, st, p);
       break;
     default:
-      if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false, true, 4, 3>), grid, dim3(512), lds, st, p);
-      else hipLaunchKernelGGL((wgrad_bf16_kernel<128, 128, 2, 2, false, false, 4, 3>), grid, dim3(512), lds, st, p);
+      if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_ld_kernel<128, 128, 2, 2, false, true, 4, 3>), grid, dim3(512), lds, st, p);
+      else hipLaunchKernelGGL((wgrad_bf16_ld_kernel<128, 128, 2, 2, false, false, 4, 3>), grid, dim3(512), lds, st, p);
       break;
   }
 #undef STC_WB

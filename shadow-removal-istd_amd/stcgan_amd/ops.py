@@ -144,7 +144,8 @@ _BF16_TILES = [(128, 128, 2, 2, 2, 64), (256, 128, 2, 2, 2, 64), (128, 64, 2, 2,
                (128, 128, 2, 2, 3, 32), (128, 128, 2, 2, 2, 32), (256, 128, 4, 2, 3, 32), (128, 64, 2, 2, 3, 32),
                (128, 128, 2, 4, 2, 64), (128, 128, 4, 2, 2, 64), (128, 64, 4, 2, 2, 64), (256, 128, 4, 4, 2, 64),
                (128, 256, 4, 4, 2, 64), (128, 128, 2, 2, 4, 64, 4), (128, 128, 2, 2, 3, 64, 4),
-               (256, 128, 4, 2, 3, 64, 4), (128, 64, 2, 2, 4, 64, 4)]
+               (256, 128, 4, 2, 3, 64, 4), (128, 64, 2, 2, 4, 64, 4), (128, 128, 2, 2, 2, 64, 2),
+               (128, 64, 2, 2, 2, 64, 2), (128, 256, 2, 4, 2, 64, 2)]
 
 
 def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
@@ -160,8 +161,10 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
         return "narrow_tiled_kernel", True
     if cfg >= 0:
         t = _BF16_TILES[cfg]
-        ld = t[6] if len(t) > 6 else 0  # loader waves
-        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}, {str(bnb).lower()}, {ld}>", ks == 1
+        if len(t) > 6:  # loader-wave blocks
+            return (f"igemm_bf16_ld_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}, {str(bnb).lower()}, {t[6]}>",
+                    ks == 1)
+        return f"igemm_bf16_kernel<{t[0]}, {t[1]}, {t[2]}, {t[3]}, {t[4]}, {t[5]}, {str(bnb).lower()}>", ks == 1
     tname = {torch.float32: "float", torch.bfloat16: "__hip_bfloat16"}[dt]
     return f"igemm_kernel<{tname}, {bm}, {bn}>", ks == 1
 
@@ -310,7 +313,9 @@ def _wgrad_kernel_name(plan, Hd, Wd):
     pow2 = lambda v: v > 0 and (v & (v - 1)) == 0  # noqa: E731
     fast = Wd % 64 == 0 or (pow2(Wd) and ghw % 64 == 0) or (pow2(ghw) and pow2(Wd) and 64 % ghw == 0)
     fast = fast and cfg != 3  # the 256x256 tile keeps the general addressing (register budget)
-    return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}, {ld}, {nst}>"
+    if ld:
+        return f"wgrad_bf16_ld_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}, {ld}, {nst}>"
+    return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}>"
 
 
 # The narrow-R VALU weight gradient (stc_conv_wgrad_rows) for the PatchGAN logits layer (~25 us vs ~75 us
