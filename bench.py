@@ -180,13 +180,14 @@ def roofline_of_step(tr, x, m, y, args, B, s):
     def timed_step(single):
         # single: one stream (no side-stream networks or weight gradients), so each launch's events bracket
         # it alone; else the bench's own overlapped step (in situ: kernels share the GPU with the lanes')
-        ops._timer = []
+        ops._timer, ops._call_timer = [], []
         lanes, overlap = tr.streams, engine.WGRAD_OVERLAP
         if single:
             tr.streams, engine.WGRAD_OVERLAP = False, False
         tr.train_step(x, m, y)
         torch.cuda.synchronize()
         launches, ops._timer = ops._timer, None
+        calls, ops._call_timer = ops._call_timer, None
         tr.streams, engine.WGRAD_OVERLAP = lanes, overlap
         per, shapes = {}, {}
         for name, _single, fl, e0, e1, desc in launches:
@@ -196,9 +197,14 @@ def roofline_of_step(tr, x, m, y, args, B, s):
             a[1] += fl
             a[2] += ms
             shapes.setdefault(name, []).append((round(ms * 1e3, 1), desc))
+        whole = {}  # weight-gradient calls: main kernel + split-pixel reduction
+        for name, c0, c1 in calls:
+            whole[name] = whole.get(name, 0.0) + c0.elapsed_time(c1)
+        timed_step.whole = whole
         return launches, per, shapes
 
     launches, per, shapes = timed_step(True)
+    whole_single = dict(timed_step.whole)
     dom = max(per, key=lambda k: per[k][2])
     n_dom, fl_dom, ms_dom = per[dom]
     peak = PEAK_TFLOPS[args.dtype]
@@ -251,8 +257,15 @@ def roofline_of_step(tr, x, m, y, args, B, s):
             break
     conv_ms = sum(v[2] for v in per.values())
     conv_gf = sum(v[1] for v in per.values()) / 1e9
+    incl = None  # the dominant kernel with its split-pixel reduction charged to it (weight gradients)
+    if dom in whole_single:
+        a_incl = fl_dom / (whole_single[dom] * 1e-3) / 1e12
+        incl = {"achieved": round(a_incl, 2), "frac": round(a_incl / peak, 4), "ms": round(whole_single[dom], 3),
+                "note": "HIP events around each whole stc_conv_wgrad_ex call of this kernel (main kernel + the "
+                        "fixed-order split reduction), single-stream step"}
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+            "frac": round(achieved / peak, 4), "with_reduction": incl,
+            "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_src": traffic_src,
             "frac_mode": "single-stream step (each launch alone); frac_in_situ: the same kernel in the bench's "
                          "overlapped step (side-stream networks and weight gradients on)",

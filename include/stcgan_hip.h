@@ -132,6 +132,19 @@ int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin, const void
                     const stc_bnb_fuse* bnb, float* part2, int nchunks,
                     void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ---- conv with an activation epilogue (the layers without BatchNorm) -----------------------------
+ * The outermost down conv of the generators (STCGAN/networks.py:99-101: conv, then LeakyReLU(0.2) for the
+ * next conv and -- in-place on the skip -- ReLU for the up path) and the PatchGAN's first conv
+ * (networks.py:165-166: conv + bias, LeakyReLU(0.2)).  Replaces stc_conv_fwd into a raw tensor followed by
+ * stc_bn_apply(table = NULL): y1 = act(v, slope1) and, when y2.p != NULL, y2 = act(v, slope2), computed from
+ * the bf16-rounded conv output v exactly as stc_bn_apply would (bit-identical), with no raw tensor written
+ * or re-read.  stc_conv_fwd_act_ok: 1 when the shape runs as one bf16 LDS-DMA GEMM launch with 16-byte
+ * NHWC views (else use the two-call form).                                                            */
+int stc_conv_fwd_act_ok(int dtype, int kind, int B, stc_view x, int Cin, int Cout, stc_view y1, stc_view y2);
+int stc_conv_fwd_act(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
+                     stc_view y1, float slope1, stc_view y2, float slope2, const float* bias,
+                     void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---- BatchNorm finalize fused into the producing conv (no finalize launch on the chain) ----------
  * Replaces, per BatchNorm2d of STCGAN/networks.py:107,109,170,179 (train mode), the pair
  * stc_conv_fwd_ex + stc_bn_finalize (forward) and the dbeta/dgamma reduction of stc_bn_bwd_apply

@@ -673,7 +673,9 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
 int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
-                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr);
+                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr,
+                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f);
+bool bf16_conv_act_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y1, const stc_view* y2);
 int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st);
 bool bf16_narrow_eligible(int kind, int Cin, int Cout);
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout);
@@ -938,4 +940,19 @@ extern "C" int stc_conv_bwd_bnfin(int dtype, int kind, int B, stc_view dy, int C
                                  workspace_bytes, stream);
   if (rc) return rc;
   return bnfin_fallback(f, part2, nchunks, bnb->C, true, st);
+}
+
+// ---- conv + activation epilogue (layers without BatchNorm)
+extern "C" int stc_conv_fwd_act_ok(int dtype, int kind, int B, stc_view x, int Cin, int Cout, stc_view y1, stc_view y2) {
+  if (kind < 0 || kind > 3 || !bf16_path(dtype, kind, Cin, Cout)) return 0;
+  return bf16_conv_act_ok(kind, B, x, Cin, Cout, y1, y2.p ? &y2 : nullptr) ? 1 : 0;
+}
+
+extern "C" int stc_conv_fwd_act(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
+                                stc_view y1, float slope1, stc_view y2, float slope2, const float* bias,
+                                void* workspace, int64_t workspace_bytes, void* stream) {
+  STC_REQUIRE(stc_conv_fwd_act_ok(dtype, kind, B, x, Cin, Cout, y1, y2),
+              "stc_conv_fwd_act: no activation epilogue for this shape (check stc_conv_fwd_act_ok)");
+  return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y1, bias, 0, 0, nullptr, 0, nullptr, workspace, workspace_bytes,
+                       (hipStream_t)stream, nullptr, nullptr, nullptr, &y2, y2.p ? 2 : 1, slope1, slope2);
 }

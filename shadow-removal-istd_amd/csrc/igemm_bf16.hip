@@ -65,7 +65,26 @@ struct GParams {
   // (part2) -> dbeta/dgamma, by the last-arriving blocks; stat_chunks = the chunk count of stats/part2
   int fin_on, stat_chunks;
   BnFin fin;
+  // Activation epilogue (layers with no BatchNorm: the first conv of G / D, STCGAN/networks.py:99,165-166):
+  // act_n = 1 or 2 activated copies of the bf16-rounded output, out1 = act(v, act_s1) into c (instead of the
+  // raw value), out2 = act(v, act_s2) into the c2 view -- what conv + stc_bn_apply(table = NULL) write, bit
+  // for bit, without the raw tensor and its re-read.
+  int act_n;
+  float act_s1, act_s2;
+  char* c2;
+  long long c2_bs, c2_rs;
+  int c2_ps, c2_co;
 };
+
+// 8 bf16 (one uint4) -> act(v, slope) per element, rounded back to bf16 (as stc_bn_apply with no table)
+__device__ __forceinline__ uint4 act_bf16x8(uint4 v, float slope) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+  unsigned o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    o[q] = pack_bf16x2(act(__uint_as_float(w[q] << 16), slope), act(__uint_as_float(w[q] & 0xffff0000u), slope));
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
 
 // {dn, dn*xhat} of 8 consecutive BN channels at one pixel (v: this conv's 8 output values)
 __device__ __forceinline__ void bnb_accum(const GParams& p, int b, int oy, int ox, int ch, const float* v, float* sa,
@@ -560,8 +579,17 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
         const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
         const unsigned off = (unsigned)b * (unsigned)p.c_bs + (unsigned)oy * (unsigned)p.c_rs + (unsigned)ox * (unsigned)p.c_ps +
                              cbase;
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) =
-            *reinterpret_cast<const uint4*>(tl + (r0 + it * RS) * PITCH + cc * 16);
+        const uint4 tv = *reinterpret_cast<const uint4*>(tl + (r0 + it * RS) * PITCH + cc * 16);
+        if (p.act_n == 0) {
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = tv;
+        } else {
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = act_bf16x8(tv, p.act_s1);
+          if (p.act_n == 2) {
+            const unsigned off2 = (unsigned)b * (unsigned)p.c2_bs + (unsigned)oy * (unsigned)p.c2_rs +
+                                  (unsigned)ox * (unsigned)p.c2_ps + (unsigned)(p.c2_co + n);
+            *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c2) + off2) = act_bf16x8(tv, p.act_s2);
+          }
+        }
         m += RS;
         x += RS;
         while (x >= p.GW) {
@@ -1236,7 +1264,8 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
 int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
-                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr) {
+                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr,
+                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f) {
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   GParams p{};
@@ -1280,7 +1309,27 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
     p.bs_self = bnb->slope_self; p.bs_other = bnb->slope_other;
     p.bC = bnb->C; p.bch_off = bnb->ch_off;
   }
+  if (act_n) {
+    STC_REQUIRE(p.vec_out && !bnb && !stats && !fin && (act_n == 1 || (act2 && act2->p)),
+                "bf16 conv: activation epilogue needs a 16-byte NHWC bf16 output and no statistics");
+    p.act_n = act_n; p.act_s1 = act_s1; p.act_s2 = act_s2;
+    if (act_n == 2) {
+      p.c2 = (char*)act2->p; p.c2_bs = act2->bs; p.c2_rs = act2->rs; p.c2_ps = act2->ps; p.c2_co = act2->co;
+    }
+  }
   return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st, fin);
+}
+
+// The activation epilogue applies when the layer runs as one LDS-DMA GEMM launch (no split-K) with 16-byte
+// NHWC bf16 views for both outputs.
+bool bf16_conv_act_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y1, const stc_view* y2) {
+  if (!bf16_conv_eligible(kind, B, x, Cin, Cout) || !vec_out_ok(B, y1, Cout, 0) || Cout % 8 != 0) return false;
+  if (y2 && y2->p && (!vec_out_ok(B, *y2, Cout, 0) || y2->H != y1.H || y2->W != y1.W)) return false;
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  const int Hg = kind == STC_CONVT_S2 ? x.H : y1.H, Wg = kind == STC_CONVT_S2 ? x.W : y1.W;
+  const Bf16Problem pr = bf16_problem(B * Hg * Wg, Cout, taps * Cin, g.nphase, nullptr, true);
+  return pr.pl.ksplit == 1;
 }
 
 }  // namespace stc

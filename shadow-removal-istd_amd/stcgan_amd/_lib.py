@@ -65,6 +65,8 @@ _SIGS = {
     "stc_conv_bwd_bn": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _i32, _vp, _i64, _vp]),
     "stc_conv_fwd_ex": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _i32, _i32, _vp, _i32, _vp, _vp,
                                _i64, _vp]),
+    "stc_conv_fwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View]),
+    "stc_conv_fwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _f32, View, _f32, _vp, _vp, _i64, _vp]),
     "stc_bn_fin_counters": (_i32, []),
     "stc_conv_fwd_bnfin": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _i32, _vp, _vp, _vp, _i64,
                                   _vp]),

@@ -241,7 +241,7 @@ def gen_forward(plan, sources, train, dt, cache, save):
     def cin_t(k):
         return co[k] if k == Lv - 1 else 2 * co[k]
 
-    rd = [_nhwc(B, *S[k + 1], co[k], dt, dev) for k in range(Lv)]
+    rd = [None] + [_nhwc(B, *S[k + 1], co[k], dt, dev) for k in range(1, Lv)]  # (rd[0]: below)
     ad = [_nhwc(B, *S[k + 1], co[k], dt, dev) if k < Lv - 1 else None for k in range(Lv)]
     cr = [_nhwc(B, *S[k + 1], cin_t(k), dt, dev) for k in range(Lv)]
     rq = [None] + [_nhwc(B, *_pad2(S, k), co[k - 1], dt, dev) for k in range(1, Lv)]
@@ -253,9 +253,15 @@ def gen_forward(plan, sources, train, dt, cache, save):
 
     # ---- down path
     w0 = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_FWD, co[0], cin_pad, dt)
-    ops.conv(L.CONV_S2, B, L.nhwc_view(xin), cin_pad, w0, co[0], L.nhwc_view(rd[0]), dt)
-    ops.bn_apply(B, L.nhwc_view(rd[0]), co[0], dt, None, L.nhwc_view(ad[0]), LRELU,
-                 L.nhwc_view(cr[0], 0), 0.0)
+    if ops.conv_act(L.CONV_S2, B, L.nhwc_view(xin), cin_pad, w0, co[0], L.nhwc_view(ad[0]), LRELU, dt,
+                    L.nhwc_view(cr[0], 0), 0.0):
+        # no raw r_0: its only reader, the backward's ReLU/LeakyReLU test, sees the same signs in ad[0]
+        rd[0] = ad[0]
+    else:
+        rd[0] = _nhwc(B, *S[1], co[0], dt, dev)
+        ops.conv(L.CONV_S2, B, L.nhwc_view(xin), cin_pad, w0, co[0], L.nhwc_view(rd[0]), dt)
+        ops.bn_apply(B, L.nhwc_view(rd[0]), co[0], dt, None, L.nhwc_view(ad[0]), LRELU,
+                     L.nhwc_view(cr[0], 0), 0.0)
     for k in range(1, Lv):
         wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
         if k <= Lv - 2:
@@ -481,17 +487,21 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None, stats_only=
             ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nchw_view(out), dt, bias=cv.bias,
                      out_f32=True)
             break
-        o = _nhwc(B, h, w, cout, dt, dev)
         tab, st = None, None
+        a = _nhwc(B, h, w, cout, dt, dev)
         if i >= 1:  # conv -> BatchNorm -> LeakyReLU (networks.py:167-180); no conv bias there
             assert cv.bias is None
+            o = _nhwc(B, h, w, cout, dt, dev)
             t, st = _conv_bn(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(o), dt,
                              plan.bns[i - 1], train, dev)
             tab = (t[0], t[1])
+            if not (stats_only and i == n - 2):  # (stats_only: only the logits layer reads this activation)
+                ops.bn_apply(B, L.nhwc_view(o), cout, dt, tab, L.nhwc_view(a), LRELU)
+        elif ops.conv_act(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(a), LRELU, dt, bias=cv.bias):
+            o = a  # no raw output: the backward's LeakyReLU test sees the same signs in the activation
         else:
+            o = _nhwc(B, h, w, cout, dt, dev)
             ops.conv(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(o), dt, bias=cv.bias)
-        a = _nhwc(B, h, w, cout, dt, dev)
-        if not (stats_only and i == n - 2):  # (stats_only: only the logits layer reads this activation)
             ops.bn_apply(B, L.nhwc_view(o), cout, dt, tab, L.nhwc_view(a), LRELU)
         raw.append(o)
         act.append(a)

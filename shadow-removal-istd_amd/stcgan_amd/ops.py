@@ -46,6 +46,9 @@ def _pro(pro):
 # (kernel, single-kernel call, flops, start event, end event, description); the events bracket the call's
 # MAIN kernel only (stc_time_next_main_kernel), not a split-K / split-pixel reduction it enqueues after it.
 _timer = None
+# when a list: wgrad() also appends (kernel, start, end) events around the WHOLE call (main kernel + its
+# split-pixel reduction), so that the roofline can charge the reduction to the kernel
+_call_timer = None
 
 
 def _main_events():
@@ -109,6 +112,37 @@ def conv_query(kind, B, gh, gw, cin, cout, dt, out_f32=False, force=None):
 # (B, Hd, Wd, R, Cg); values {tile config, splits}.  Empty in production.
 FORCE_CONV = {}
 FORCE_WGRAD = {}
+
+
+# conv + activation epilogue for the layers without BatchNorm (stc_conv_fwd_act); STC_ACT_EPI=0: conv + bn_apply
+FUSE_ACT = os.environ.get("STC_ACT_EPI", "1") != "0"
+
+
+def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bias=None):
+    """Conv whose output goes straight through LeakyReLU/ReLU (no BatchNorm): y1 = act(out, s1) [and
+    y2 = act(out, s2)] from the conv epilogue, bit-identical to conv + bn_apply(table None) without the raw
+    tensor.  Returns False (nothing launched) when the shape has no such epilogue: the caller then runs the
+    two-call form."""
+    l = lib()
+    y2 = y2v if y2v is not None else L.NULL_VIEW
+    if not FUSE_ACT or dt != torch.bfloat16 or not l.stc_conv_fwd_act_ok(L.dtype_code(dt), kind, B, xv, cin, cout,
+                                                                           y1v, y2):
+        return False
+    gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (y1v.H, y1v.W)
+    dev = w_packed.device
+    nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
+    ws, nb = _ws(nbytes, dev)
+    timer = _timer
+    if timer is not None:
+        e0, e1 = _main_events()
+    rc = l.stc_conv_fwd_act(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, y1v, float(s1), y2, float(s2),
+                            ptr(bias), ptr(ws), nb, stream())
+    if timer is not None:
+        _disarm()
+    check(rc, "stc_conv_fwd_act")
+    if timer is not None:
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+    return True
 
 
 def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
@@ -378,19 +412,27 @@ def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=Non
     dsc, dsh = _pro(dpro)
     gsc, gsh = _pro(gpro)
     fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
-    timer = _timer
+    timer, ctimer = _timer, _call_timer
     if timer is not None:
         e0, e1 = _main_events()
+    if ctimer is not None:
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
     rc = l.stc_conv_wgrad_ex(L.dtype_code(dt), B, stride, Dv, R, dsc, dsh, 0 if dslope is None else 1,
                              0.0 if dslope is None else float(dslope), Gv, Cg, Cg_out, gsc, gsh,
                              0 if gslope is None else 1, 0.0 if gslope is None else float(gslope), ptr(dW), fp,
                              ptr(ws), nb, stream())
+    if ctimer is not None:
+        c1.record()
     if timer is not None:
         _disarm()
     check(rc, "stc_conv_wgrad_ex")
-    if timer is not None:
+    if timer is not None or ctimer is not None:
         dma = dt == torch.bfloat16 and dpro is None and gpro is None and dslope is None and gslope is None
         name = _wgrad_kernel_name(plan, Dv.H, Dv.W) if dma else "wgrad_kernel"
+    if ctimer is not None:
+        ctimer.append((name, c0, c1))
+    if timer is not None:
         timer.append((name, not plan[4], 2.0 * B * Dv.H * Dv.W * R * 16 * Cg, e0, e1,
                       f"wgrad s{stride} P={B * Dv.H * Dv.W} R{R} Cg{Cg}"))
     return dW

@@ -118,15 +118,21 @@ def test_c3_generator_layers(name):
     for k in range(Lv):
         w = plan.conv[k].weight.detach()
         r = F.conv2d(prev, q(w), None, 2, 1)
-        C.bf16(f"fwd conv{k} raw", f(rd[k]), q(r))
+        if rd[k].data_ptr() == (ad[k].data_ptr() if ad[k] is not None else -1):
+            # activation epilogue (no BatchNorm, ops.conv_act): no raw tensor -- the activation of the
+            # bf16-rounded conv output is checked below against the torch conv
+            rdk = q(r)
+        else:
+            C.bf16(f"fwd conv{k} raw", f(rd[k]), q(r))
+            rdk = f(rd[k])
         if k in plan.bnd:
             mean, rstd = sv["st_d"][k]
             C.fp32(f"fwd bn_d{k} mean", mean, r.mean(dim=(0, 2, 3)), 1e-4)
             C.fp32(f"fwd bn_d{k} rstd", rstd, torch.rsqrt(r.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 1e-4)
             sc, sh = sv["tab_d"][k][0], sv["tab_d"][k][1]
-            n = f(rd[k]) * sc[None, :, None, None] + sh[None, :, None, None]
+            n = rdk * sc[None, :, None, None] + sh[None, :, None, None]
         else:
-            n = f(rd[k])
+            n = rdk
         if k < Lv - 1:
             C.bf16(f"fwd act{k} (conv{k + 1} input)", f(ad[k]), q(F.leaky_relu(n, 0.2)))
             prev = f(ad[k])
@@ -235,15 +241,19 @@ def test_c3_discriminator_layers(name):
             C.fp32("fwd logits", c.detach(), r, 1e-3)
             break
         r = F.conv2d(inp, q(w), cv.bias.detach() if cv.bias is not None else None, s, 1)
-        C.bf16(f"fwd conv{i} raw", f(raw[i + 1]), q(r))
+        if raw[i + 1].data_ptr() == act[i + 1].data_ptr():  # activation epilogue: no raw tensor (ops.conv_act)
+            rawi = q(r)
+        else:
+            C.bf16(f"fwd conv{i} raw", f(raw[i + 1]), q(r))
+            rawi = f(raw[i + 1])
         if tabs[i + 1] is not None:
             mean, rstd = stats[i + 1]
             C.fp32(f"fwd bn{i} mean", mean, r.mean(dim=(0, 2, 3)), 1e-4)
             C.fp32(f"fwd bn{i} rstd", rstd, torch.rsqrt(r.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 1e-4)
             sc, sh = tabs[i + 1]
-            n = f(raw[i + 1]) * sc[None, :, None, None] + sh[None, :, None, None]
+            n = rawi * sc[None, :, None, None] + sh[None, :, None, None]
         else:
-            n = f(raw[i + 1])
+            n = rawi
         C.bf16(f"fwd act{i + 1}", f(act[i + 1]), q(F.leaky_relu(n, 0.2)))
     # backward
     for i in range(n_l - 1, -1, -1):

@@ -76,7 +76,7 @@ CASES = [  # B, Cin, Cout, H(grid), W(grid)
     (1, 256, 64, 7, 9),
 ]
 CFGS = ([None] + [(c, 1) for c in range(20)] + [(0, 2), (5, 4), (8, 2), (12, 4), (14, 2), (17, 4)] +
-        [(c, 1) for c in (29, 30, 31, 32)] + [(29, 4), (31, 2)])  # loader-wave tiles
+        [(c, 1) for c in (29, 30, 31, 32, 33, 34, 35)] + [(29, 4), (31, 2), (33, 2)])  # loader-wave tiles
 
 
 @pytest.mark.parametrize("force", CFGS, ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
@@ -91,7 +91,8 @@ def test_conv_s2(case, force):
 
 
 @pytest.mark.parametrize("force", [None, (0, 1), (1, 1), (3, 1), (5, 2), (8, 1), (9, 1), (13, 1), (11, 2), (14, 1),
-                                   (15, 1), (16, 1), (17, 2), (18, 1), (19, 1), (29, 1), (30, 2), (31, 1), (32, 1)],
+                                   (15, 1), (16, 1), (17, 2), (18, 1), (19, 1), (29, 1), (30, 2), (31, 1), (32, 1), (33, 1),
+                                   (34, 1), (35, 1)],
                          ids=lambda f: "auto" if f is None else f"cfg{f[0]}_ks{f[1]}")
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 def test_convT_s2(case, force):
