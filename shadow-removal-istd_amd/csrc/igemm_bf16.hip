@@ -64,6 +64,7 @@ struct GParams {
   // BatchNorm finalize in this launch (bnfin.hpp): statistics -> tables (stats) or the backward sums
   // (part2) -> dbeta/dgamma, by the last-arriving blocks; stat_chunks = the chunk count of stats/part2
   int fin_on, stat_chunks;
+  int phase_major;  // grid linear over (tile, phase), phase fastest (set by the launcher)
   BnFin fin;
   // Activation epilogue (layers with no BatchNorm: the first conv of G / D, STCGAN/networks.py:99,165-166):
   // act_n = 1 or 2 activated copies of the bf16-rounded output, out1 = act(v, act_s1) into c (instead of the
@@ -197,16 +198,28 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
   const int wm = wave / WN, wn = wave % WN;
   const int lw = LD > 0 ? wave - NW : wave;  // index among the loading waves
 
-  const int nwg = p.mtiles * p.ntiles;
+  // XCD-aware bijective remap of the linear block id (blocks b, b+8, ... share an XCD).  phase_major (the
+  // 4-phase ConvT geometry without split-K): the grid is linear over (tile, phase) with the phase fastest,
+  // so the 4 phase blocks of a tile -- which read the same input pixels -- run side by side on one XCD
+  // and share its L2, instead of each phase sweeping the whole input a quarter of the launch apart.
+  const int nwg = p.mtiles * p.ntiles * (p.phase_major ? p.nphase : 1);
   int bid = blockIdx.x;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
+  int ph, split;
+  if (p.phase_major) {
+    ph = bid % p.nphase;
+    bid /= p.nphase;
+    split = 0;
+  } else {
+    ph = (int)blockIdx.z / p.ksplit;
+    split = (int)blockIdx.z % p.ksplit;
+  }
   const int mt = bid / p.ntiles, nt = bid % p.ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int z = blockIdx.z;
-  const int ph = z / p.ksplit, split = z % p.ksplit;
+  const int z = ph * p.ksplit + split;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
   const int nsteps = (kend - kbeg + BK - 1) / BK;
@@ -1148,7 +1161,10 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
   }
   if (stats || part2)
     STC_REQUIRE(stats_chunks >= pr.stats_chunks, "bf16 igemm: stats chunks %d < %d", stats_chunks, pr.stats_chunks);
-  dim3 grid(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
+  static const bool pm_on = getenv("STC_PHASE_MAJOR") == nullptr || atoi(getenv("STC_PHASE_MAJOR")) != 0;
+  p.phase_major = (pm_on && p.nphase > 1 && pl.ksplit == 1) ? 1 : 0;
+  dim3 grid = p.phase_major ? dim3(pl.mtiles * pl.ntiles * p.nphase, 1, 1)
+                            : dim3(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
   const size_t lds = bf16_lds_bytes(pl.cfg);
 #define STC_B(I, BM_, BN_, WM_, WN_, NST_, BK_)                                                             \
   case I:                                                                                                   \
