@@ -3,7 +3,7 @@
 // One launch covers every parameter tensor of an optimiser: a device table of
 // {param, grad, exp_avg, exp_avg_sq, numel, first_block} records; each block finds
 // its tensor by binary search over first_block.  HBM-bound: 16 B read + 12 B written
-// per element.
+// per element (+ 2 B per packed bf16 operand in adam_pack_kernel).
 #include "common.hpp"
 
 namespace stc {
@@ -68,6 +68,16 @@ __device__ __forceinline__ float adam_elem(float pi, float gi, float& mi, float&
   return pi + (-lr_over_bc1) * (mi / denom);
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ void st4(float* q, const float4& a) {  // NT: streaming store (not re-read this step)
+  if (NT) __builtin_nontemporal_store(f32x4{a.x, a.y, a.z, a.w}, reinterpret_cast<f32x4*>(q));
+  else *reinterpret_cast<float4*>(q) = a;
+}
+
+// XCD: blocks b, b+8, ... (one XCD) take consecutive tiles, so the neighbouring tiles whose packed bf16
+// runs share 128-byte lines are written through one L2 close together.  NT: p / m / v stored streaming.
+template <bool XCD, bool NT>
 __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, int ntensors, float lr_over_bc1,
                                                         float bc2_sqrt, float beta1, float beta2, float eps,
                                                         const float* __restrict__ coef) {
@@ -77,7 +87,11 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, 
     bc2_sqrt = coef[1];
   }
   int lo = 0, hi = ntensors - 1;
-  const int blk = blockIdx.x;
+  int blk = blockIdx.x;
+  if (XCD) {
+    const int nwg = gridDim.x, xcd = blk & 7, q = nwg >> 3, r = nwg & 7;
+    blk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (blk >> 3);
+  }
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (table[mid * AP_W + 5] <= blk) lo = mid;
@@ -137,9 +151,9 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, 
     a.y = adam_elem(a.y, gq.y, mq.y, vq.y, lr_over_bc1, bc2_sqrt, beta1, beta2, eps);
     a.z = adam_elem(a.z, gq.z, mq.z, vq.z, lr_over_bc1, bc2_sqrt, beta1, beta2, eps);
     a.w = adam_elem(a.w, gq.w, mq.w, vq.w, lr_over_bc1, bc2_sqrt, beta1, beta2, eps);
-    *reinterpret_cast<float4*>(p + e0[r]) = a;
-    *reinterpret_cast<float4*>(m + e0[r]) = mq;
-    *reinterpret_cast<float4*>(v + e0[r]) = vq;
+    st4<NT>(p + e0[r], a);
+    st4<NT>(m + e0[r], mq);
+    st4<NT>(v + e0[r], vq);
     tile[pl][t0][ql] = a.x; tile[pl][t0 + 1][ql] = a.y;
     tile[pl][t0 + 2][ql] = a.z; tile[pl][t0 + 3][ql] = a.w;
   }
@@ -257,6 +271,22 @@ __global__ __launch_bounds__(256) void grad_acc_kernel(GradAccArgs a) {
   }
 }
 
+// Variant of the update launches: STC_ADAM_VARIANT bit 0 XCD-grouped tiles, bit 1 streaming stores (read per
+// call so an A/B can switch it in one process).  Default 2: streaming p / m / v stores -- nothing reads them
+// again this step -- take the generators' update 961 -> 808 us and the train step -0.1 ms; the XCD grouping
+// gains nothing (profiles/r03/diag/adam_variants.log).  Every variant is bit-identical.
+typedef void (*AdamPackFn)(const long long*, int, float, float, float, float, float, const float*);
+static AdamPackFn adam_pack_fn() {
+  const char* e = getenv("STC_ADAM_VARIANT");
+  const int v = e ? atoi(e) : 2;
+  switch (v & 3) {
+    case 1: return adam_pack_kernel<true, false>;
+    case 2: return adam_pack_kernel<false, true>;
+    case 3: return adam_pack_kernel<true, true>;
+    default: return adam_pack_kernel<false, false>;
+  }
+}
+
 }  // namespace stc
 
 using namespace stc;
@@ -266,7 +296,7 @@ extern "C" int stc_adam_pack_step(const int64_t* table, int ntensors, int64_t to
   STC_REQUIRE(ntensors > 0 && step >= 1, "stc_adam_pack_step: bad arguments");
   const double bc1 = 1.0 - pow((double)beta1, (double)step);
   const double bc2 = 1.0 - pow((double)beta2, (double)step);
-  hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(adam_pack_fn(), dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
                      (const long long*)table, ntensors, (float)((double)lr / bc1), (float)sqrt(bc2), beta1, beta2, eps,
                      (const float*)nullptr);
   STC_CHECK_LAUNCH();
@@ -282,7 +312,7 @@ extern "C" int stc_adam_pack_step_dev(const int64_t* table, int ntensors, int64_
   hipLaunchKernelGGL(adam_coef_kernel, dim3(1), dim3(64), 0, st, (long long*)step_dev, lr_dev, bc1_tab, bc2s_tab,
                      tab_len, coef_dev);
   STC_CHECK_LAUNCH();
-  hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)total_blocks), dim3(256), 0, st, (const long long*)table,
+  hipLaunchKernelGGL(adam_pack_fn(), dim3((unsigned)total_blocks), dim3(256), 0, st, (const long long*)table,
                      ntensors, 0.f, 1.f, beta1, beta2, eps, (const float*)coef_dev);
   STC_CHECK_LAUNCH();
   return 0;
@@ -312,7 +342,7 @@ extern "C" int stc_adam_pack_apply(const int64_t* table, int ntensors, int64_t t
     lbc1 = (float)((double)lr / bc1);
     bc2s = (float)sqrt(bc2);
   }
-  hipLaunchKernelGGL(adam_pack_kernel, dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(adam_pack_fn(), dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
                      (const long long*)table, ntensors, lbc1, bc2s, beta1, beta2, eps, coef_dev);
   STC_CHECK_LAUNCH();
   return 0;

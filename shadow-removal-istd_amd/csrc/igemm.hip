@@ -674,8 +674,12 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
                   const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr,
-                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f);
+                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f,
+                  const struct BnAct* bna = nullptr);
 bool bf16_conv_act_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y1, const stc_view* y2);
+bool bf16_conv_bnact_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y);
+int bf16_conv_fwd_bnact(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
+                        const float* bias, const stc_bn_act& a, void* ws, int64_t ws_bytes, hipStream_t st);
 int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st);
 bool bf16_narrow_eligible(int kind, int Cin, int Cout);
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout);
@@ -955,4 +959,19 @@ extern "C" int stc_conv_fwd_act(int dtype, int kind, int B, stc_view x, int Cin,
               "stc_conv_fwd_act: no activation epilogue for this shape (check stc_conv_fwd_act_ok)");
   return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y1, bias, 0, 0, nullptr, 0, nullptr, workspace, workspace_bytes,
                        (hipStream_t)stream, nullptr, nullptr, nullptr, &y2, y2.p ? 2 : 1, slope1, slope2);
+}
+
+// ---- deep split-K layers: conv + BatchNorm (train) + activation in two launches
+extern "C" int stc_conv_fwd_bn_act_ok(int dtype, int kind, int B, stc_view x, int Cin, int Cout, stc_view y) {
+  if (kind < 0 || kind > 3 || !bf16_path(dtype, kind, Cin, Cout)) return 0;
+  return bf16_conv_bnact_ok(kind, B, x, Cin, Cout, y) ? 1 : 0;
+}
+
+extern "C" int stc_conv_fwd_bn_act(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
+                                   stc_view y, const float* bias, const stc_bn_act* a, void* workspace,
+                                   int64_t workspace_bytes, void* stream) {
+  STC_REQUIRE(a && stc_conv_fwd_bn_act_ok(dtype, kind, B, x, Cin, Cout, y),
+              "stc_conv_fwd_bn_act: no fused form for this shape (check stc_conv_fwd_bn_act_ok)");
+  return bf16_conv_fwd_bnact(kind, B, x, Cin, w_packed, Cout, y, bias, *a, workspace, workspace_bytes,
+                             (hipStream_t)stream);
 }

@@ -869,6 +869,213 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
   if (p.fin_on) bnfin_arrive_stats(p.fin, p.stats, p.stat_chunks, p.N, blockIdx.x, 0, p.N, 0, 1, fin_red);
 }
 
+// Deep split-K layers (<= 2048 GEMM rows: the 1x1 - 8x8 levels of the generators, STCGAN/networks.py:104-128):
+// the split-K reduction, the BatchNorm batch statistics, their finalize and the BN + activation apply as ONE
+// launch, where it was three (splitk_reduce_stats, bn_finalize, bn_apply).  A block owns 8 whole channels --
+// every row of them -- so no other block's data is needed: it sums the slabs (fixed order), writes the raw
+// bf16 output (the BN backward's input), takes the exact two-pass mean / centred sum of squares of the fp32
+// results (fixed-order block reduction in fp64), writes mean / rstd / scale / shift / running statistics,
+// then applies BN + activation to the bf16-rounded values (as stc_bn_apply does) into one or two views.
+struct BnAct {
+  const float *gamma, *beta;
+  float *rmean, *rvar;
+  long long* nbt;
+  float momentum, eps;
+  float *mean_o, *rstd_o, *scale, *shift;
+  char* a1;
+  long long a1_bs, a1_rs;
+  int a1_ps, a1_co;
+  float s1;
+  char* a2;  // optional second activation (null: none)
+  long long a2_bs, a2_rs;
+  int a2_ps, a2_co;
+  float s2;
+  int aH, aW;  // extent the activations cover (the decoder crops an odd level)
+};
+constexpr int BNA_T = 1024;     // threads per block (16 waves)
+constexpr int BNA_ITEMS = 2048;  // (slab group, row) items per launch: <= 2048 GEMM rows, 2 per thread
+
+// Slabs [s0, s1) of one GEMM row's 8 channels summed in order onto acc (groups of 4 slabs: 8 loads in flight).
+__device__ __forceinline__ void bna_slab_sum(const GParams& p, int row, int n, int s0, int s1, float* acc) {
+  const int ph = row / p.M, m = row - ph * p.M;
+  const long long MN = (long long)p.M * p.N;
+  const float* src = p.ws + ((long long)ph * p.ksplit * p.M + m) * p.N + n;
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    float4 x0[4], x1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      x0[u] = *reinterpret_cast<const float4*>(src + (s + u) * MN);
+      x1[u] = *reinterpret_cast<const float4*>(src + (s + u) * MN + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[0] += x0[u].x; acc[1] += x0[u].y; acc[2] += x0[u].z; acc[3] += x0[u].w;
+      acc[4] += x1[u].x; acc[5] += x1[u].y; acc[6] += x1[u].z; acc[7] += x1[u].w;
+    }
+  }
+  for (; s < s1; ++s) {
+    const float4 x0 = *reinterpret_cast<const float4*>(src + s * MN);
+    const float4 x1 = *reinterpret_cast<const float4*>(src + s * MN + 4);
+    acc[0] += x0.x; acc[1] += x0.y; acc[2] += x0.z; acc[3] += x0.w;
+    acc[4] += x1.x; acc[5] += x1.y; acc[6] += x1.z; acc[7] += x1.w;
+  }
+}
+
+// Grid: one block per 8 channels.  The slabs of a row are split into G contiguous groups (G = 1: the
+// separate reduce's exact order, bias first; G > 1: each group summed in order from 0, the groups added onto
+// the bias in group order through LDS) so that R * G items keep all 1024 threads loading: the deep levels
+// have few rows and many splits, and one thread walking every slab of a row was latency-bound.
+__global__ void __launch_bounds__(BNA_T) splitk_bn_act_kernel(const GParams p, const BnAct a, const int G) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* part = reinterpret_cast<float*>(smem);  // [G * R][8] group partials (G > 1)
+  __shared__ double red[BNA_T / 64][8];
+  __shared__ float tab[16];
+  const int n = blockIdx.x * 8;  // this block's 8 channels
+  const int R = p.nphase * p.M;
+  const int GHW = p.GH * p.GW;
+  const int t = threadIdx.x;
+  float bz[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bz[e] = p.bias ? p.bias[n + e] : 0.f;
+  float v[2][8];  // rows t and t + 1024 (fp32 results; rows past R hold 0)
+  // 1. slab sums
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int it = t + BNA_T * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    if (it >= R * G) continue;
+    if (G == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = bz[e];
+      bna_slab_sum(p, it, n, 0, p.ksplit, v[i]);
+    } else {
+      const int g = it / R, row = it - g * R;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      bna_slab_sum(p, row, n, g * p.ksplit / G, (g + 1) * p.ksplit / G, acc);
+      float4* d = reinterpret_cast<float4*>(part + (long long)it * 8);
+      d[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      d[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+  }
+  if (G > 1) {  // R * G <= 2048 with G >= 2: every row is t < 1024
+    __syncthreads();
+    if (t < R) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[0][e] = bz[e];
+      for (int g = 0; g < G; ++g) {
+        const float4* q = reinterpret_cast<const float4*>(part + ((long long)g * R + t) * 8);
+        const float4 x0 = q[0], x1 = q[1];
+        v[0][0] += x0.x; v[0][1] += x0.y; v[0][2] += x0.z; v[0][3] += x0.w;
+        v[0][4] += x1.x; v[0][5] += x1.y; v[0][6] += x1.z; v[0][7] += x1.w;
+      }
+    }
+  }
+  // raw bf16 output (the BatchNorm backward's input)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = t + BNA_T * i;
+    if (row >= R) continue;
+    const int ph = row / p.M, m = row - ph * p.M;
+    const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+    const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+    const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+    uint4 o;
+    o.x = pack_bf16x2(v[i][0], v[i][1]); o.y = pack_bf16x2(v[i][2], v[i][3]);
+    o.z = pack_bf16x2(v[i][4], v[i][5]); o.w = pack_bf16x2(v[i][6], v[i][7]);
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + (long long)b * p.c_bs + (long long)oy * p.c_rs +
+                              (long long)ox * p.c_ps + p.c_co + n) = o;
+  }
+  // 2. exact two-pass statistics of the fp32 results: wave butterflies, then the 16 waves in a fixed tree (fp64)
+  const int lane = t & 63, wv = t >> 6;
+  __shared__ double res[2][8];
+  auto block_sum8 = [&](const double* loc, double* out) {  // out: LDS, every thread reads it after the call
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      double d = loc[e];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      if (lane == 0) red[wv][e] = d;
+    }
+    __syncthreads();
+    if (t < 8) {
+      double w[BNA_T / 64];
+#pragma unroll
+      for (int k = 0; k < BNA_T / 64; ++k) w[k] = red[k][t];
+#pragma unroll
+      for (int h = BNA_T / 128; h > 0; h >>= 1)
+#pragma unroll
+        for (int k = 0; k < h; ++k) w[k] += w[k + h];
+      out[t] = w[0];
+    }
+    __syncthreads();
+  };
+  double loc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) loc[e] = (double)v[0][e] + (double)v[1][e];
+  block_sum8(loc, res[0]);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const double mu = res[0][e] / (double)R;
+    double q = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (t + BNA_T * i >= R) continue;
+      const double d = (double)v[i][e] - mu;
+      q += d * d;
+    }
+    loc[e] = q;
+  }
+  block_sum8(loc, res[1]);
+  // 3. finalize: tables + running statistics of the block's channels
+  if (t < 8) {
+    const int e = t;
+    const double mu = res[0][e] / (double)R, m2 = res[1][e];
+    bn_finalize_store(n + e, (double)R, mu, m2, a.gamma, a.beta, a.rmean, a.rvar, a.nbt, a.momentum, a.eps,
+                      a.mean_o, a.rstd_o, a.scale, a.shift);
+    const double var = m2 / (double)R;
+    const float rs = (float)(1.0 / sqrt(var + (double)a.eps));
+    const float sc = (a.gamma ? a.gamma[n + e] : 1.f) * rs;
+    tab[e] = sc;
+    tab[8 + e] = (a.beta ? a.beta[n + e] : 0.f) - (float)mu * sc;
+  }
+  __syncthreads();
+  float sc[8], sf[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sc[e] = tab[e]; sf[e] = tab[8 + e]; }
+  // 4. BN + activation of the bf16-rounded values (stc_bn_apply's arithmetic)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = t + BNA_T * i;
+    if (row >= R) continue;
+    const int ph = row / p.M, m = row - ph * p.M;
+    const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+    const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+    const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+    if (oy >= a.aH || ox >= a.aW) continue;
+    float xn[8];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const unsigned w = pack_bf16x2(v[i][e], v[i][e + 1]);
+      xn[e] = fmaf(__uint_as_float(w << 16), sc[e], sf[e]);
+      xn[e + 1] = fmaf(__uint_as_float(w & 0xffff0000u), sc[e + 1], sf[e + 1]);
+    }
+    uint4 o1;
+    o1.x = pack_bf16x2(act(xn[0], a.s1), act(xn[1], a.s1)); o1.y = pack_bf16x2(act(xn[2], a.s1), act(xn[3], a.s1));
+    o1.z = pack_bf16x2(act(xn[4], a.s1), act(xn[5], a.s1)); o1.w = pack_bf16x2(act(xn[6], a.s1), act(xn[7], a.s1));
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.a1) + (long long)b * a.a1_bs + (long long)oy * a.a1_rs +
+                              (long long)ox * a.a1_ps + a.a1_co + n) = o1;
+    if (a.a2) {
+      uint4 o2;
+      o2.x = pack_bf16x2(act(xn[0], a.s2), act(xn[1], a.s2)); o2.y = pack_bf16x2(act(xn[2], a.s2), act(xn[3], a.s2));
+      o2.z = pack_bf16x2(act(xn[4], a.s2), act(xn[5], a.s2)); o2.w = pack_bf16x2(act(xn[6], a.s2), act(xn[7], a.s2));
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.a2) + (long long)b * a.a2_bs + (long long)oy * a.a2_rs +
+                                (long long)ox * a.a2_ps + a.a2_co + n) = o2;
+    }
+  }
+}
+
 // The same reduction for few rows over many splits (the deep 1x1 - 4x4 layers): one wave per (row,
 // 8-channel group), lane l summing splits l, l + 64, ... in order, then a fixed xor butterfly.  Every
 // row is its own statistics chunk ({1, 0, 0, value}: Chan-mergeable) and, with the fused BN backward,
@@ -1128,9 +1335,14 @@ int bf16_igemm_query(int M, int N, int K, int nphase, const int32_t* force, int6
 int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st);
 
 int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_bytes, float* stats, int stats_chunks,
-                      hipStream_t st, const BnFin* fin) {
+                      hipStream_t st, const BnFin* fin, const BnAct* bna = nullptr) {
   Bf16Problem pr = bf16_problem(p.M, p.N, p.K, p.nphase, force, p.vec_out != 0);
   const BPlan& pl = pr.pl;
+  if (bna)
+    STC_REQUIRE(pl.ksplit > 1 && (long long)p.nphase * p.M <= BNA_ITEMS && p.N % 8 == 0 && p.vec_out && !stats &&
+                    !p.part2 && !fin,
+                "bf16 igemm: the fused split-K BatchNorm needs split K, <= %d rows and no other statistics",
+                BNA_ITEMS);
   p.fin_on = 0;
   p.stat_chunks = pr.stats_chunks;
   bool fin_after = false;  // the wide split-K reduction has no in-kernel finalize: a separate launch
@@ -1230,7 +1442,13 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     p.stats = stats;
     p.part2 = part2;
     const long long rows = (long long)p.nphase * p.M;
-    if (pr.wide) {
+    if (bna) {
+      STC_REQUIRE(rows <= BNA_ITEMS, "bf16 conv: fused split-K BatchNorm over %lld rows", rows);
+      int G = 1;
+      while (G * 2 <= p.ksplit && rows * G * 2 <= BNA_ITEMS) G *= 2;
+      const size_t lds = G > 1 ? (size_t)rows * G * 8 * sizeof(float) : 0;
+      hipLaunchKernelGGL(splitk_bn_act_kernel, dim3((unsigned)(p.N / 8)), dim3(BNA_T), lds, st, p, *bna, G);
+    } else if (pr.wide) {
       const long long units = rows * (p.N / 8);
       hipLaunchKernelGGL(splitk_reduce_wide_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, st, p);
     } else {
@@ -1281,7 +1499,8 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
                   const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr,
-                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f) {
+                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f,
+                  const BnAct* bna = nullptr) {
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   GParams p{};
@@ -1333,7 +1552,33 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
       p.c2 = (char*)act2->p; p.c2_bs = act2->bs; p.c2_rs = act2->rs; p.c2_ps = act2->ps; p.c2_co = act2->co;
     }
   }
-  return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st, fin);
+  return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st, fin, bna);
+}
+
+// The fused split-K BatchNorm applies when the layer's plan splits K and has <= 2048 GEMM rows.
+bool bf16_conv_bnact_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y) {
+  if (!bf16_conv_eligible(kind, B, x, Cin, Cout) || !vec_out_ok(B, y, Cout, 0) || Cout % 8 != 0) return false;
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  const int Hg = kind == STC_CONVT_S2 ? x.H : y.H, Wg = kind == STC_CONVT_S2 ? x.W : y.W;
+  const Bf16Problem pr = bf16_problem(B * Hg * Wg, Cout, taps * Cin, g.nphase, nullptr, true);
+  return pr.pl.ksplit > 1 && (long long)g.nphase * B * Hg * Wg <= BNA_ITEMS;
+}
+
+int bf16_conv_fwd_bnact(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
+                        const float* bias, const stc_bn_act& a, void* ws, int64_t ws_bytes, hipStream_t st) {
+  STC_REQUIRE(bf16_conv_bnact_ok(kind, B, x, Cin, Cout, y), "bf16 conv: no fused split-K BatchNorm for this shape");
+  STC_REQUIRE(a.scale && a.shift && a.a1.p && a.a1.cs == 1 && (!a.a2.p || a.a2.cs == 1),
+              "bf16 conv: fused BatchNorm needs scale/shift and NHWC activation views");
+  BnAct b{};
+  b.gamma = a.gamma; b.beta = a.beta; b.rmean = a.running_mean; b.rvar = a.running_var;
+  b.nbt = (long long*)a.num_batches_tracked; b.momentum = a.momentum; b.eps = a.eps;
+  b.mean_o = a.mean; b.rstd_o = a.rstd; b.scale = a.scale; b.shift = a.shift;
+  b.a1 = (char*)a.a1.p; b.a1_bs = a.a1.bs; b.a1_rs = a.a1.rs; b.a1_ps = a.a1.ps; b.a1_co = a.a1.co; b.s1 = a.slope1;
+  b.a2 = (char*)a.a2.p; b.a2_bs = a.a2.bs; b.a2_rs = a.a2.rs; b.a2_ps = a.a2.ps; b.a2_co = a.a2.co; b.s2 = a.slope2;
+  b.aH = a.a1.H; b.aW = a.a1.W;
+  return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, 0, 0, nullptr, 0, nullptr, ws, ws_bytes, st, nullptr,
+                       nullptr, nullptr, nullptr, 0, 0.f, 0.f, &b);
 }
 
 // The activation epilogue applies when the layer runs as one LDS-DMA GEMM launch (no split-K) with 16-byte

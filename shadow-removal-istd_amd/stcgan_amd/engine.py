@@ -265,10 +265,17 @@ def gen_forward(plan, sources, train, dt, cache, save):
     for k in range(1, Lv):
         wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
         if k <= Lv - 2:
-            tab_d[k], st_d[k] = conv_bn(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k],
-                                        L.nhwc_view(rd[k]), plan.bnd[k])
-            ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]), LRELU,
-                         L.nhwc_view(cr[k], 0), 0.0)
+            t = torch.empty((2, co[k]), dtype=torch.float32, device=dev)
+            st = ops.conv_bn_act(L.CONV_S2, B, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]), dt,
+                                 plan.bnd[k], t[0], t[1], L.nhwc_view(ad[k]), LRELU, L.nhwc_view(cr[k], 0),
+                                 0.0) if train else None
+            if st is not None:  # deep split-K level: reduction + statistics + finalize + apply in one launch
+                tab_d[k], st_d[k] = t, st
+            else:
+                tab_d[k], st_d[k] = conv_bn(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k],
+                                            L.nhwc_view(rd[k]), plan.bnd[k])
+                ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]),
+                             LRELU, L.nhwc_view(cr[k], 0), 0.0)
         else:  # innermost: no down-norm (STCGAN/networks.py:118-124)
             ops.conv(L.CONV_S2, B, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]), dt)
             ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, None, L.nhwc_view(cr[k]), 0.0)
@@ -276,10 +283,16 @@ def gen_forward(plan, sources, train, dt, cache, save):
     for k in range(Lv - 1, 0, -1):
         wt = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_FWD, co[k - 1], cin_t(k), dt)
         # statistics over the full ConvT extent (before the crop of an odd level)
-        tab_u[k], st_u[k] = conv_bn(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
-                                    plan.bnu[k])
-        ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
-                     L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
+        t = torch.empty((2, co[k - 1]), dtype=torch.float32, device=dev)
+        st = ops.conv_bn_act(L.CONVT_S2, B, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]), dt,
+                             plan.bnu[k], t[0], t[1], L.nhwc_view(cr[k - 1], co[k - 1], *S[k]), 0.0) if train else None
+        if st is not None:  # deep split-K level: one launch after the GEMM (statistics over the full extent)
+            tab_u[k], st_u[k] = t, st
+        else:
+            tab_u[k], st_u[k] = conv_bn(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
+                                        plan.bnu[k])
+            ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
+                         L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
     # ---- outermost: tanh(convT_0(cr[0]) + bias) -> NCHW fp32
     Ho, Wo = 2 * S[1][0], 2 * S[1][1]
     y = torch.empty((B, plan.out_c, Ho, Wo), dtype=torch.float32, device=dev)

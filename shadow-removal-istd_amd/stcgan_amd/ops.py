@@ -145,6 +145,45 @@ def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bi
     return True
 
 
+# deep split-K layers: conv + BatchNorm + activation in two launches (stc_conv_fwd_bn_act) -- opt-in
+# (STC_BN_ACT=1): a block must own whole channels, so the fused pass runs on N/8 blocks reading 32-byte
+# row pieces and measured slower (20-28 us) than the three full-chip launches it replaces
+FUSE_BN_ACT = os.environ.get("STC_BN_ACT", "0") == "1"
+
+
+def conv_bn_act(kind, B, xv, cin, w_packed, cout, yv, dt, bn, scale_out, shift_out, a1v, s1, a2v=None, s2=0.0):
+    """Deep split-K conv -> train-mode BatchNorm -> activation(s): yv gets the raw output, a1v = act(BN, s1)
+    [a2v = act(BN, s2)]; the BN tables go to scale_out / shift_out and the running statistics are updated.
+    Returns (mean, rstd), or None (nothing launched) when the shape has no fused form."""
+    l = lib()
+    if not FUSE_BN_ACT or dt != torch.bfloat16 or not l.stc_conv_fwd_bn_act_ok(L.dtype_code(dt), kind, B, xv, cin,
+                                                                                 cout, yv):
+        return None
+    gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
+    if FORCE_CONV and FORCE_CONV.get((kind, B, gh, gw, cin, cout)) is not None:
+        return None  # a forced plan runs through conv_stats
+    dev = w_packed.device
+    nbytes, _nch, _plan = conv_query(kind, B, gh, gw, cin, cout, dt)
+    ws, nb = _ws(nbytes, dev)
+    mean = torch.empty(cout, dtype=torch.float32, device=dev)
+    rstd = torch.empty(cout, dtype=torch.float32, device=dev)
+    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+    a = L.BnAct(ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), ptr(bn.num_batches_tracked),
+                float(mom), float(bn.eps), ptr(mean), ptr(rstd), ptr(scale_out), ptr(shift_out), a1v, float(s1),
+                a2v if a2v is not None else L.NULL_VIEW, float(s2))
+    timer = _timer
+    if timer is not None:
+        e0, e1 = _main_events()
+    rc = l.stc_conv_fwd_bn_act(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, None, ctypes.byref(a),
+                               ptr(ws), nb, stream())
+    if timer is not None:
+        _disarm()
+    check(rc, "stc_conv_fwd_bn_act")
+    if timer is not None:
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+    return mean, rstd
+
+
 def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
     """Conv forward + fused BatchNorm partial statistics of its output (stc_conv_fwd_ex).
     Returns (part [chunks, cout, 4] fp32, chunks) for bn_finalize."""
