@@ -51,6 +51,9 @@ def live():
     return t
 
 
+VARIANTS = [int(v) for v in os.environ.get("AB_VARIANTS", "0,1,2,3").split(",")]
+
+
 def run(variant, reps=10):
     os.environ["STC_ADAM_VARIANT"] = str(variant)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -85,4 +88,4 @@ if len(sys.argv) > 1 and sys.argv[1] == "hash":
           "  ".join(f"{k} {digest(v)}" for k, v in cats.items()))
     sys.exit(0)
 for _ in range(3):
-    print("  ".join(f"v{v} {run(v):8.1f} us" for v in (0, 1, 2, 3)), flush=True)
+    print("  ".join(f"v{v} {run(v):8.1f} us" for v in VARIANTS), flush=True)

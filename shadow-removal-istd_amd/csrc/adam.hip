@@ -69,18 +69,29 @@ __device__ __forceinline__ float adam_elem(float pi, float gi, float& mi, float&
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ void st4(float* q, const float4& a) {  // NT: streaming store (not re-read this step)
   if (NT) __builtin_nontemporal_store(f32x4{a.x, a.y, a.z, a.w}, reinterpret_cast<f32x4*>(q));
   else *reinterpret_cast<float4*>(q) = a;
 }
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float* q) {  // NT: streaming load (read once)
+  if (NT) {
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(q));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return *reinterpret_cast<const float4*>(q);
+}
 
-// XCD: blocks b, b+8, ... (one XCD) take consecutive tiles, so the neighbouring tiles whose packed bf16
-// runs share 128-byte lines are written through one L2 close together.  NT: p / m / v stored streaming.
-template <bool XCD, bool NT>
+// V bit 0 (XCD): blocks b, b+8, ... (one XCD) take consecutive tiles, so the neighbouring tiles whose packed
+// bf16 runs share 128-byte lines are written through one L2 close together.  Bit 1: p / m / v stored
+// streaming.  Bit 2: packed operands stored streaming.  Bit 3: the 4x4 weights' p / g / m / v loaded streaming.
+template <int V>
 __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, int ntensors, float lr_over_bc1,
                                                         float bc2_sqrt, float beta1, float beta2, float eps,
                                                         const float* __restrict__ coef) {
+  constexpr bool XCD = V & 1, NT = V & 2, NTP = V & 4, NTL = V & 8;
   __shared__ __attribute__((aligned(16))) float tile[16][16][20];  // [p][tap][q] (rows of 20: 16-byte aligned q quads)
   if (coef != nullptr) {  // device-resident step (graph replay): the coefficients adam_coef_kernel computed
     lr_over_bc1 = coef[0];
@@ -135,10 +146,10 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, 
     ok[r] = pl < np && ql < nq;
     e0[r] = ok[r] ? ((long long)(p0 + pl) * Q + q0) * 16 + 4 * lane : 0;
     if (ok[r]) {
-      pp[r] = *reinterpret_cast<const float4*>(p + e0[r]);
-      gg[r] = *reinterpret_cast<const float4*>(g + e0[r]);
-      mm[r] = *reinterpret_cast<const float4*>(m + e0[r]);
-      vv[r] = *reinterpret_cast<const float4*>(v + e0[r]);
+      pp[r] = ld4<NTL>(p + e0[r]);
+      gg[r] = ld4<NTL>(g + e0[r]);
+      mm[r] = ld4<NTL>(m + e0[r]);
+      vv[r] = ld4<NTL>(v + e0[r]);
     }
   }
 #pragma unroll
@@ -195,12 +206,11 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(const long long* table, 
       }
       if (c4 + 4 <= lim_c) {
         if (f32) {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) = make_float4(w[0], w[1], w[2], w[3]);
+          st4<NTP>(reinterpret_cast<float*>(out) + o, make_float4(w[0], w[1], w[2], w[3]));
         } else {
-          uint2 u;
-          u.x = pack_bf16x2(w[0], w[1]);
-          u.y = pack_bf16x2(w[2], w[3]);
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + o) = u;
+          const u32x2 u{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3])};
+          if (NTP) __builtin_nontemporal_store(u, reinterpret_cast<u32x2*>(reinterpret_cast<bf16*>(out) + o));
+          else *reinterpret_cast<u32x2*>(reinterpret_cast<bf16*>(out) + o) = u;
         }
       } else {
         for (int e = 0; e < lim_c - c4; ++e) {
@@ -271,19 +281,20 @@ __global__ __launch_bounds__(256) void grad_acc_kernel(GradAccArgs a) {
   }
 }
 
-// Variant of the update launches: STC_ADAM_VARIANT bit 0 XCD-grouped tiles, bit 1 streaming stores (read per
-// call so an A/B can switch it in one process).  Default 2: streaming p / m / v stores -- nothing reads them
-// again this step -- take the generators' update 961 -> 808 us and the train step -0.1 ms; the XCD grouping
-// gains nothing (profiles/r03/diag/adam_variants.log).  Every variant is bit-identical.
+// Variant of the update launches: STC_ADAM_VARIANT = adam_pack_kernel's V bits (read per call so an A/B can
+// switch it in one process).  Default 10: streaming p / m / v stores and streaming loads -- nothing re-reads
+// them this step -- take the generators' update 961 -> 730 us and the train step -0.2 ms (interleaved pairs);
+// streaming the packed operands is slower (the next forward reads them from the memory-side cache), the XCD
+// grouping gains nothing (profiles/r03/diag/adam_variants.log).  Every variant is bit-identical.
 typedef void (*AdamPackFn)(const long long*, int, float, float, float, float, float, const float*);
 static AdamPackFn adam_pack_fn() {
   const char* e = getenv("STC_ADAM_VARIANT");
-  const int v = e ? atoi(e) : 2;
-  switch (v & 3) {
-    case 1: return adam_pack_kernel<true, false>;
-    case 2: return adam_pack_kernel<false, true>;
-    case 3: return adam_pack_kernel<true, true>;
-    default: return adam_pack_kernel<false, false>;
+  const int v = e ? atoi(e) : 10;
+  switch (v & 15) {
+#define STC_AV(k) case k: return adam_pack_kernel<k>;
+    STC_AV(0) STC_AV(1) STC_AV(2) STC_AV(3) STC_AV(6) STC_AV(14)
+#undef STC_AV
+    default: return adam_pack_kernel<10>;
   }
 }
 
