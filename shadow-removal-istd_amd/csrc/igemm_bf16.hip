@@ -550,6 +550,41 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
     // bf16 tile through LDS: [BM][BN] with a 16-byte row pad, then 16-byte row stores
     constexpr int PITCH = BN * 2 + 16;
     char* tl = smem;
+    constexpr int CPR = BN / 8;  // 16-byte chunks per row (64*NW is a multiple of CPR: fixed cc per thread)
+    constexpr int ITER = BM * CPR / (64 * NW);
+    static_assert(ITER * 64 * NW == BM * CPR, "whole store iterations");
+    const int cc = tid % CPR;
+    const int n = n0 + cc * 8;
+    // fused BatchNorm backward: the BN-input / second-gradient rows of a group of G output rows (addresses
+    // independent of the GEMM result); the first group is issued before the tile staging below, so its
+    // memory latency overlaps the accumulator shuffle and the barrier
+    constexpr int G = ITER < 4 ? ITER : 4;
+    static_assert(ITER % G == 0, "whole groups");
+    const int nch = n - p.bch_off;  // BN channel of this thread's chunk
+    const bool bnb_on = nch >= 0 && nch < p.bC;
+    const int nchc = bnb_on ? nch : 0;
+    auto bnb_loads = [&](int it0, uint4* xr, uint4* gr, bool* ok) {
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int row = (tid + (it0 + u) * 64 * NW) / CPR;
+        const int m = m0 + row;
+        const bool in = m < p.M && n < p.N;
+        const int mm = in ? m : m0;
+        const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
+        const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+        const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
+        ok[u] = in && bnb_on && oy < p.bxH && ox < p.bxW;
+        const int oyc = ok[u] ? oy : 0, oxc = ok[u] ? ox : 0;
+        xr[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.bx) + (long long)b * p.bx_bs +
+                                                (long long)oyc * p.bx_rs + (long long)oxc * p.bx_ps + p.bx_co + nchc);
+        gr[u] = p.bg ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.bg) + (long long)b * p.bg_bs +
+                                                       (long long)oyc * p.bg_rs + (long long)oxc * p.bg_ps + p.bg_co + nchc)
+                     : make_uint4(0u, 0u, 0u, 0u);
+      }
+    };
+    uint4 pxr[G], pgr[G];
+    bool pok[G];
+    if constexpr (BNB) bnb_loads(0, pxr, pgr, pok);
     // Column pairs: lanes l and l^1 hold columns c and c^1 of the same 4 rows; one DPP lane swap of two
     // values gives the even lane rows 0-1 and the odd lane rows 2-3 of the pair, each written as one
     // bf16x2 dword (half the LDS stores of per-element 16-bit writes)
@@ -572,11 +607,6 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
         *reinterpret_cast<unsigned*>(dst + PITCH) = pack_bf16x2(sel(a1, x1), sel(x1, a3));
       }
     __syncthreads();
-    constexpr int CPR = BN / 8;  // 16-byte chunks per row (64*NW is a multiple of CPR: fixed cc per thread)
-    constexpr int ITER = BM * CPR / (64 * NW);
-    static_assert(ITER * 64 * NW == BM * CPR, "whole store iterations");
-    const int cc = tid % CPR;
-    const int n = n0 + cc * 8;
     if constexpr (!BNB) {
       // rows r0 + RS*it of this thread: the pixel (b, y, x) is advanced incrementally (element
       // offsets < 2^31: vec_out is only set when the whole output view fits)
@@ -619,37 +649,30 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
     float sa[8], sb[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { sa[e] = 0.f; sb[e] = 0.f; }
-    const int nch = n - p.bch_off;  // BN channel of this thread's chunk
-    const bool bnb_on = nch >= 0 && nch < p.bC;
-    const int nchc = bnb_on ? nch : 0;
     // groups of G rows: the BN-input / second-gradient loads of a group are in flight together
     // (one latency per group instead of one per row), then the reduction arithmetic
-    constexpr int G = ITER < 4 ? ITER : 4;
-    static_assert(ITER % G == 0, "whole groups");
+#pragma unroll
     for (int it0 = 0; it0 < ITER; it0 += G) {
       uint4 tv[G], xr[G], gr[G];
       bool ok[G];
+      if (it0 == 0) {
+#pragma unroll
+        for (int u = 0; u < G; ++u) { xr[u] = pxr[u]; gr[u] = pgr[u]; ok[u] = pok[u]; }
+      } else {
+        bnb_loads(it0, xr, gr, ok);
+      }
 #pragma unroll
       for (int u = 0; u < G; ++u) {
         const int row = (tid + (it0 + u) * 64 * NW) / CPR;
         const int m = m0 + row;
-        const bool in = m < p.M && n < p.N;
-        const int mm = in ? m : m0;
-        const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
-        const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
-        const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
         tv[u] = *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
-        if (in) {
+        if (m < p.M && n < p.N) {
+          const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+          const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+          const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
           const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = tv[u];
         }
-        ok[u] = in && bnb_on && oy < p.bxH && ox < p.bxW;
-        const int oyc = ok[u] ? oy : 0, oxc = ok[u] ? ox : 0;
-        xr[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.bx) + (long long)b * p.bx_bs +
-                                                (long long)oyc * p.bx_rs + (long long)oxc * p.bx_ps + p.bx_co + nchc);
-        gr[u] = p.bg ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.bg) + (long long)b * p.bg_bs +
-                                                       (long long)oyc * p.bg_rs + (long long)oxc * p.bg_ps + p.bg_co + nchc)
-                     : make_uint4(0u, 0u, 0u, 0u);
       }
 #pragma unroll
       for (int u = 0; u < G; ++u) {
