@@ -678,6 +678,9 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
                   const struct BnAct* bna = nullptr);
 bool bf16_conv_act_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y1, const stc_view* y2);
 bool bf16_conv_bnact_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y);
+bool halo8_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y1, const stc_view* y2);
+int halo8_conv_act(int B, const stc_view& x, const void* w_packed, const stc_view& y1, const stc_view* y2, int act_n,
+                   float s1, float s2, const float* bias, hipStream_t st);
 int bf16_conv_fwd_bnact(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
                         const float* bias, const stc_bn_act& a, void* ws, int64_t ws_bytes, hipStream_t st);
 int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st);
@@ -957,6 +960,8 @@ extern "C" int stc_conv_fwd_act(int dtype, int kind, int B, stc_view x, int Cin,
                                 void* workspace, int64_t workspace_bytes, void* stream) {
   STC_REQUIRE(stc_conv_fwd_act_ok(dtype, kind, B, x, Cin, Cout, y1, y2),
               "stc_conv_fwd_act: no activation epilogue for this shape (check stc_conv_fwd_act_ok)");
+  if (halo8_ok(kind, B, x, Cin, Cout, y1, &y2))  // the first layers (Cin = 8): input rows staged in LDS
+    return halo8_conv_act(B, x, w_packed, y1, &y2, y2.p ? 2 : 1, slope1, slope2, bias, (hipStream_t)stream);
   return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y1, bias, 0, 0, nullptr, 0, nullptr, workspace, workspace_bytes,
                        (hipStream_t)stream, nullptr, nullptr, nullptr, &y2, y2.p ? 2 : 1, slope1, slope2);
 }

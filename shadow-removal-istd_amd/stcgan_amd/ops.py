@@ -141,7 +141,8 @@ def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bi
         _disarm()
     check(rc, "stc_conv_fwd_act")
     if timer is not None:
-        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+        halo = kind == L.CONV_S2 and cin == 8 and cout == 64 and os.environ.get("STC_HALO8", "0") == "1"
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, name="halo8_conv_kernel" if halo else None)
     return True
 
 
@@ -242,8 +243,8 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
     return f"igemm_kernel<{tname}, {bm}, {bn}>", ks == 1
 
 
-def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=False):
-    name, single = kernel_name(kind, B, gh, gw, cin, cout, dt, bnb)
+def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=False, name=None):
+    name, single = (name, True) if name else kernel_name(kind, B, gh, gw, cin, cout, dt, bnb)
     outs = B * gh * gw * (4 if kind == L.CONVT_S2 else 1)
     taps = 4 if kind == L.CONVT_S2 else 16
     timer.append((name, single, 2.0 * outs * cout * taps * cin, e0, e1,
