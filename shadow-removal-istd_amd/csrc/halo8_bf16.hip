@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(H8_T) halo8_conv_kernel(const H8Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int RW = p.IW + 2;  // staged row: input columns -1 .. IW
   uint4* rows = reinterpret_cast<uint4*>(smem);
-  char* stg = smem + (size_t)4 * RW * 16;
+  char* stg = smem + (size_t)4 * RW * 16 * p.ro;  // after the ro staged row quads
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int cl = lane & 15, kq = lane >> 4;
   // B fragments: column fragment j, K step kk: W[16j + cl][32kk + 8kq .. +7]
