@@ -168,7 +168,7 @@ int halo8_conv_act(int B, const stc_view& x, const void* w_packed, const stc_vie
   const char* ge = getenv("STC_HALO8_GRID");  // (tuning hooks: blocks per CU, output rows per iteration)
   const char* re = getenv("STC_HALO8_RO");
   const long long per_cu = ge ? std::max(1, atoi(ge)) : 4;
-  p.ro = re ? std::max(1, std::min(4, atoi(re))) : 2;
+  p.ro = re ? std::max(1, std::min(4, atoi(re))) : 1;
   while (p.ro > 1 && (size_t)4 * (p.IW + 2) * 16 * p.ro > 96 * 1024) --p.ro;
   const long long iters = (nrows + p.ro - 1) / p.ro;
   const unsigned grid = (unsigned)std::min<long long>(iters, 256LL * per_cu);  // persistent blocks
