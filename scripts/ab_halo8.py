@@ -18,12 +18,10 @@ y = torch.empty((B, 128, 128, 64), device=dev, dtype=torch.bfloat16)
 mb = (x.numel() + y.numel()) * 2 / 1e6
 
 
-def run(halo, grid=None, ro=None, reps=50):
+def run(halo, grid=None, reps=50):
     os.environ["STC_HALO8"] = "1" if halo else "0"
     if grid:
         os.environ["STC_HALO8_GRID"] = str(grid)
-    if ro:
-        os.environ["STC_HALO8_RO"] = str(ro)
     for _ in range(3):
         ops.conv_act(L.CONV_S2, B, L.nhwc_view(x), 8, w, 64, L.nhwc_view(y), 0.2, torch.bfloat16)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -38,7 +36,7 @@ def run(halo, grid=None, ro=None, reps=50):
 for _ in range(2):
     t0 = run(False)
     line = f"gemm tile {t0:6.1f} us ({mb / t0:.2f} TB/s compulsory)"
-    for g, ro in ((4, 1), (2, 2), (3, 2), (4, 2), (2, 4), (3, 4)):
-        t = run(True, g, ro)
-        line += f" | halo {g}/CU ro{ro} {t:6.1f} us ({mb / t:.2f} TB/s)"
+    for g in (1, 2, 4, 8):
+        t = run(True, g)
+        line += f" | halo {g}/CU {t:6.1f} us ({mb / t:.2f} TB/s)"
     print(line, flush=True)
