@@ -145,73 +145,6 @@ int stc_conv_fwd_act(int dtype, int kind, int B, stc_view x, int Cin, const void
                      stc_view y1, float slope1, stc_view y2, float slope2, const float* bias,
                      void* workspace, int64_t workspace_bytes, void* stream);
 
-/* ---- deep split-K layers: conv + BatchNorm (train) + activation in two launches --------------------
- * The generators' 1x1 - 8x8 levels (STCGAN/networks.py:104-128: conv / convT -> BatchNorm2d -> LeakyReLU
- * or ReLU) run as a split-K GEMM whose reduction kernel also takes the exact batch statistics, finalizes
- * them (mean / rstd / scale / shift and the running-statistics update, as stc_bn_finalize) and applies
- * BN + activation -- a block owns whole channels, so nothing crosses blocks.  Replaces stc_conv_fwd_ex +
- * stc_bn_finalize + stc_bn_apply (three launches after the GEMM -> one).  y receives the raw conv output
- * (the BN backward's input); a1 = act(BN(y), slope1) and, with a2.p != NULL, a2 = act(BN(y), slope2) over
- * a1's H x W extent (the decoder crops an odd level).  stc_conv_fwd_bn_act_ok: 1 when the shape's plan
- * splits K and has <= 2048 GEMM rows (else use the separate calls).                                  */
-typedef struct {
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  int64_t* num_batches_tracked;
-  float momentum, eps;
-  float* mean;
-  float* rstd;
-  float* scale;
-  float* shift;
-  stc_view a1;
-  float slope1;
-  stc_view a2;
-  float slope2;
-} stc_bn_act;
-int stc_conv_fwd_bn_act_ok(int dtype, int kind, int B, stc_view x, int Cin, int Cout, stc_view y);
-int stc_conv_fwd_bn_act(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
-                        stc_view y, const float* bias, const stc_bn_act* a, void* workspace,
-                        int64_t workspace_bytes, void* stream);
-
-/* ---- BatchNorm finalize fused into the producing conv (no finalize launch on the chain) ----------
- * Replaces, per BatchNorm2d of STCGAN/networks.py:107,109,170,179 (train mode), the pair
- * stc_conv_fwd_ex + stc_bn_finalize (forward) and the dbeta/dgamma reduction of stc_bn_bwd_apply
- * (backward).  On the bf16 LDS-DMA path the conv's last-arriving blocks (or those of its split-K
- * reduction) merge the chunk partials in a fixed order (two levels: chunk groups, then groups) and
- * write the results; other paths run the separate kernels with the same semantics.
- *   stc_conv_fwd_bnfin: conv + statistics + mean/rstd/scale/shift + running-statistics update
- *                       (stc_bn_finalize's outputs), stats_part as for stc_conv_fwd_ex.
- *   stc_conv_bwd_bnfin: stc_conv_bwd_bn + dbeta = sum dn, dgamma = sum dn*xhat into fin->dbeta/dgamma;
- *                       then call stc_bn_bwd_apply with part2 = NULL and nchunks = 0 (it reads the
- *                       finished dgamma/dbeta).
- * counters: uint32 [stc_bn_fin_counters()], zeroed once by the caller; every call leaves them zero,
- * so calls that share a counter buffer must be ordered on one stream.  scratch: float [64*C*4].   */
-typedef struct {
-  void* counters;
-  float* scratch;
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  int64_t* num_batches_tracked;
-  float momentum, eps;
-  float* mean;
-  float* rstd;
-  float* scale;
-  float* shift;
-  float* dgamma;
-  float* dbeta;
-} stc_bn_fin;
-int stc_bn_fin_counters(void);
-int stc_conv_fwd_bnfin(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
-                       stc_view y, const float* bias, float* stats_part, int stats_chunks, const stc_bn_fin* fin,
-                       const int32_t* force_plan, void* workspace, int64_t workspace_bytes, void* stream);
-int stc_conv_bwd_bnfin(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout, stc_view out,
-                       const stc_bnb_fuse* bnb, float* part2, int nchunks, const stc_bn_fin* fin,
-                       void* workspace, int64_t workspace_bytes, void* stream);
-
 /* ---- weight gradient ---------------------------------------------------------
  * dW[r][ci][kh][kw] = sum_{b,oy,ox} D[b,oy,ox,r] * G[b, oy*s+kh-1, ox*s+kw-1, ci]
  *   Conv2d s2/s1 : D = dy (grid = output), G = x (input), s = stride

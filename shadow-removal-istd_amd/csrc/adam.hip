@@ -281,22 +281,11 @@ __global__ __launch_bounds__(256) void grad_acc_kernel(GradAccArgs a) {
   }
 }
 
-// Variant of the update launches: STC_ADAM_VARIANT = adam_pack_kernel's V bits (read per call so an A/B can
-// switch it in one process).  Default 10: streaming p / m / v stores and streaming loads -- nothing re-reads
-// them this step -- take the generators' update 961 -> 730 us and the train step -0.2 ms (interleaved pairs);
-// streaming the packed operands is slower (the next forward reads them from the memory-side cache), the XCD
-// grouping gains nothing (profiles/r03/diag/adam_variants.log).  Every variant is bit-identical.
-typedef void (*AdamPackFn)(const long long*, int, float, float, float, float, float, const float*);
-static AdamPackFn adam_pack_fn() {
-  const char* e = getenv("STC_ADAM_VARIANT");
-  const int v = e ? atoi(e) : 10;
-  switch (v & 15) {
-#define STC_AV(k) case k: return adam_pack_kernel<k>;
-    STC_AV(0) STC_AV(1) STC_AV(2) STC_AV(3) STC_AV(6) STC_AV(14)
-#undef STC_AV
-    default: return adam_pack_kernel<10>;
-  }
-}
+// The update launch: adam_pack_kernel<10> -- streaming p / m / v stores and streaming loads (nothing re-reads
+// them this step) took the generators' update 961 -> 730 us and the train step -0.2 ms (interleaved pairs);
+// streaming the packed operands was slower (the next forward reads them from the memory-side cache) and the
+// XCD grouping gained nothing (profiles/r03/diag/adam_variants.log: the other V bits, all bit-identical).
+static inline auto adam_pack_fn() { return adam_pack_kernel<10>; }
 
 }  // namespace stc
 

@@ -10,7 +10,6 @@
 // input (n = x*scale + shift), reduced to sum(dn), sum(dn*xhat), then applied.
 // All reductions are fixed-order => bitwise reproducible.
 #include "common.hpp"
-#include "bnfin.hpp"
 
 namespace stc {
 
@@ -881,10 +880,7 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
               "stc_bn_bwd_apply: bad C=%d / views", C);
   hipStream_t st = (hipStream_t)stream;
   GradIn gi = mkgrad(g1, slope1, g2, slope2);
-  if (mean && part2 == nullptr && nchunks == 0) {
-    // dgamma / dbeta already final (stc_conv_bwd_bnfin)
-    STC_REQUIRE(dgamma && dbeta && gamma && rstd && scale && shift, "stc_bn_bwd_apply: missing BN tensors");
-  } else if (mean) {
+  if (mean) {
     STC_REQUIRE(part2 && dgamma && dbeta && gamma && rstd && scale && shift, "stc_bn_bwd_apply: missing BN tensors");
     if (nchunks <= 256)
       hipLaunchKernelGGL(bn_bwd_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part2, nchunks, C, dgamma, dbeta);
@@ -906,20 +902,3 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
   STC_CHECK_LAUNCH();
   return 0;
 }
-
-namespace stc {
-// The finalize of stc_conv_fwd_bnfin / stc_conv_bwd_bnfin as its own launch (paths whose producer has no
-// in-kernel finalize): the same merges as stc_bn_finalize / stc_bn_bwd_apply's reduction.
-int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st) {
-  if (!sums)
-    return stc_bn_finalize(part, nchunks, C, f.gamma, f.beta, f.rmean, f.rvar, (int64_t*)f.nbt, f.momentum, f.eps,
-                           f.mean_o, f.rstd_o, f.scale, f.shift, st);
-  STC_REQUIRE(f.dgamma && f.dbeta, "bn finalize: dgamma/dbeta required");
-  if (nchunks <= 256)
-    hipLaunchKernelGGL(bn_bwd_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nchunks, C, f.dgamma, f.dbeta);
-  else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, nchunks, C, f.dgamma, f.dbeta);
-  STC_CHECK_LAUNCH();
-  return 0;
-}
-}  // namespace stc

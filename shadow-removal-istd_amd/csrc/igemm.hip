@@ -20,7 +20,6 @@
 // Register-staged double buffer: the global loads of K-step s+1 are in flight
 // while step s runs on MFMA; one barrier per step.
 #include "common.hpp"
-#include "bnfin.hpp"
 
 namespace stc {
 
@@ -673,17 +672,9 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
 int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
-                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr,
-                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f,
-                  const struct BnAct* bna = nullptr);
+                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr,
+                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f);
 bool bf16_conv_act_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y1, const stc_view* y2);
-bool bf16_conv_bnact_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y);
-bool halo8_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y1, const stc_view* y2);
-int halo8_conv_act(int B, const stc_view& x, const void* w_packed, const stc_view& y1, const stc_view* y2, int act_n,
-                   float s1, float s2, const float* bias, hipStream_t st);
-int bf16_conv_fwd_bnact(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
-                        const float* bias, const stc_bn_act& a, void* ws, int64_t ws_bytes, hipStream_t st);
-int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st);
 bool bf16_narrow_eligible(int kind, int Cin, int Cout);
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout);
 int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
@@ -897,58 +888,6 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
                            bnb->g_other, bnb->slope_other, part2, need, stream);
 }
 
-// ---- BatchNorm finalize fused into the producer (bnfin.hpp)
-static BnFin mkfin(const stc_bn_fin& f) {
-  BnFin r{};
-  r.counters = (unsigned*)f.counters; r.scratch = f.scratch;
-  r.gamma = f.gamma; r.beta = f.beta; r.rmean = f.running_mean; r.rvar = f.running_var;
-  r.nbt = (long long*)f.num_batches_tracked; r.momentum = f.momentum; r.eps = f.eps;
-  r.mean_o = f.mean; r.rstd_o = f.rstd; r.scale = f.scale; r.shift = f.shift;
-  r.dgamma = f.dgamma; r.dbeta = f.dbeta;
-  return r;
-}
-
-extern "C" int stc_bn_fin_counters(void) { return BNFIN_L1 + BNFIN_L2; }
-
-extern "C" int stc_conv_fwd_bnfin(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
-                                  stc_view y, const float* bias, float* stats_part, int stats_chunks,
-                                  const stc_bn_fin* fin, const int32_t* force_plan, void* workspace,
-                                  int64_t workspace_bytes, void* stream) {
-  STC_REQUIRE(kind >= 0 && kind <= 3, "stc_conv_fwd_bnfin: bad kind %d", kind);
-  STC_REQUIRE(fin && fin->counters && fin->scratch && fin->scale && fin->shift && stats_part,
-              "stc_conv_fwd_bnfin: counters, scratch, scale/shift and stats_part required");
-  hipStream_t st = (hipStream_t)stream;
-  const BnFin f = mkfin(*fin);
-  if (bf16_path(dtype, kind, Cin, Cout) && bf16_conv_eligible(kind, B, x, Cin, Cout))
-    return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, 0, 0, stats_part, stats_chunks, force_plan, workspace,
-                         workspace_bytes, st, nullptr, nullptr, &f);
-  const int rc = stc_conv_fwd_ex(dtype, kind, B, x, Cin, w_packed, Cout, y, bias, 0, 0, stats_part, stats_chunks,
-                                 force_plan, workspace, workspace_bytes, stream);
-  if (rc) return rc;
-  return bnfin_fallback(f, stats_part, stats_chunks, Cout, false, st);
-}
-
-extern "C" int stc_conv_bwd_bnfin(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout,
-                                  stc_view out, const stc_bnb_fuse* bnb, float* part2, int nchunks,
-                                  const stc_bn_fin* fin, void* workspace, int64_t workspace_bytes, void* stream) {
-  STC_REQUIRE(bnb && part2 && fin && fin->counters && fin->scratch && fin->dgamma && fin->dbeta,
-              "stc_conv_bwd_bnfin: bnb, part2, counters, scratch and dgamma/dbeta required");
-  hipStream_t st = (hipStream_t)stream;
-  const BnFin f = mkfin(*fin);
-  if (bnb_fused_path(dtype, kind, B, dy, Cin, Cout, out)) {
-    const int Hg = kind == STC_CONVT_S2 ? dy.H : out.H, Wg = kind == STC_CONVT_S2 ? dy.W : out.W;
-    int32_t need = 0;
-    bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &need, nullptr);
-    STC_REQUIRE(nchunks == need, "stc_conv_bwd_bnfin: %d chunks != %d (use stc_conv_bwd_bn_chunks)", nchunks, need);
-    return bf16_conv_fwd(kind, B, dy, Cin, w_packed, Cout, out, nullptr, 0, 0, nullptr, need, nullptr, workspace,
-                         workspace_bytes, st, bnb, part2, &f);
-  }
-  const int rc = stc_conv_bwd_bn(dtype, kind, B, dy, Cin, w_packed, Cout, out, bnb, part2, nchunks, workspace,
-                                 workspace_bytes, stream);
-  if (rc) return rc;
-  return bnfin_fallback(f, part2, nchunks, bnb->C, true, st);
-}
-
 // ---- conv + activation epilogue (layers without BatchNorm)
 extern "C" int stc_conv_fwd_act_ok(int dtype, int kind, int B, stc_view x, int Cin, int Cout, stc_view y1, stc_view y2) {
   if (kind < 0 || kind > 3 || !bf16_path(dtype, kind, Cin, Cout)) return 0;
@@ -960,23 +899,6 @@ extern "C" int stc_conv_fwd_act(int dtype, int kind, int B, stc_view x, int Cin,
                                 void* workspace, int64_t workspace_bytes, void* stream) {
   STC_REQUIRE(stc_conv_fwd_act_ok(dtype, kind, B, x, Cin, Cout, y1, y2),
               "stc_conv_fwd_act: no activation epilogue for this shape (check stc_conv_fwd_act_ok)");
-  if (halo8_ok(kind, B, x, Cin, Cout, y1, &y2))  // the first layers (Cin = 8): input rows staged in LDS
-    return halo8_conv_act(B, x, w_packed, y1, &y2, y2.p ? 2 : 1, slope1, slope2, bias, (hipStream_t)stream);
   return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y1, bias, 0, 0, nullptr, 0, nullptr, workspace, workspace_bytes,
-                       (hipStream_t)stream, nullptr, nullptr, nullptr, &y2, y2.p ? 2 : 1, slope1, slope2);
-}
-
-// ---- deep split-K layers: conv + BatchNorm (train) + activation in two launches
-extern "C" int stc_conv_fwd_bn_act_ok(int dtype, int kind, int B, stc_view x, int Cin, int Cout, stc_view y) {
-  if (kind < 0 || kind > 3 || !bf16_path(dtype, kind, Cin, Cout)) return 0;
-  return bf16_conv_bnact_ok(kind, B, x, Cin, Cout, y) ? 1 : 0;
-}
-
-extern "C" int stc_conv_fwd_bn_act(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
-                                   stc_view y, const float* bias, const stc_bn_act* a, void* workspace,
-                                   int64_t workspace_bytes, void* stream) {
-  STC_REQUIRE(a && stc_conv_fwd_bn_act_ok(dtype, kind, B, x, Cin, Cout, y),
-              "stc_conv_fwd_bn_act: no fused form for this shape (check stc_conv_fwd_bn_act_ok)");
-  return bf16_conv_fwd_bnact(kind, B, x, Cin, w_packed, Cout, y, bias, *a, workspace, workspace_bytes,
-                             (hipStream_t)stream);
+                       (hipStream_t)stream, nullptr, nullptr, &y2, y2.p ? 2 : 1, slope1, slope2);
 }

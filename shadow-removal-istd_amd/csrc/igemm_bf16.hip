@@ -16,10 +16,8 @@
 //     statistics of the tile fused in (two-pass: tile mean, then centred sum of
 //     squares, in fp32 from the accumulators) -> part[tile][n] = {count, 0, M2, mean},
 //     the format stc_bn_finalize merges (Chan's parallel variance).
-#include <cstdlib>
 
 #include "common.hpp"
-#include "bnfin.hpp"
 
 namespace stc {
 
@@ -61,11 +59,7 @@ struct GParams {
   const float *bsc, *bsh, *bmu, *brs;
   float bs_self, bs_other;
   int bC, bch_off;
-  // BatchNorm finalize in this launch (bnfin.hpp): statistics -> tables (stats) or the backward sums
-  // (part2) -> dbeta/dgamma, by the last-arriving blocks; stat_chunks = the chunk count of stats/part2
-  int fin_on, stat_chunks;
   int phase_major;  // grid linear over (tile, phase), phase fastest (set by the launcher)
-  BnFin fin;
   // Activation epilogue (layers with no BatchNorm: the first conv of G / D, STCGAN/networks.py:99,165-166):
   // act_n = 1 or 2 activated copies of the bf16-rounded output, out1 = act(v, act_s1) into c (instead of the
   // raw value), out2 = act(v, act_s2) into the c2 view -- what conv + stc_bn_apply(table = NULL) write, bit
@@ -541,7 +535,7 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
         m2 += m2w + dl * dl * (cnt * nw / nt);
         cnt = nt;
       }
-      wt_store4(p.stats + (tile * p.N + n) * 4, make_float4(cnt, 0.f, m2, mean));  // (read in-launch: bnfin.hpp)
+      *reinterpret_cast<float4*>(p.stats + (tile * p.N + n) * 4) = make_float4(cnt, 0.f, m2, mean);
     }
     __syncthreads();
   }
@@ -640,9 +634,6 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
           if (++y == p.GH) { y = 0; ++b; }
         }
       }
-      if (p.fin_on && p.stats)
-        bnfin_arrive_stats(p.fin, p.stats, p.stat_chunks, p.N, ph * p.mtiles + mt, n0, min(n0 + BN, p.N), nt, p.ntiles,
-                           smem);
       return;
     }
     // fused BatchNorm-backward reduction: {sum dn, sum dn*xhat} of this thread's 8-channel chunk
@@ -710,14 +701,8 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
         const long long tile = (long long)ph * p.mtiles + mt;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          wt_store2(p.part2 + (tile * p.bC + ch0 + e) * 2, ta[e], tb[e]);
+          *reinterpret_cast<float2*>(p.part2 + (tile * p.bC + ch0 + e) * 2) = make_float2(ta[e], tb[e]);
       }
-    }
-    if (p.fin_on) {
-      // this block's BN channels: [n0, n0 + BN) - bch_off, clipped to [0, bC) (uniform over the blocks of nt)
-      const int lo = max(n0 - p.bch_off, 0), hi = min(min(n0 + BN, p.N) - p.bch_off, p.bC);
-      if (lo < hi)
-        bnfin_arrive_sums(p.fin, p.part2, p.stat_chunks, p.bC, ph * p.mtiles + mt, lo, hi, nt, p.ntiles, smem);
     }
     return;
   }
@@ -863,11 +848,9 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        wt_store2(p.part2 + ((long long)blockIdx.x * p.bC + bnch + e) * 2, ta[e], tb[e]);
+        *reinterpret_cast<float2*>(p.part2 + ((long long)blockIdx.x * p.bC + bnch + e) * 2) = make_float2(ta[e], tb[e]);
     }
   }
-  __shared__ double fin_red[2 * 256 + 1];  // (bnfin.hpp LDS: 2 doubles per thread + the ticket flag)
-  if (p.part2 && p.fin_on) bnfin_arrive_sums(p.fin, p.part2, p.stat_chunks, p.bC, blockIdx.x, 0, p.bC, 0, 1, fin_red);
   if (!p.stats) return;
   __shared__ float red[2][256][8];
   __shared__ float rcnt[256];
@@ -887,215 +870,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_stats_kernel(const GParams 
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      wt_store4(p.stats + ((long long)blockIdx.x * p.N + n + e) * 4, make_float4(nn, a1[e], a2[e], sh[e]));
-  }
-  if (p.fin_on) bnfin_arrive_stats(p.fin, p.stats, p.stat_chunks, p.N, blockIdx.x, 0, p.N, 0, 1, fin_red);
-}
-
-// Deep split-K layers (<= 2048 GEMM rows: the 1x1 - 8x8 levels of the generators, STCGAN/networks.py:104-128):
-// the split-K reduction, the BatchNorm batch statistics, their finalize and the BN + activation apply as ONE
-// launch, where it was three (splitk_reduce_stats, bn_finalize, bn_apply).  A block owns 8 whole channels --
-// every row of them -- so no other block's data is needed: it sums the slabs (fixed order), writes the raw
-// bf16 output (the BN backward's input), takes the exact two-pass mean / centred sum of squares of the fp32
-// results (fixed-order block reduction in fp64), writes mean / rstd / scale / shift / running statistics,
-// then applies BN + activation to the bf16-rounded values (as stc_bn_apply does) into one or two views.
-struct BnAct {
-  const float *gamma, *beta;
-  float *rmean, *rvar;
-  long long* nbt;
-  float momentum, eps;
-  float *mean_o, *rstd_o, *scale, *shift;
-  char* a1;
-  long long a1_bs, a1_rs;
-  int a1_ps, a1_co;
-  float s1;
-  char* a2;  // optional second activation (null: none)
-  long long a2_bs, a2_rs;
-  int a2_ps, a2_co;
-  float s2;
-  int aH, aW;  // extent the activations cover (the decoder crops an odd level)
-};
-constexpr int BNA_T = 1024;     // threads per block (16 waves)
-constexpr int BNA_ITEMS = 2048;  // (slab group, row) items per launch: <= 2048 GEMM rows, 2 per thread
-
-// Slabs [s0, s1) of one GEMM row's 8 channels summed in order onto acc (groups of 4 slabs: 8 loads in flight).
-__device__ __forceinline__ void bna_slab_sum(const GParams& p, int row, int n, int s0, int s1, float* acc) {
-  const int ph = row / p.M, m = row - ph * p.M;
-  const long long MN = (long long)p.M * p.N;
-  const float* src = p.ws + ((long long)ph * p.ksplit * p.M + m) * p.N + n;
-  int s = s0;
-  for (; s + 4 <= s1; s += 4) {
-    float4 x0[4], x1[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      x0[u] = *reinterpret_cast<const float4*>(src + (s + u) * MN);
-      x1[u] = *reinterpret_cast<const float4*>(src + (s + u) * MN + 4);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      acc[0] += x0[u].x; acc[1] += x0[u].y; acc[2] += x0[u].z; acc[3] += x0[u].w;
-      acc[4] += x1[u].x; acc[5] += x1[u].y; acc[6] += x1[u].z; acc[7] += x1[u].w;
-    }
-  }
-  for (; s < s1; ++s) {
-    const float4 x0 = *reinterpret_cast<const float4*>(src + s * MN);
-    const float4 x1 = *reinterpret_cast<const float4*>(src + s * MN + 4);
-    acc[0] += x0.x; acc[1] += x0.y; acc[2] += x0.z; acc[3] += x0.w;
-    acc[4] += x1.x; acc[5] += x1.y; acc[6] += x1.z; acc[7] += x1.w;
-  }
-}
-
-// Grid: one block per 8 channels.  The slabs of a row are split into G contiguous groups (G = 1: the
-// separate reduce's exact order, bias first; G > 1: each group summed in order from 0, the groups added onto
-// the bias in group order through LDS) so that R * G items keep all 1024 threads loading: the deep levels
-// have few rows and many splits, and one thread walking every slab of a row was latency-bound.
-__global__ void __launch_bounds__(BNA_T) splitk_bn_act_kernel(const GParams p, const BnAct a, const int G) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* part = reinterpret_cast<float*>(smem);  // [G * R][8] group partials (G > 1)
-  __shared__ double red[BNA_T / 64][8];
-  __shared__ float tab[16];
-  const int n = blockIdx.x * 8;  // this block's 8 channels
-  const int R = p.nphase * p.M;
-  const int GHW = p.GH * p.GW;
-  const int t = threadIdx.x;
-  float bz[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bz[e] = p.bias ? p.bias[n + e] : 0.f;
-  float v[2][8];  // rows t and t + 1024 (fp32 results; rows past R hold 0)
-  // 1. slab sums
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int it = t + BNA_T * i;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
-    if (it >= R * G) continue;
-    if (G == 1) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[i][e] = bz[e];
-      bna_slab_sum(p, it, n, 0, p.ksplit, v[i]);
-    } else {
-      const int g = it / R, row = it - g * R;
-      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      bna_slab_sum(p, row, n, g * p.ksplit / G, (g + 1) * p.ksplit / G, acc);
-      float4* d = reinterpret_cast<float4*>(part + (long long)it * 8);
-      d[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      d[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    }
-  }
-  if (G > 1) {  // R * G <= 2048 with G >= 2: every row is t < 1024
-    __syncthreads();
-    if (t < R) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[0][e] = bz[e];
-      for (int g = 0; g < G; ++g) {
-        const float4* q = reinterpret_cast<const float4*>(part + ((long long)g * R + t) * 8);
-        const float4 x0 = q[0], x1 = q[1];
-        v[0][0] += x0.x; v[0][1] += x0.y; v[0][2] += x0.z; v[0][3] += x0.w;
-        v[0][4] += x1.x; v[0][5] += x1.y; v[0][6] += x1.z; v[0][7] += x1.w;
-      }
-    }
-  }
-  // raw bf16 output (the BatchNorm backward's input)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = t + BNA_T * i;
-    if (row >= R) continue;
-    const int ph = row / p.M, m = row - ph * p.M;
-    const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
-    const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
-    const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
-    uint4 o;
-    o.x = pack_bf16x2(v[i][0], v[i][1]); o.y = pack_bf16x2(v[i][2], v[i][3]);
-    o.z = pack_bf16x2(v[i][4], v[i][5]); o.w = pack_bf16x2(v[i][6], v[i][7]);
-    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + (long long)b * p.c_bs + (long long)oy * p.c_rs +
-                              (long long)ox * p.c_ps + p.c_co + n) = o;
-  }
-  // 2. exact two-pass statistics of the fp32 results: wave butterflies, then the 16 waves in a fixed tree (fp64)
-  const int lane = t & 63, wv = t >> 6;
-  __shared__ double res[2][8];
-  auto block_sum8 = [&](const double* loc, double* out) {  // out: LDS, every thread reads it after the call
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      double d = loc[e];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-      if (lane == 0) red[wv][e] = d;
-    }
-    __syncthreads();
-    if (t < 8) {
-      double w[BNA_T / 64];
-#pragma unroll
-      for (int k = 0; k < BNA_T / 64; ++k) w[k] = red[k][t];
-#pragma unroll
-      for (int h = BNA_T / 128; h > 0; h >>= 1)
-#pragma unroll
-        for (int k = 0; k < h; ++k) w[k] += w[k + h];
-      out[t] = w[0];
-    }
-    __syncthreads();
-  };
-  double loc[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) loc[e] = (double)v[0][e] + (double)v[1][e];
-  block_sum8(loc, res[0]);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const double mu = res[0][e] / (double)R;
-    double q = 0;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (t + BNA_T * i >= R) continue;
-      const double d = (double)v[i][e] - mu;
-      q += d * d;
-    }
-    loc[e] = q;
-  }
-  block_sum8(loc, res[1]);
-  // 3. finalize: tables + running statistics of the block's channels
-  if (t < 8) {
-    const int e = t;
-    const double mu = res[0][e] / (double)R, m2 = res[1][e];
-    bn_finalize_store(n + e, (double)R, mu, m2, a.gamma, a.beta, a.rmean, a.rvar, a.nbt, a.momentum, a.eps,
-                      a.mean_o, a.rstd_o, a.scale, a.shift);
-    const double var = m2 / (double)R;
-    const float rs = (float)(1.0 / sqrt(var + (double)a.eps));
-    const float sc = (a.gamma ? a.gamma[n + e] : 1.f) * rs;
-    tab[e] = sc;
-    tab[8 + e] = (a.beta ? a.beta[n + e] : 0.f) - (float)mu * sc;
-  }
-  __syncthreads();
-  float sc[8], sf[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { sc[e] = tab[e]; sf[e] = tab[8 + e]; }
-  // 4. BN + activation of the bf16-rounded values (stc_bn_apply's arithmetic)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = t + BNA_T * i;
-    if (row >= R) continue;
-    const int ph = row / p.M, m = row - ph * p.M;
-    const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
-    const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
-    const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
-    if (oy >= a.aH || ox >= a.aW) continue;
-    float xn[8];
-#pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-      const unsigned w = pack_bf16x2(v[i][e], v[i][e + 1]);
-      xn[e] = fmaf(__uint_as_float(w << 16), sc[e], sf[e]);
-      xn[e + 1] = fmaf(__uint_as_float(w & 0xffff0000u), sc[e + 1], sf[e + 1]);
-    }
-    uint4 o1;
-    o1.x = pack_bf16x2(act(xn[0], a.s1), act(xn[1], a.s1)); o1.y = pack_bf16x2(act(xn[2], a.s1), act(xn[3], a.s1));
-    o1.z = pack_bf16x2(act(xn[4], a.s1), act(xn[5], a.s1)); o1.w = pack_bf16x2(act(xn[6], a.s1), act(xn[7], a.s1));
-    *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.a1) + (long long)b * a.a1_bs + (long long)oy * a.a1_rs +
-                              (long long)ox * a.a1_ps + a.a1_co + n) = o1;
-    if (a.a2) {
-      uint4 o2;
-      o2.x = pack_bf16x2(act(xn[0], a.s2), act(xn[1], a.s2)); o2.y = pack_bf16x2(act(xn[2], a.s2), act(xn[3], a.s2));
-      o2.z = pack_bf16x2(act(xn[4], a.s2), act(xn[5], a.s2)); o2.w = pack_bf16x2(act(xn[6], a.s2), act(xn[7], a.s2));
-      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(a.a2) + (long long)b * a.a2_bs + (long long)oy * a.a2_rs +
-                                (long long)ox * a.a2_ps + a.a2_co + n) = o2;
-    }
+      *reinterpret_cast<float4*>(p.stats + ((long long)blockIdx.x * p.N + n + e) * 4) = make_float4(nn, a1[e], a2[e], sh[e]);
   }
 }
 
@@ -1236,29 +1011,16 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
     ks = force_ks > 0 ? force_ks : 1;
   } else {
     int order[5], no = 0;
-    // The loader-wave tiles 29 / 31 win these layers in isolation (profiles/r03/diag/loader_tiles_conv.log,
-    // up to 20 %) but lose 0.36 ms per train step in situ: one of their blocks fills a CU's LDS, so the
-    // side streams' kernels cannot share it.  STC_PLAN_R3=1 selects them (A/B).
-    static const bool r3 = getenv("STC_PLAN_R3") != nullptr;
-    if (!r3 && N >= 256) {
+    // (the loader-wave tiles 29 / 31 win these layers in isolation, profiles/r03/diag/loader_tiles_conv.log, but
+    // lose 0.36 ms per train step in situ: one of their blocks fills a CU's LDS, so the side streams' kernels
+    // cannot share it; they stay reachable through force_plan only)
+    if (N >= 256) {
       if ((long long)M * nphase >= 8192 && K >= 8192) {
         order[0] = 6; order[1] = 7; order[2] = 0; order[3] = 4; order[4] = 5; no = 5;
-      } else if ((long long)M * nphase >= 8192) { order[0] = 6; order[1] = 0; order[2] = 4; order[3] = 5; }
-      else { order[0] = 0; order[1] = 4; order[2] = 12; order[3] = 5; }
-      if (no == 0) no = 4;
-    } else if (!r3 && N >= 128) {
-      order[0] = 0; order[1] = 4; order[2] = 5; no = 3;
-    } else if (N >= 256) {
-      if ((long long)M * nphase >= 8192 && K >= 8192) {  // long reductions: 8-wave 128x256 (s1 dgrad)
-        order[0] = 6; order[1] = 7; order[2] = 0; order[3] = 4; order[4] = 5; no = 5;
-      } else if ((long long)M * nphase >= 16384) { order[0] = 31; order[1] = 6; order[2] = 0; order[3] = 4; order[4] = 5; no = 5; }
-      else if (nphase == 1 && M >= 2048 && M < 8192 && K >= 4096) {  // e5: 128x128 + loaders, 4-way split-K
-        order[0] = 29; no = 1;
-      } else { order[0] = 29; order[1] = 0; order[2] = 4; order[3] = 12; order[4] = 5; no = 5; }
-      if (no == 0) no = 4;
+      } else if ((long long)M * nphase >= 8192) { order[0] = 6; order[1] = 0; order[2] = 4; order[3] = 5; no = 4; }
+      else { order[0] = 0; order[1] = 4; order[2] = 12; order[3] = 5; no = 4; }
     } else if (N >= 128) {
-      if (K >= 2048 && (long long)M * nphase >= 65536) { order[0] = 31; order[1] = 0; order[2] = 4; order[3] = 5; no = 4; }
-      else { order[0] = 0; order[1] = 4; order[2] = 5; no = 3; }
+      order[0] = 0; order[1] = 4; order[2] = 5; no = 3;
     } else if (K <= 128) {  // first layers (Cin = 8): 3-stage BK = 32, 3-4 blocks per CU
       order[0] = 23; order[1] = 2; order[2] = 5; no = 3;
     } else if (K <= 512) {  // (Cin = 128 ConvT-geometry dgrads: the 3-stage BK = 32 128x64 tile, -9 %)
@@ -1285,9 +1047,6 @@ static BPlan bf16_plan(int M, int N, int K, int nphase, int force_cfg, int force
     }
   }
   if (!allow_split) ks = 1;
-  // A/B hook: the same tiles with 2 loader waves (bit-identical; STC_PLAN_LD2=1)
-  static const bool ld2 = getenv("STC_PLAN_LD2") != nullptr;
-  if (ld2 && force_cfg < 0) cfg = cfg == 0 ? 33 : cfg == 7 ? 35 : (cfg == 2 || cfg == 11) ? 34 : cfg;
   const TileCfg& t = kTiles[cfg];
   pl.cfg = cfg;
   pl.BM = t.BM;
@@ -1355,33 +1114,11 @@ int bf16_igemm_query(int M, int N, int K, int nphase, const int32_t* force, int6
 }
 
 // p: filled by the caller (geometry, operands, output); returns 0 or error.
-int bnfin_fallback(const BnFin& f, const float* part, int nchunks, int C, bool sums, hipStream_t st);
 
 int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_bytes, float* stats, int stats_chunks,
-                      hipStream_t st, const BnFin* fin, const BnAct* bna = nullptr) {
+                      hipStream_t st) {
   Bf16Problem pr = bf16_problem(p.M, p.N, p.K, p.nphase, force, p.vec_out != 0);
   const BPlan& pl = pr.pl;
-  if (bna)
-    STC_REQUIRE(pl.ksplit > 1 && (long long)p.nphase * p.M <= BNA_ITEMS && p.N % 8 == 0 && p.vec_out && !stats &&
-                    !p.part2 && !fin,
-                "bf16 igemm: the fused split-K BatchNorm needs split K, <= %d rows and no other statistics",
-                BNA_ITEMS);
-  p.fin_on = 0;
-  p.stat_chunks = pr.stats_chunks;
-  bool fin_after = false;  // the wide split-K reduction has no in-kernel finalize: a separate launch
-  if (fin) {
-    STC_REQUIRE(stats || p.part2, "bf16 igemm: finalize without statistics");
-    p.fin = *fin;
-    bnfin_groups(pr.stats_chunks, &p.fin.gs, &p.fin.ngroups);
-    const int nct = pl.ksplit > 1 ? 1 : pl.ntiles;
-    STC_REQUIRE(p.fin.ngroups <= BNFIN_MAXG && p.fin.ngroups * nct <= BNFIN_L1 && nct <= BNFIN_L2,
-                "bf16 igemm: finalize grouping %d x %d out of range", p.fin.ngroups, nct);
-    // In-launch only behind the split-K reduction (a short grid): in the main GEMM every block would have to
-    // drain its output stores before its ticket, holding its CU slot one store latency longer per round of
-    // blocks -- measured +1 ms per train step against the separate finalize launch.
-    fin_after = !(pl.ksplit > 1 && !pr.wide);
-    p.fin_on = fin_after ? 0 : 1;
-  }
   p.ksplit = pl.ksplit; p.kchunk = pl.kchunk; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles;
   p.stats = nullptr;
   p.ws = nullptr;
@@ -1396,8 +1133,7 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
   }
   if (stats || part2)
     STC_REQUIRE(stats_chunks >= pr.stats_chunks, "bf16 igemm: stats chunks %d < %d", stats_chunks, pr.stats_chunks);
-  static const bool pm_on = getenv("STC_PHASE_MAJOR") == nullptr || atoi(getenv("STC_PHASE_MAJOR")) != 0;
-  p.phase_major = (pm_on && p.nphase > 1 && pl.ksplit == 1) ? 1 : 0;
+  p.phase_major = (p.nphase > 1 && pl.ksplit == 1) ? 1 : 0;
   dim3 grid = p.phase_major ? dim3(pl.mtiles * pl.ntiles * p.nphase, 1, 1)
                             : dim3(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
   const size_t lds = bf16_lds_bytes(pl.cfg);
@@ -1465,13 +1201,7 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     p.stats = stats;
     p.part2 = part2;
     const long long rows = (long long)p.nphase * p.M;
-    if (bna) {
-      STC_REQUIRE(rows <= BNA_ITEMS, "bf16 conv: fused split-K BatchNorm over %lld rows", rows);
-      int G = 1;
-      while (G * 2 <= p.ksplit && rows * G * 2 <= BNA_ITEMS) G *= 2;
-      const size_t lds = G > 1 ? (size_t)rows * G * 8 * sizeof(float) : 0;
-      hipLaunchKernelGGL(splitk_bn_act_kernel, dim3((unsigned)(p.N / 8)), dim3(BNA_T), lds, st, p, *bna, G);
-    } else if (pr.wide) {
+    if (pr.wide) {
       const long long units = rows * (p.N / 8);
       hipLaunchKernelGGL(splitk_reduce_wide_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, st, p);
     } else {
@@ -1479,11 +1209,6 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
       hipLaunchKernelGGL(splitk_reduce_stats_kernel, dim3(blocks), dim3(256), 0, st, p, pr.reduce_rows);
     }
     STC_CHECK_LAUNCH();
-  }
-  if (fin_after) {
-    const bool sums = p.part2 != nullptr;
-    const int rc = bnfin_fallback(p.fin, sums ? p.part2 : stats, pr.stats_chunks, sums ? p.bC : p.N, sums, st);
-    if (rc) return rc;
   }
   return 0;
 }
@@ -1521,9 +1246,8 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
 int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
-                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr, const BnFin* fin = nullptr,
-                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f,
-                  const BnAct* bna = nullptr) {
+                  const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr,
+                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f) {
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   GParams p{};
@@ -1568,40 +1292,14 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
     p.bC = bnb->C; p.bch_off = bnb->ch_off;
   }
   if (act_n) {
-    STC_REQUIRE(p.vec_out && !bnb && !stats && !fin && (act_n == 1 || (act2 && act2->p)),
+    STC_REQUIRE(p.vec_out && !bnb && !stats && (act_n == 1 || (act2 && act2->p)),
                 "bf16 conv: activation epilogue needs a 16-byte NHWC bf16 output and no statistics");
     p.act_n = act_n; p.act_s1 = act_s1; p.act_s2 = act_s2;
     if (act_n == 2) {
       p.c2 = (char*)act2->p; p.c2_bs = act2->bs; p.c2_rs = act2->rs; p.c2_ps = act2->ps; p.c2_co = act2->co;
     }
   }
-  return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st, fin, bna);
-}
-
-// The fused split-K BatchNorm applies when the layer's plan splits K and has <= 2048 GEMM rows.
-bool bf16_conv_bnact_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y) {
-  if (!bf16_conv_eligible(kind, B, x, Cin, Cout) || !vec_out_ok(B, y, Cout, 0) || Cout % 8 != 0) return false;
-  const Geometry g = geometry(kind);
-  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
-  const int Hg = kind == STC_CONVT_S2 ? x.H : y.H, Wg = kind == STC_CONVT_S2 ? x.W : y.W;
-  const Bf16Problem pr = bf16_problem(B * Hg * Wg, Cout, taps * Cin, g.nphase, nullptr, true);
-  return pr.pl.ksplit > 1 && (long long)g.nphase * B * Hg * Wg <= BNA_ITEMS;
-}
-
-int bf16_conv_fwd_bnact(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
-                        const float* bias, const stc_bn_act& a, void* ws, int64_t ws_bytes, hipStream_t st) {
-  STC_REQUIRE(bf16_conv_bnact_ok(kind, B, x, Cin, Cout, y), "bf16 conv: no fused split-K BatchNorm for this shape");
-  STC_REQUIRE(a.scale && a.shift && a.a1.p && a.a1.cs == 1 && (!a.a2.p || a.a2.cs == 1),
-              "bf16 conv: fused BatchNorm needs scale/shift and NHWC activation views");
-  BnAct b{};
-  b.gamma = a.gamma; b.beta = a.beta; b.rmean = a.running_mean; b.rvar = a.running_var;
-  b.nbt = (long long*)a.num_batches_tracked; b.momentum = a.momentum; b.eps = a.eps;
-  b.mean_o = a.mean; b.rstd_o = a.rstd; b.scale = a.scale; b.shift = a.shift;
-  b.a1 = (char*)a.a1.p; b.a1_bs = a.a1.bs; b.a1_rs = a.a1.rs; b.a1_ps = a.a1.ps; b.a1_co = a.a1.co; b.s1 = a.slope1;
-  b.a2 = (char*)a.a2.p; b.a2_bs = a.a2.bs; b.a2_rs = a.a2.rs; b.a2_ps = a.a2.ps; b.a2_co = a.a2.co; b.s2 = a.slope2;
-  b.aH = a.a1.H; b.aW = a.a1.W;
-  return bf16_conv_fwd(kind, B, x, Cin, w_packed, Cout, y, bias, 0, 0, nullptr, 0, nullptr, ws, ws_bytes, st, nullptr,
-                       nullptr, nullptr, nullptr, 0, 0.f, 0.f, &b);
+  return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st);
 }
 
 // The activation epilogue applies when the layer runs as one LDS-DMA GEMM launch (no split-K) with 16-byte

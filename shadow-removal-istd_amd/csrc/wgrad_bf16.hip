@@ -498,8 +498,8 @@ static WbPlan wb_plan(int P, int R, int Cg, const int32_t* force) {
     else if (R <= 64) cfg = 1;
     else if (ncol >= 1024 && ((R >= 512 && P >= 16384) || (R >= 256 && P >= 65536))) cfg = 3;
     // 128x128 + 4 loader waves, 3-stage ring (96 KiB: a 64 KiB conv block still fits beside it): 5-13 % under
-    // cfg 0 in isolation, -0.16 ms per train step in situ (profiles/r03/diag/plan_ab.log); STC_WPLAN_R2=1: cfg 0
-    else cfg = getenv("STC_WPLAN_R2") ? 0 : 7;
+    // cfg 0 in isolation, -0.16 ms per train step in situ (profiles/r03/diag/plan_ab.log)
+    else cfg = 7;
   }
   const WbCfg& c = kWbCfg[cfg];
   pl.cfg = cfg;

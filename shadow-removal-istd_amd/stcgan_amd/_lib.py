@@ -38,24 +38,6 @@ class BnbFuse(ctypes.Structure):
                 ("slope_other", ctypes.c_float), ("C", ctypes.c_int32), ("ch_off", ctypes.c_int32)]
 
 
-class BnFin(ctypes.Structure):
-    """stc_bn_fin: the BatchNorm finalize fused into the conv that produces its partials."""
-    _fields_ = [("counters", ctypes.c_void_p), ("scratch", ctypes.c_void_p), ("gamma", ctypes.c_void_p),
-                ("beta", ctypes.c_void_p), ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
-                ("num_batches_tracked", ctypes.c_void_p), ("momentum", ctypes.c_float), ("eps", ctypes.c_float),
-                ("mean", ctypes.c_void_p), ("rstd", ctypes.c_void_p), ("scale", ctypes.c_void_p),
-                ("shift", ctypes.c_void_p), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p)]
-
-
-class BnAct(ctypes.Structure):
-    """stc_bn_act: BatchNorm (train) + activation fused into a deep split-K conv's reduction."""
-    _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("running_mean", ctypes.c_void_p),
-                ("running_var", ctypes.c_void_p), ("num_batches_tracked", ctypes.c_void_p),
-                ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("mean", ctypes.c_void_p),
-                ("rstd", ctypes.c_void_p), ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p), ("a1", View),
-                ("slope1", ctypes.c_float), ("a2", View), ("slope2", ctypes.c_float)]
-
-
 class PackDesc(ctypes.Structure):
     """stc_pack_desc: one stc_pack_weight job of a multi-tensor stc_pack_weights launch."""
     _fields_ = [("mode", ctypes.c_int32), ("P", ctypes.c_int32), ("Q", ctypes.c_int32), ("N_pad", ctypes.c_int32),
@@ -74,14 +56,8 @@ _SIGS = {
     "stc_conv_bwd_bn": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _i32, _vp, _i64, _vp]),
     "stc_conv_fwd_ex": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _i32, _i32, _vp, _i32, _vp, _vp,
                                _i64, _vp]),
-    "stc_conv_fwd_bn_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View]),
-    "stc_conv_fwd_bn_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _vp, _i64, _vp]),
     "stc_conv_fwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View]),
     "stc_conv_fwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _f32, View, _f32, _vp, _vp, _i64, _vp]),
-    "stc_bn_fin_counters": (_i32, []),
-    "stc_conv_fwd_bnfin": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _i32, _vp, _vp, _vp, _i64,
-                                  _vp]),
-    "stc_conv_bwd_bnfin": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _i32, _vp, _vp, _i64, _vp]),
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
                               _f32, _vp, _vp, _i64, _vp]),
     "stc_conv_wgrad_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32]),

@@ -208,7 +208,8 @@ class ISTDLoader:
     ``np.random`` when ``workers == 0``.  With ``world > 1`` every rank draws the same global batch
     and decodes and prepares only its shard (``shard_bounds``), as nn.DataParallel scatters it; a
     final batch smaller than ``world`` is skipped on every rank (no rank may sit out a step's
-    collectives), and the loss means of a ragged final batch weight the ranks equally."""
+    collectives), and the trainer weights each rank's loss means of a ragged final batch by its share
+    (``last_global``: the global size of the batch last yielded; stcgan.batch_weight)."""
 
     DIRS = {"img": "A", "mask": "B", "matte": "matte", "target": "C_fixed"}
 
@@ -230,6 +231,7 @@ class ISTDLoader:
         self.resize = resize
         self.aug = dict(scale=scale, angle=angle, flip_prob=flip_prob, crop_size=crop_size)
         self.rank, self.world, self.device = rank, world, device
+        self.last_global = None  # global size of the batch last yielded
 
     def __len__(self):
         n = len(self.names)
@@ -274,6 +276,7 @@ class ISTDLoader:
                 tensors = [resize(t, self.resize) for t in tensors]
             H, W = tensors[0].shape[1:3]
             scales, angles, params, geom = draw_params(len(sel), H, W, rng=rng, **self.aug)
+            self.last_global = len(sel)  # (the trainer's batch_weight)
             sl = slice(lo, hi)
             out = apply_draws(tensors, None if scales is None else scales[sl], None if angles is None else angles[sl],
                               params[sl], geom)

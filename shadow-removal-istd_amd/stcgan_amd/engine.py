@@ -107,9 +107,9 @@ class GradWriter:
     gradients are enqueued (``done``), so its buckets are all-reduced while the backward continues."""
 
     def __init__(self, net):
-        from .parallel import flat_grads
+        from .parallel import exchange_of, flat_grads
         self.flat = flat_grads(net)
-        self.exchange = getattr(net, "grad_exchange", None)
+        self.exchange = exchange_of(net)
         self.acc = []
         self._acc_ids = set()
 
@@ -118,6 +118,12 @@ class GradWriter:
         if g is None:
             p.grad = self.flat.view(p)
             return p.grad
+        if not self.flat.owns(g, p):
+            # a gradient that is not this network's flat-buffer view (assigned by the caller, or carried along by
+            # a module move): moved into the view, so that the exchange averages what the optimiser reads
+            v = self.flat.view(p)
+            v.copy_(g)
+            p.grad = g = v
         s = torch.empty(p.shape, dtype=torch.float32, device=p.device)
         self.acc.append((g, s, p))
         self._acc_ids.add(id(p))
@@ -202,18 +208,11 @@ def _pad2(S, k):
     return (2 * S[k + 1][0], 2 * S[k + 1][1])
 
 
-def _fin_bn(bn):
-    """The BatchNorm whose backward sums are finalized inside the input-gradient conv (None: separate kernel)."""
-    return bn if ops.FUSE_FINALIZE else None
-
-
 def _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev):
     """Conv whose output feeds a BatchNorm2d: returns ((2, cout) scale/shift table, (mean, rstd) or None).
     Train mode: the batch statistics come out of the conv itself (stc_conv_fwd_ex)."""
     t = torch.empty((2, cout), dtype=torch.float32, device=dev)
-    if train and ops.FUSE_FINALIZE:
-        st = ops.conv_stats_fin(kind, B, xv, cin, w, cout, yv, dt, bn, t[0], t[1])
-    elif train:
+    if train:
         part, nch = ops.conv_stats(kind, B, xv, cin, w, cout, yv, dt)
         st = ops.bn_finalize_part(part, nch, cout, bn, t[0], t[1])
     else:
@@ -265,17 +264,10 @@ def gen_forward(plan, sources, train, dt, cache, save):
     for k in range(1, Lv):
         wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
         if k <= Lv - 2:
-            t = torch.empty((2, co[k]), dtype=torch.float32, device=dev)
-            st = ops.conv_bn_act(L.CONV_S2, B, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]), dt,
-                                 plan.bnd[k], t[0], t[1], L.nhwc_view(ad[k]), LRELU, L.nhwc_view(cr[k], 0),
-                                 0.0) if train else None
-            if st is not None:  # deep split-K level: reduction + statistics + finalize + apply in one launch
-                tab_d[k], st_d[k] = t, st
-            else:
-                tab_d[k], st_d[k] = conv_bn(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k],
-                                            L.nhwc_view(rd[k]), plan.bnd[k])
-                ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]),
-                             LRELU, L.nhwc_view(cr[k], 0), 0.0)
+            tab_d[k], st_d[k] = conv_bn(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k],
+                                        L.nhwc_view(rd[k]), plan.bnd[k])
+            ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]),
+                         LRELU, L.nhwc_view(cr[k], 0), 0.0)
         else:  # innermost: no down-norm (STCGAN/networks.py:118-124)
             ops.conv(L.CONV_S2, B, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]), dt)
             ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, None, L.nhwc_view(cr[k]), 0.0)
@@ -283,16 +275,10 @@ def gen_forward(plan, sources, train, dt, cache, save):
     for k in range(Lv - 1, 0, -1):
         wt = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_FWD, co[k - 1], cin_t(k), dt)
         # statistics over the full ConvT extent (before the crop of an odd level)
-        t = torch.empty((2, co[k - 1]), dtype=torch.float32, device=dev)
-        st = ops.conv_bn_act(L.CONVT_S2, B, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]), dt,
-                             plan.bnu[k], t[0], t[1], L.nhwc_view(cr[k - 1], co[k - 1], *S[k]), 0.0) if train else None
-        if st is not None:  # deep split-K level: one launch after the GEMM (statistics over the full extent)
-            tab_u[k], st_u[k] = t, st
-        else:
-            tab_u[k], st_u[k] = conv_bn(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
-                                        plan.bnu[k])
-            ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
-                         L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
+        tab_u[k], st_u[k] = conv_bn(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
+                                    plan.bnu[k])
+        ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
+                     L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
     # ---- outermost: tanh(convT_0(cr[0]) + bias) -> NCHW fp32
     Ho, Wo = 2 * S[1][0], 2 * S[1][1]
     y = torch.empty((B, plan.out_c, Ho, Wo), dtype=torch.float32, device=dev)
@@ -368,7 +354,7 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
         ops.conv_bn_backward(L.CONV_S2, B, dqv, cg, wd, cin_t, L.nhwc_view(gcat[k], 0, *S[k + 1]), dt,
                              bn_x=L.nhwc_view(rq[k + 1]), C=C, bn_state=(t[0], t[1], mean, rstd),
                              gamma=bn.weight, s_self=0.0, ch_off=C, dxv=L.nhwc_view(dq),
-                             dgamma=dest(bn.weight), dbeta=dest(bn.bias), bn=_fin_bn(bn))
+                             dgamma=dest(bn.weight), dbeta=dest(bn.bias))
         if need_w:
             W.done([plan.convT[k].weight], lane)
             W.done([bn.weight, bn.bias])
@@ -425,7 +411,7 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
             ops.conv_bn_backward(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt, bn_x=xv, C=cprev,
                                  bn_state=(t[0], t[1], mean, rstd), gamma=bn.weight, s_self=LRELU,
                                  g_other=g1, s_other=0.0, dxv=L.nhwc_view(dr), dgamma=dest(bn.weight),
-                                 dbeta=dest(bn.bias), bn=_fin_bn(bn))
+                                 dbeta=dest(bn.bias))
             if need_w:
                 W.done([plan.conv[k].weight], lane)
                 W.done([bn.weight, bn.bias])
@@ -615,7 +601,7 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, W):
                                  bn_state=(tabs[i][0], tabs[i][1], mean, rstd), gamma=bn.weight,
                                  s_self=LRELU, dxv=L.nhwc_view(gn),
                                  dgamma=W.dest(bn.weight) if need_w else None,
-                                 dbeta=W.dest(bn.bias) if need_w else None, bn=_fin_bn(bn))
+                                 dbeta=W.dest(bn.bias) if need_w else None)
             if need_w:
                 W.done(own, lane)
                 W.done([bn.weight, bn.bias])

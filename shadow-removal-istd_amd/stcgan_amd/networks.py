@@ -57,6 +57,7 @@ class _HipNet(nn.Module):
         # parallel.BucketExchange averaging this network's gradients over the ranks while its backward runs
         # (set by the trainer when world > 1), or None
         self.grad_exchange = None
+        self._exchange_spec = None
         # dict reusing gathered inputs across this network's calls on the same tensors (set by the trainer
         # for one train step), or None
         self.input_cache = None
@@ -95,6 +96,9 @@ class _HipNet(nn.Module):
         # the flat gradient buffer (parallel.flat_grads) lives on the parameters' device: a new one is made
         # on the next backward; an exchange bound to the old buffer is dropped with it
         self._flat_grads = None
+        ex = self.grad_exchange
+        if ex is not None:  # re-made on the new buffer by the next backward (engine.GradWriter)
+            self._exchange_spec = (ex.bucket_elems * 4 / (1 << 20), ex.active, ex.on_complete, ex.expected)
         self.grad_exchange = None
         return super()._apply(fn, *args, **kwargs)
 

@@ -4,7 +4,6 @@ Every function here enqueues HIP kernels of libstcgan_hip.so on torch's current
 stream; torch is used only for device memory (caching allocator) and streams.
 """
 import ctypes
-import os
 
 import torch
 
@@ -114,8 +113,9 @@ FORCE_CONV = {}
 FORCE_WGRAD = {}
 
 
-# conv + activation epilogue for the layers without BatchNorm (stc_conv_fwd_act); STC_ACT_EPI=0: conv + bn_apply
-FUSE_ACT = os.environ.get("STC_ACT_EPI", "1") != "0"
+# conv + activation epilogue for the layers without BatchNorm (stc_conv_fwd_act); False (A/B scripts): conv +
+# bn_apply
+FUSE_ACT = True
 
 
 def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bias=None):
@@ -141,48 +141,8 @@ def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bi
         _disarm()
     check(rc, "stc_conv_fwd_act")
     if timer is not None:
-        halo = kind == L.CONV_S2 and cin == 8 and cout == 64 and os.environ.get("STC_HALO8", "0") == "1"
-        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, name="halo8_conv_kernel" if halo else None)
-    return True
-
-
-# deep split-K layers: conv + BatchNorm + activation in two launches (stc_conv_fwd_bn_act) -- opt-in
-# (STC_BN_ACT=1): a block must own whole channels, so the fused pass runs on N/8 blocks reading 32-byte
-# row pieces and measured slower (20-28 us) than the three full-chip launches it replaces
-FUSE_BN_ACT = os.environ.get("STC_BN_ACT", "0") == "1"
-
-
-def conv_bn_act(kind, B, xv, cin, w_packed, cout, yv, dt, bn, scale_out, shift_out, a1v, s1, a2v=None, s2=0.0):
-    """Deep split-K conv -> train-mode BatchNorm -> activation(s): yv gets the raw output, a1v = act(BN, s1)
-    [a2v = act(BN, s2)]; the BN tables go to scale_out / shift_out and the running statistics are updated.
-    Returns (mean, rstd), or None (nothing launched) when the shape has no fused form."""
-    l = lib()
-    if not FUSE_BN_ACT or dt != torch.bfloat16 or not l.stc_conv_fwd_bn_act_ok(L.dtype_code(dt), kind, B, xv, cin,
-                                                                                 cout, yv):
-        return None
-    gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
-    if FORCE_CONV and FORCE_CONV.get((kind, B, gh, gw, cin, cout)) is not None:
-        return None  # a forced plan runs through conv_stats
-    dev = w_packed.device
-    nbytes, _nch, _plan = conv_query(kind, B, gh, gw, cin, cout, dt)
-    ws, nb = _ws(nbytes, dev)
-    mean = torch.empty(cout, dtype=torch.float32, device=dev)
-    rstd = torch.empty(cout, dtype=torch.float32, device=dev)
-    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
-    a = L.BnAct(ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), ptr(bn.num_batches_tracked),
-                float(mom), float(bn.eps), ptr(mean), ptr(rstd), ptr(scale_out), ptr(shift_out), a1v, float(s1),
-                a2v if a2v is not None else L.NULL_VIEW, float(s2))
-    timer = _timer
-    if timer is not None:
-        e0, e1 = _main_events()
-    rc = l.stc_conv_fwd_bn_act(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, None, ctypes.byref(a),
-                               ptr(ws), nb, stream())
-    if timer is not None:
-        _disarm()
-    check(rc, "stc_conv_fwd_bn_act")
-    if timer is not None:
         _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
-    return mean, rstd
+    return True
 
 
 def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
@@ -252,7 +212,7 @@ def _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=False, name=N
 
 
 def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state, gamma, s_self, ch_off=0,
-                     g_other=None, s_other=0.0, dxv=None, dgamma=None, dbeta=None, bn=None):
+                     g_other=None, s_other=0.0, dxv=None, dgamma=None, dbeta=None):
     """Input-gradient conv (output yv) whose output feeds a BatchNorm backward, with the BN
     reduction fused into the conv (stc_conv_bwd_bn), then the BN apply (stc_bn_bwd_apply):
     dx = BN-backward of dn = out*act'(n, s_self) [+ g_other*act'(n, s_other)].
@@ -272,18 +232,11 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
         e0, e1 = _main_events()
     dgamma = _out1(dgamma, C, dev)
     dbeta = _out1(dbeta, C, dev)
-    if bn is not None:  # dbeta/dgamma finalized inside the conv launch (stc_conv_bwd_bnfin)
-        cnt, scr = _fin_state(bn, C, dev, "bwd")
-        fin = L.BnFin(cnt.data_ptr(), scr.data_ptr(), None, None, None, None, None, 0.0, 0.0, None, None, None, None,
-                      ptr(dgamma), ptr(dbeta))
-        rc = l.stc_conv_bwd_bnfin(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse),
-                                  ptr(part), nch, ctypes.byref(fin), ptr(ws), nb, stream())
-    else:
-        rc = l.stc_conv_bwd_bn(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse),
-                               ptr(part), nch, ptr(ws), nb, stream())
+    rc = l.stc_conv_bwd_bn(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse),
+                           ptr(part), nch, ptr(ws), nb, stream())
     if timer is not None:
         _disarm()
-    check(rc, "stc_conv_bwd_bnfin" if bn is not None else "stc_conv_bwd_bn")
+    check(rc, "stc_conv_bwd_bn")
     if timer is not None:
         _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=yv.cs == 1)
     # apply: g1 = the conv output at the BN channels over the BN extent
@@ -291,59 +244,9 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
     g1._keep = yv
     check(l.stc_bn_bwd_apply(L.dtype_code(dt), B, bn_x, C, ptr(scale), ptr(shift), ptr(mean), ptr(rstd), ptr(gamma),
                              g1, float(s_self), g_other if g_other is not None else L.NULL_VIEW, float(s_other),
-                             None if bn is not None else ptr(part), 0 if bn is not None else nch, dxv, ptr(dgamma),
+                             ptr(part), nch, dxv, ptr(dgamma),
                              ptr(dbeta), stream()), "stc_bn_bwd_apply")
     return dgamma, dbeta
-
-
-# BatchNorm finalize fused into the producing conv (stc_conv_fwd_bnfin / stc_conv_bwd_bnfin); STC_BNFIN=0 runs
-# the separate finalize kernels (default until the A/B favours the fused form)
-FUSE_FINALIZE = os.environ.get("STC_BNFIN", "0") != "0"
-
-
-def _fin_state(bn, C, dev, which):
-    """Per-BatchNorm (module, device, forward/backward) counters and level-2 scratch of the finalize fused
-    into the producing conv (stc_bn_fin): the counters are zeroed once here and left zero by every call."""
-    key = (str(dev), which)
-    states = bn.__dict__.setdefault("_stc_fin", {})
-    st = states.get(key)
-    if st is None or st[1].numel() < 64 * C * 4:
-        st = (torch.zeros(lib().stc_bn_fin_counters(), dtype=torch.int32, device=dev),
-              torch.empty(64 * C * 4, dtype=torch.float32, device=dev))
-        states[key] = st
-    return st
-
-
-def conv_stats_fin(kind, B, xv, cin, w_packed, cout, yv, dt, bn, scale_out, shift_out, bias=None, force=None):
-    """Conv forward + its BatchNorm's batch statistics, finalized inside the conv launch
-    (stc_conv_fwd_bnfin: the producer's last-arriving blocks merge the partials and write the tables and the
-    running statistics -- no separate finalize kernel).  Returns (mean, rstd)."""
-    dev = w_packed.device
-    gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
-    if force is None and FORCE_CONV:
-        force = FORCE_CONV.get((kind, B, gh, gw, cin, cout))
-    nbytes, nch, plan = conv_query(kind, B, gh, gw, cin, cout, dt, force=force)
-    ws, nb = _ws(nbytes, dev)
-    part = torch.empty((nch, cout, 4), dtype=torch.float32, device=dev)
-    mean = torch.empty(cout, dtype=torch.float32, device=dev)
-    rstd = torch.empty(cout, dtype=torch.float32, device=dev)
-    cnt, scr = _fin_state(bn, cout, dev, "fwd")
-    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
-    fin = L.BnFin(cnt.data_ptr(), scr.data_ptr(), ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
-                  ptr(bn.running_var), ptr(bn.num_batches_tracked), float(mom), float(bn.eps), ptr(mean), ptr(rstd),
-                  ptr(scale_out), ptr(shift_out), None, None)
-    fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
-    timer = _timer
-    if timer is not None:
-        e0, e1 = _main_events()
-    rc = lib().stc_conv_fwd_bnfin(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ptr(bias), ptr(part),
-                                  nch, ctypes.byref(fin), fp, ptr(ws), nb, stream())
-    if timer is not None:
-        _disarm()
-    check(rc, "stc_conv_fwd_bnfin")
-    if timer is not None:
-        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
-    return mean, rstd
 
 
 def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True):
@@ -393,10 +296,10 @@ def _wgrad_kernel_name(plan, Hd, Wd):
 
 
 # The narrow-R VALU weight gradient (stc_conv_wgrad_rows) for the PatchGAN logits layer (~25 us vs ~75 us
-# for the padded GEMM).  STC_WGRAD_ROWS=0 (or rows_kernel=False per call) takes the GEMM path.  Its
+# for the padded GEMM).  rows_kernel=False per call takes the GEMM path.  Its
 # accumulations are forced to non-packed v_fma_f32 (csrc/wgrad.hip): compiled to v_pk_fma_f32 with op_sel,
 # it returned sporadically different low-half sums with two processes on one GPU (tests/test_gpu_dist.py).
-_ROWS_DEFAULT = os.environ.get("STC_WGRAD_ROWS", "1") == "1"
+_ROWS_DEFAULT = True
 
 
 def _out1(t, n, device):

@@ -55,7 +55,11 @@ class Adam(torch.optim.Optimizer):
 
     def _full_step(self, gi, group, skip=()):
         """The general path (first steps, moved tensors, new packed operands); ``skip``: parameters already
-        updated this step (by overlap), left out."""
+        updated this step (by overlap), left out.  With device-resident step counts (device_step) the host
+        counts are first brought level with the device counter (replays advance only that), and the counter
+        is set to the count this step reaches, so the next steady-state step (or replay) continues from it."""
+        if self._dev is not None and gi in self._dev:
+            self._pull_device_steps(gi, skip)
         b1, b2 = group["betas"]
         # group params by step count (all equal in practice).  The step count is mirrored in a
         # Python int (no per-parameter tensor op / .item() on the host path), and the state's
@@ -105,6 +109,9 @@ class Adam(torch.optim.Optimizer):
                 ver = ops.pack_version(p)
                 for (pkey, cache, out) in targets:
                     cache[pkey] = (ver, out)
+        if self._dev is not None and gi in self._dev and len(by_step) == 1:
+            (step,), = (tuple(by_step),)
+            self._dev[gi]["step"].fill_(int(step))  # (stream-ordered; a captured graph keeps this tensor)
         self._fast.pop(gi, None)
         if len(by_step) == 1 and not skip:
             (step, plist), = by_step.items()
@@ -293,7 +300,11 @@ class Adam(torch.optim.Optimizer):
             upd = plist
         else:  # the rest on the general path; the updated part's host-side state advanced here
             upd = [plist[i] for i in done]
-            torch._foreach_add_([f["step_tensors"][i] for i in done], 1.0)
+            if self._dev is not None and gi in self._dev:
+                self._pull_device_steps(gi, {id(p) for p in upd})  # (device counts: already advanced)
+                step = f["step"] + 1
+            else:
+                torch._foreach_add_([f["step_tensors"][i] for i in done], 1.0)
         ops.bump(upd)
         for p in upd:
             i = f["index"][id(p)]
@@ -360,6 +371,21 @@ class Adam(torch.optim.Optimizer):
                 d["lr_dev"].fill_(float(np.float32(lr)))
                 d["lr"] = lr
 
+    def _pull_device_steps(self, gi, updated=()):
+        """Host step counts of group ``gi`` from its device counter: parameters whose update of this step already
+        ran (``updated``: ids) get the count this step reaches, the others the count before it."""
+        d, f = self._dev.get(gi), self._fast.get(gi)
+        if d is None or f is None:  # (no steady-state record, e.g. after load_state_dict: the host state rules)
+            return
+        s = int(d["step"].item())
+        if gi in self._ov_coef:  # this step's advance already happened (overlapped bucket updates)
+            s -= 1
+        for p, st in zip(f["plist"], f["step_tensors"]):
+            v = s + 1 if id(p) in updated else s
+            st.fill_(float(v))
+            self._steps[id(p)] = (st, v)
+        f["step"] = s
+
     def sync_steps(self):
         """Host step counts (state["step"], the steady-state mirrors) from the device counters."""
         if not self._dev:
@@ -385,9 +411,20 @@ class Adam(torch.optim.Optimizer):
         return (p.numel() + 1023) // 1024
 
     def load_state_dict(self, state_dict):
+        if self._ov_done:  # updates of an overlapped backward that no step() finished
+            self.step()
         self._fast = {}
         self._steps = {}
-        return super().load_state_dict(state_dict)
+        self._ov_done = {}
+        out = super().load_state_dict(state_dict)
+        # device-resident counts (device_step): the loaded state's; the counter tensors are kept (a captured
+        # graph holds them), the next step takes the general path and writes them
+        if self._dev:
+            for gi, d in self._dev.items():
+                st = [self.state[p]["step"] for p in self.param_groups[gi]["params"] if "step" in self.state[p]]
+                if st:
+                    d["step"].fill_(int(st[0].item()))
+        return out
 
     def _record(self, p):
         """(table row without first_block, blocks, packed targets) of one parameter."""

@@ -100,7 +100,7 @@ def average_scalars(values):
     if world() == 1:
         return dict(values)
     keys = list(values)
-    t = torch.stack([values[k].float().reshape(()) for k in keys])
+    t = torch.stack([values[k].double().reshape(()) for k in keys])  # (float64: the epoch sums)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     t.div_(world())
     return {k: t[i] for i, k in enumerate(keys)}
@@ -145,6 +145,20 @@ def flat_grads(net):
         fg = FlatGrads(list(net.parameters()))
         net._flat_grads = fg
     return fg
+
+
+def exchange_of(net):
+    """The network's BucketExchange (``net.grad_exchange``, set by the trainer), re-made on the current flat
+    buffer when the module moved since (networks._HipNet._apply drops the exchange bound to the old buffer and
+    keeps its settings), so the ranks keep averaging its gradients after a ``.to()``."""
+    ex = getattr(net, "grad_exchange", None)
+    spec = getattr(net, "_exchange_spec", None)
+    if ex is None and spec is not None:
+        bucket_mb, active, on_complete, expected = spec
+        ex = net.grad_exchange = BucketExchange(flat_grads(net), bucket_mb, active)
+        ex.on_complete, ex.expected = on_complete, expected
+        net._exchange_spec = None
+    return ex
 
 
 class BucketExchange:
@@ -224,6 +238,18 @@ class BucketExchange:
                     if self.on_complete is not None and (not self.active or self._op() != dist.ReduceOp.SUM):
                         self.on_complete(self.member_params[b], stream, self.works[b])
 
+    def check_order(self):
+        """Debug check (tests, CPU gloo runs): every rank launched its buckets' collectives in the same order
+        (the engine reports layers in autograd order; a divergence would pair different buckets in one
+        collective).  Collective itself; raises on a mismatch.  Call before ``finish`` (which resets)."""
+        if world() == 1:
+            return
+        mine = list(self.launch_order)
+        allo = [None] * world()
+        dist.all_gather_object(allo, mine)
+        if any(o != allo[0] for o in allo):
+            raise RuntimeError(f"BucketExchange: bucket launch order differs across ranks: {allo}")
+
     def finish(self):
         w = world()
         if not self.active:
@@ -256,7 +282,16 @@ class GradAllReduce:
                     f.view(p).copy_(p.grad)
                 p.grad = f.view(p)
                 if p.requires_grad and world() > 1:
-                    self.hooks.append(p.register_post_accumulate_grad_hook(lambda q, ex=ex: ex.ready([q])))
+                    self.hooks.append(p.register_post_accumulate_grad_hook(lambda q, ex=ex, f=f: self._ready(f, ex, q)))
+
+    @staticmethod
+    def _ready(f, ex, q):
+        # after a zero_grad(set_to_none=True) autograd accumulates into a fresh tensor, not the view: move it in
+        if not f.owns(q.grad, q):
+            v = f.view(q)
+            v.copy_(q.grad)
+            q.grad = v
+        ex.ready([q])
 
     def enable_overlap(self):  # (hooks are registered at construction)
         pass

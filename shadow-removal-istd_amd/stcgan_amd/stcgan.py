@@ -53,6 +53,26 @@ class SyntheticTriplets:
             yield ([f"synthetic_{i}_{j}" for j in range(self.bs)], x, m, y)
 
 
+def batch_weight(local_n, global_n, world):
+    """Weight of one rank's batch means in the rank average (parallel.average_scalars): n_local * world /
+    n_global, so that the average of the weighted per-rank means is the mean over the global batch -- what the
+    reference computes on DataParallel's gathered outputs -- also for a ragged final batch, whose shards differ
+    by one sample (data.shard_bounds).  1.0 at world size 1 or when the global size is unknown."""
+    if world <= 1 or not global_n:
+        return 1.0
+    return local_n * world / global_n
+
+
+def accumulate(acc, vals, d_out, weight=1.0):
+    """Add one step's losses (``vals``: device fp32 scalars) and mean discriminator outputs (``d_out``: C1_real,
+    C1_fake, C2_real, C2_fake) into the float64 device sums ``acc``, each value widened to float64 first (the
+    reference adds the float32 results' .item() to Python floats) and scaled by ``weight`` (batch_weight)."""
+    for k, v in vals.items():
+        acc[k] = acc[k] + v.double() * weight
+    for k, c in zip(("D1_real", "D1_fake", "D2_real", "D2_fake"), d_out):
+        acc[k] = acc[k] + c.mean().double() * weight
+
+
 class STCGAN(object):
 
     def __init__(self, args, train_loader=None, valid_loader=None):
@@ -157,13 +177,13 @@ class STCGAN(object):
         """Set how many backward calls write each network's gradients in this step (the discriminators are
         called on real and on fake inputs inside the D step's graph)."""
         for n in names:
-            ex = getattr(self, n).grad_exchange
+            ex = parallel.exchange_of(getattr(self, n))
             if ex is not None:
                 ex.expected = expected
 
     def _finish_exchange(self, names):
         for n in names:
-            ex = getattr(self, n).grad_exchange
+            ex = parallel.exchange_of(getattr(self, n))
             if ex is not None:
                 ex.finish()
 
@@ -262,7 +282,7 @@ class STCGAN(object):
         out.record_stream(torch.cuda.current_stream(self.device))
         return out
 
-    def train_step(self, x, m, y, training=True, acc=None, inputs_ready=None):
+    def train_step(self, x, m, y, training=True, acc=None, inputs_ready=None, weight=1.0):
         """One iteration of STCGAN.run_epoch (STCGAN/stcgan.py:208-312): D step then G step.
         Returns the on-device loss scalars (no host sync).  The call order of every network
         (and so every BN running-statistics update) is the reference's; with ``streams`` the
@@ -304,11 +324,11 @@ class STCGAN(object):
         # each discriminator sees the same real and fake inputs in the D and the G step: gather them once
         self.D1.input_cache, self.D2.input_cache = {}, {}
         try:
-            return self._step(x, m, y, training, acc, main, l1, l2)
+            return self._step(x, m, y, training, acc, main, l1, l2, weight)
         finally:
             self.D1.input_cache = self.D2.input_cache = None
 
-    def _step(self, x, m, y, training, acc, main, l1, l2):
+    def _step(self, x, m, y, training, acc, main, l1, l2, weight=1.0):
         with torch.set_grad_enabled(training):
             self.optim_D.zero_grad()
             self.D1.requires_grad_(True)
@@ -378,12 +398,7 @@ class STCGAN(object):
         vals = dict(D1=D1_loss.detach(), D2=D2_loss.detach(), D=D_loss.detach(), G1=G1_loss.detach(),
                     G2=G2_loss.detach(), data1=data1_loss.detach(), data2=data2_loss.detach(), G=G_loss.detach())
         if acc is not None:
-            for k, v in vals.items():
-                acc[k] = acc[k] + v
-            acc["D1_real"] = acc["D1_real"] + d_out[0].mean()
-            acc["D1_fake"] = acc["D1_fake"] + d_out[1].mean()
-            acc["D2_real"] = acc["D2_real"] + d_out[2].mean()
-            acc["D2_fake"] = acc["D2_fake"] + d_out[3].mean()
+            accumulate(acc, vals, d_out, weight)
         return vals
 
     def capture(self, x, m, y, warmup=1):
@@ -422,6 +437,10 @@ class STCGAN(object):
         with torch.cuda.graph(graph, stream=cap):
             self.train_step(x, m, y)
         self._graph = graph
+        # the optimisers' device pointer tables the captured launches read: kept alive even when a later eager
+        # step on the general path replaces them (freed, their memory could be reused under the graph)
+        self._graph_refs = [t for o in (self.optim_G, self.optim_D) for f in o._fast.values()
+                            for t in [f["table"]] + [sub[0] for sub in f["subs"].values()]]
 
         def replay():
             for o in (self.optim_G, self.optim_D):
@@ -436,7 +455,10 @@ class STCGAN(object):
             parallel.broadcast_buffers([self.G1, self.G2, self.D1, self.D2])
         self._lanes_stale = True  # (the broadcast above, a checkpoint load, a caller's writes between epochs)
         keys = ["G", "D", "D1", "D2", "G1", "G2", "data1", "data2"]
-        acc = {k: torch.zeros((), device=self.device) for k in keys + ["D1_real", "D1_fake", "D2_real", "D2_fake"]}
+        # float64 sums, as the reference's Python-float accumulation of .item() values (STCGAN/stcgan.py:256-262,
+        # 308-312) that ReduceLROnPlateau then reads
+        acc = {k: torch.zeros((), dtype=torch.float64, device=self.device)
+               for k in keys + ["D1_real", "D1_fake", "D2_real", "D2_fake"]}
         data_loader = self.train_loader if training else self.valid_loader
         n_batches = 0
         # with the side lanes, batches are prepared on an input stream and handed over with an event, so the
@@ -460,7 +482,9 @@ class STCGAN(object):
             if b is None:
                 break
             x, m, y = b
-            self.train_step(x, m, y, training=training, acc=acc, inputs_ready=ready)
+            # a ragged final batch is split unevenly over the ranks: weight each rank's means by its share
+            w = batch_weight(x.shape[0], getattr(data_loader, "last_global", None), parallel.world())
+            self.train_step(x, m, y, training=training, acc=acc, inputs_ready=ready, weight=w)
             n_batches += 1
         # global-batch values on every rank (DataParallel computes the losses on the gathered
         # batch), so each rank's ReduceLROnPlateau sees the same sums: one collective, one host sync

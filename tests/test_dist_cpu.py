@@ -199,6 +199,25 @@ def _worker_semantics(rank, world, port, out):
     order = list(ex.launch_order)
     ex.finish()
     res["order"] = (held, order, fg.view(a).clone(), fg.view(b).clone(), [fg.spans[id(a)], fg.spans[id(b)]])
+    # (5) a ragged final batch of 5 (shards 3 + 2, data.shard_bounds): each rank's means weighted by its share
+    # (stcgan.batch_weight) average to the global-batch means the reference logs (STCGAN/stcgan.py:256-262)
+    from stcgan_amd import data, stcgan
+    per_sample = torch.tensor([0.5, 1.25, -2.0, 4.0, 0.75])
+    c_out = torch.arange(5 * 4, dtype=torch.float32).reshape(5, 1, 2, 2) / 7.0
+    lo, hi = data.shard_bounds(5, rank, world)
+    acc = {k: torch.zeros((), dtype=torch.float64) for k in ("D", "D1_real", "D1_fake", "D2_real", "D2_fake")}
+    w = stcgan.batch_weight(hi - lo, 5, world)
+    stcgan.accumulate(acc, {"D": per_sample[lo:hi].mean()}, [c_out[lo:hi]] * 4, w)
+    res["ragged"] = ((lo, hi), {k: float(v) for k, v in parallel.average_scalars(acc).items()})
+    # (6) GradAllReduce across a set_to_none zero_grad: autograd's fresh gradients are moved into the views
+    q = torch.zeros(4, requires_grad=True)
+    sync2 = parallel.GradAllReduce([[q]])
+    for it in range(2):
+        q.grad = None  # (optimizer.zero_grad(set_to_none=True))
+        (q * float(rank + 1 + it)).sum().backward()
+        sync2.exchanges[0].check_order()
+        sync2()
+    res["zero_grad"] = (q.grad.clone(), sync2.flats[0].owns(q.grad, q))
     import io
     buf = io.BytesIO()
     torch.save(res, buf)  # bytes, not shared-memory tensors: the worker exits before the parent reads
@@ -238,3 +257,13 @@ def test_dataparallel_semantics_world2():
         assert spans == [(5, 3), (0, 5)]  # reverse module order: b first
         assert held == [] and order == [0, 1]
         assert torch.equal(ga, torch.full((3,), 3.0)) and torch.equal(gb, torch.full((5,), 1.5))
+        # ragged final batch: the logged values are the global-batch means
+        per_sample = torch.tensor([0.5, 1.25, -2.0, 4.0, 0.75], dtype=torch.float64)
+        c_out = torch.arange(5 * 4, dtype=torch.float32).reshape(5, 1, 2, 2) / 7.0
+        bounds, vals = r["ragged"]
+        assert abs(vals["D"] - float(per_sample.mean())) < 1e-6  # (fp32 per-rank means)
+        assert abs(vals["D1_fake"] - float(c_out.double().mean())) < 1e-6
+        # second backward after zero_grad(set_to_none): still averaged over ranks ((1+2)/2 + 1)
+        g, owned = r["zero_grad"]
+        assert owned and torch.equal(g, torch.full((4,), 2.5))
+    assert r0["ragged"][0] == (0, 3) and r1["ragged"][0] == (3, 5)

@@ -72,3 +72,34 @@ def test_captured_step_is_bit_identical(dtype, ngf, loss_type):
     replay()
     assert not _same(_state(eager), _state(graphed))
     assert float(graphed.optim_G.state[next(graphed.G1.parameters())]["step"]) == 7.0
+
+
+def test_general_path_step_after_replays():
+    """Replays advance only the device step counters; an eager step that then takes the optimiser's general path
+    (here: every packed operand re-registered, ops.invalidate_packs) must continue from the device count, and so
+    must the replay after it (the host count used to be stale there)."""
+    from stcgan_amd import ops
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    B = 2
+    x = torch.rand((B, 3, 256, 256), generator=g, device="cuda") * 2 - 1
+    m = (torch.rand((B, 1, 256, 256), generator=g, device="cuda") < 0.5).float() * 2 - 1
+    y = torch.rand((B, 3, 256, 256), generator=g, device="cuda") * 2 - 1
+    eager = _trainer("bf16", 16, "normal")
+    graphed = _trainer("bf16", 16, "normal")
+    replay = graphed.capture(x, m, y, warmup=1)  # 3 eager steps inside
+    for _ in range(3):
+        eager.train_step(x, m, y)
+    for _ in range(2):  # no sync_steps between the replays and the eager step below
+        eager.train_step(x, m, y)
+        replay()
+    ops.invalidate_packs()  # both trainers' next step: the general Adam path
+    eager.train_step(x, m, y)
+    graphed.train_step(x, m, y)
+    bad = _same(_state(eager), _state(graphed))
+    assert not bad, bad[:8]
+    eager.train_step(x, m, y)
+    replay()
+    bad = _same(_state(eager), _state(graphed))
+    assert not bad, bad[:8]
+    assert float(graphed.optim_D.state[next(graphed.D1.parameters())]["step"]) == 7.0
