@@ -173,6 +173,26 @@ def make_trainer(ngf, dtype, local):
     return STCGAN(a)
 
 
+def alg_bytes(name, desc):
+    """Algorithmic HBM bytes of one GEMM-family launch (bf16 operands): the input, the output and the weights once
+    (weight gradients: both operands once + the fp32 gradient; the fused BatchNorm-backward epilogue also reads
+    the BN input and the second gradient, output-sized), from the timer's description (ops._time_entry)."""
+    import re
+    g = {k: int(v) for k, v in re.findall(r"(B|grid|cin|cout|P=|R|Cg)(\d+)", desc.replace("x", " x"))}
+    if desc.startswith("wgrad"):
+        P, R, C = g["P="], g["R"], g["Cg"]
+        return 2 * P * R + 2 * (4 if " s2 " in desc else 1) * P * C + 4 * 16 * R * C
+    gh, gw = (int(v) for v in re.search(r"grid(\d+)x(\d+)", desc).groups())
+    B, cin, cout = g["B"], g["cin"], g["cout"]
+    kind = desc.split()[0]
+    outs = {"conv_s2": (B * 4 * gh * gw, B * gh * gw), "conv_s1": (B * (gh + 1) * (gw + 1), B * gh * gw),
+            "s1_dgrad": (B * (gh - 1) * (gw - 1), B * gh * gw), "convT": (B * gh * gw, B * 4 * gh * gw)}[kind]
+    byt = 2 * outs[0] * cin + 2 * outs[1] * cout + 2 * 16 * cin * cout
+    if "true" in name.split("<", 1)[-1]:  # (BNB: the BN input and the other gradient)
+        byt += 2 * 2 * outs[1] * cout
+    return byt
+
+
 def roofline_of_step(tr, x, m, y, args, B, s):
     """Dominant kernel of one (untimed) train step by summed device time, and the north-star set."""
     import torch
@@ -192,10 +212,11 @@ def roofline_of_step(tr, x, m, y, args, B, s):
         per, shapes = {}, {}
         for name, _single, fl, e0, e1, desc in launches:
             ms = e0.elapsed_time(e1)
-            a = per.setdefault(name, [0, 0.0, 0.0])
+            a = per.setdefault(name, [0, 0.0, 0.0, 0.0])
             a[0] += 1
             a[1] += fl
             a[2] += ms
+            a[3] += alg_bytes(name, desc)
             shapes.setdefault(name, []).append((round(ms * 1e3, 1), desc))
         whole = {}  # weight-gradient calls: main kernel + split-pixel reduction
         for name, c0, c1 in calls:
@@ -206,12 +227,20 @@ def roofline_of_step(tr, x, m, y, args, B, s):
     launches, per, shapes = timed_step(True)
     whole_single = dict(timed_step.whole)
     dom = max(per, key=lambda k: per[k][2])
-    n_dom, fl_dom, ms_dom = per[dom]
+    n_dom, fl_dom, ms_dom, by_dom = per[dom]
     peak = PEAK_TFLOPS[args.dtype]
     achieved = fl_dom / (ms_dom * 1e-3) / 1e12
     _, per_situ, _ = timed_step(False)
-    n_s, fl_s, ms_s = per_situ.get(dom, (n_dom, fl_dom, float("nan")))
+    n_s, fl_s, ms_s, _ = per_situ.get(dom, (n_dom, fl_dom, float("nan"), 0.0))
     achieved_situ = fl_s / (ms_s * 1e-3) / 1e12
+    # the largest consumer of the bench's own overlapped step (in situ, side streams on) may be another kernel
+    dom_situ = max(per_situ, key=lambda k: per_situ[k][2])
+    nd, fld, msd, _ = per_situ[dom_situ]
+    situ_dominant = {"kernel": dom_situ, "launches": nd, "gflop": round(fld / 1e9, 2), "ms": round(msd, 3),
+                     "avg_us": round(msd / nd * 1e3, 1), "achieved": round(fld / (msd * 1e-3) / 1e12, 2),
+                     "frac": round(fld / (msd * 1e-3) / 1e12 / peak, 4),
+                     "single_stream_avg_us": round(per[dom_situ][2] / per[dom_situ][0] * 1e3, 1) if dom_situ in per
+                     else None}
     # the north-star kernel set: one train-mode G1+G2 forward (770.95 GFLOP at bs=32, 256^2), HIP events;
     # in the bench dtype and in the other one (the reference computes in fp32)
     flops = gen_fwd_flops(3, 1, args.ngf, B, s, s) + gen_fwd_flops(4, 3, args.ngf, B, s, s)
@@ -243,7 +272,9 @@ def roofline_of_step(tr, x, m, y, args, B, s):
     top = sorted(per.items(), key=lambda kv: -kv[1][2])[:10]
     # HBM traffic per launch of the dominant kernel: rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; gfx950
     # FETCH_SIZE x2 correction) over the bench command, committed under profiles/<round>/pmc_traffic.json
-    traffic, traffic_src = None, None
+    # (this round's profile: profiles/<round>/pmc_traffic.json, made by scripts/profile_round.sh from the bench
+    # command itself; the newest round that profiled this kernel)
+    traffic, traffic_src, mfma_busy = None, None, None
     import glob
     for fpath in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
         try:
@@ -253,8 +284,11 @@ def roofline_of_step(tr, x, m, y, args, B, s):
         hit = [v for k, v in tab.items() if dom in k]
         if hit and args.dtype == "bf16":
             traffic = int(hit[0]["hbm_bytes_per_launch"])
-            traffic_src = os.path.relpath(fpath, ROOT) + f" (mean over {hit[0]['launches']} launches, all shapes)"
+            mfma_busy = hit[0].get("mfma_busy")
+            traffic_src = (f"{os.path.relpath(fpath, ROOT)} (round {os.path.basename(os.path.dirname(fpath))}; mean "
+                           f"over {hit[0]['launches']} launches of the bench command, all shapes)")
             break
+    alg_per_launch = by_dom / n_dom
     conv_ms = sum(v[2] for v in per.values())
     conv_gf = sum(v[1] for v in per.values()) / 1e9
     incl = None  # the dominant kernel with its split-pixel reduction charged to it (weight gradients)
@@ -267,6 +301,10 @@ def roofline_of_step(tr, x, m, y, args, B, s):
             "frac": round(achieved / peak, 4), "with_reduction": incl,
             "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_src": traffic_src,
+            "algorithmic_bytes_per_launch": int(alg_per_launch),
+            "traffic_over_algorithmic": round(traffic / alg_per_launch, 3) if traffic else None,
+            "mfma_busy": mfma_busy,
+            "dominant_in_situ": situ_dominant,
             "frac_mode": "single-stream step (each launch alone); frac_in_situ: the same kernel in the bench's "
                          "overlapped step (side-stream networks and weight gradients on)",
             "achieved_in_situ": round(achieved_situ, 2), "frac_in_situ": round(achieved_situ / peak, 4),
@@ -275,6 +313,7 @@ def roofline_of_step(tr, x, m, y, args, B, s):
                       f"in situ (HIP events around the main kernel)",
             "dominant_launches_us": shapes[dom][:40],
             "per_kernel": {k: {"launches": v[0], "gflop": round(v[1] / 1e9, 2), "ms": round(v[2], 3),
+                               "alg_mb_per_launch": round(v[3] / v[0] / 1e6, 2),
                                "avg_us": round(v[2] / v[0] * 1e3, 1),
                                "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2)} for k, v in top},
             "gemm_kernels_all": {"launches": len(launches), "gflop": round(conv_gf, 2), "ms": round(conv_ms, 3),

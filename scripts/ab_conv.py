@@ -1,0 +1,60 @@
+"""A/B timer of the conv-s2 GEMMs of one train step (bs 32, 256x256, bf16): the automatic plan (the halo kernel,
+csrc/halo_bf16.hip, where it applies) against the automatic im2col plan (force {-2, 0}), interleaved rounds in
+one process, HIP events over 20 launches each; prints us / TFLOP/s per shape and the relative output difference."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "shadow-removal-istd_amd"))
+
+import torch  # noqa: E402
+
+from stcgan_amd import _lib as L  # noqa: E402
+from stcgan_amd import ops  # noqa: E402
+
+BF = torch.bfloat16
+SHAPES = [  # (grid, cin, cout, what)
+    (64, 64, 128, "e2 / D c2 fwd"),
+    (32, 128, 256, "e3 / D c3 fwd"),
+    (64, 64, 256, "d2 dgrad (ConvT 256->64)"),
+    (32, 128, 512, "d3 dgrad (ConvT 512->128)"),
+    (16, 256, 1024, "d4 dgrad (ConvT 1024->256)"),
+]
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    B = 32
+    g = torch.Generator(device=dev).manual_seed(0)
+    for gh, cin, cout, what in SHAPES:
+        x = (torch.randn((B, 2 * gh, 2 * gh, cin), generator=g, device=dev)).to(BF)
+        w = torch.randn((cout, cin, 4, 4), generator=g, device=dev) * 0.05
+        wp = ops.pack(L.PACK_CONV_FWD, w, cout, cin, BF)
+        ys = {}
+        times = {"halo": [], "im2col": []}
+        plans = {}
+        for rnd in range(5):
+            for name, force in (("halo", None), ("im2col", (-2, 0))):
+                y = torch.empty((B, gh, gh, cout), device=dev, dtype=BF)
+                plans[name] = ops.conv_query(L.CONV_S2, B, gh, gh, cin, cout, BF, force=force)[2]
+                ops.conv_stats(L.CONV_S2, B, L.nhwc_view(x), cin, wp, cout, L.nhwc_view(y), BF, force=force)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(20):
+                    ops.conv_stats(L.CONV_S2, B, L.nhwc_view(x), cin, wp, cout, L.nhwc_view(y), BF, force=force)
+                e1.record()
+                e1.synchronize()
+                times[name].append(e0.elapsed_time(e1) / 20 * 1e3)
+                ys[name] = y
+        fl = 2.0 * B * gh * gh * cout * 16 * cin
+        d = float((ys["halo"].float() - ys["im2col"].float()).abs().max() / ys["im2col"].float().abs().max())
+        line = f"{what:28s} grid{gh} cin{cin} cout{cout}:"
+        for name in ("halo", "im2col"):
+            t = sorted(times[name])
+            line += f"  {name} plan{list(plans[name])} med {t[2]:.1f} us min {t[0]:.1f} ({fl / t[0] / 1e6:.0f} TF)"
+        print(line + f"  rel diff {d:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

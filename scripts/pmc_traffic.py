@@ -1,11 +1,13 @@
 """Per-launch HBM traffic of each kernel from rocprofv3 --pmc CSV passes.
 
-usage: python scripts/pmc_traffic.py <dir with FETCH pass> <dir with WRITE pass> [out.json]
+usage: python scripts/pmc_traffic.py <dir with FETCH pass> <dir with WRITE pass> [out.json [dir with MFMA pass]]
 
 Reads every *counter_collection.csv under the two directories, sums each counter per
 dispatch, and averages per kernel name.  gfx950 correction (MI355X_MICROARCH.md §HBM):
 FETCH_SIZE (KiB) reports half the bytes of a wide coalesced streaming read, so
 read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE (KiB) is exact for 16-B stores.
+The optional MFMA pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE) gives each kernel's MFMA-busy fraction:
+busy SIMD-cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), averaged over its dispatches.
 """
 import csv
 import glob
@@ -45,7 +47,15 @@ def main():
         wr = a["write_kib"] * 1024 / max(a["n_write"], 1)
         out[k] = {"launches": a["n_fetch"], "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                   "hbm_bytes_per_launch": rd + wr}
-    for k, v in list(out.items())[:25]:
+    if len(sys.argv) > 4:
+        mf = load(sys.argv[4])
+        acc = defaultdict(list)
+        for (k, _), c in mf.items():
+            if c.get("GRBM_GUI_ACTIVE", 0) > 0 and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+                acc[k].append(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024))
+        for k, v in acc.items():
+            out.setdefault(k, {})["mfma_busy"] = round(sum(v) / len(v), 4)
+    for k, v in [kv for kv in out.items() if "launches" in kv[1]][:25]:
         print(f"{v['launches']:5d}  rd {v['read_bytes_per_launch'] / 1e6:9.2f} MB  wr {v['write_bytes_per_launch'] / 1e6:9.2f} MB  {k[:110]}")
     if len(sys.argv) > 3:
         with open(sys.argv[3], "w") as fh:

@@ -182,6 +182,10 @@ _BF16_TILES = [(128, 128, 2, 2, 2, 64), (256, 128, 2, 2, 2, 64), (128, 64, 2, 2,
                (128, 64, 2, 2, 2, 64, 2), (128, 256, 2, 4, 2, 64, 2)]
 
 
+# plan config of the conv-s2 halo kernel (stc_conv_fwd_query plan[4]; force_plan (HALO_CFG, 1) forces it)
+HALO_CFG = 100
+
+
 def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
     """(kernel symbol as rocprof shows it, launches-a-single-kernel) of one conv call
     (bnb: the input-gradient form with the BatchNorm-backward reduction fused in)."""
@@ -193,6 +197,8 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
             nb = 2 if (kind == L.CONVT_S2 and 4 * cout > 16) else 1
             return f"narrow_halo_kernel<{geom}, {nb}, 8>", ws == 0
         return "narrow_tiled_kernel", True
+    if cfg == HALO_CFG:  # conv-s2 with the LDS-resident input halo (csrc/halo_bf16.hip)
+        return f"halo_conv_s2_kernel<{gw}, {str(bnb).lower()}>", True
     if cfg >= 0:
         t = _BF16_TILES[cfg]
         if len(t) > 6:  # loader-wave blocks

@@ -1,0 +1,172 @@
+"""The conv-s2 halo kernel (csrc/halo_bf16.hip) against torch fp32 references and the im2col tile.
+
+Conv2d k4 s2 p1 (STCGAN/networks.py:104-105, 167-169, 176-178) and the ConvTranspose2d input gradient (its
+geometry, networks.py:112-128 backward) with the A operand staged as input rows in LDS.  Checked: every output
+width the kernel takes (16, 32, 64 columns: 16, 8 and 4 output rows per 256-row tile), several 64-channel
+chunks, ragged N, channel-offset input and output views (the concat buffers), bias, the BatchNorm statistics
+and the fused BatchNorm-backward sums of the epilogue, the automatic plan at the train step's sizes.
+Operands are bf16-exact, so the references differ by fp32 summation order and the final bf16 rounding only:
+1e-2 * max|ref| on outputs (as tests/test_gpu_igemm_bf16.py), 2e-3 on the statistics.  Against the im2col tile
+(a different but fixed K order) the outputs agree to the same bound.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from stcgan_amd import _lib as L
+from stcgan_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+HALO = (ops.HALO_CFG, 1)
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def rnd(*shape, seed=0, scale=1.0, dev="cpu"):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    return torch.randn(shape, generator=g, device=dev) * scale
+
+
+def q(t):
+    return t.to(BF).float()
+
+
+def run(B, x, w, Cin, Cout, GH, GW, force, co_in=0, extra_in=0, co=0, extra_c=0, bias=None):
+    """stc_conv_fwd_ex (with statistics) of NCHW fp32 x; returns (y NCHW fp32, mean, var, plan)."""
+    xb = torch.zeros((B, 2 * GH, 2 * GW, Cin + extra_in), device=DEV, dtype=BF)
+    xb[..., co_in:co_in + Cin] = nhwc(x).to(DEV, BF)
+    wp = ops.pack(L.PACK_CONV_FWD, w.to(DEV), Cout, Cin, BF)
+    y = torch.full((B, GH, GW, Cout + extra_c), float("nan"), device=DEV, dtype=BF)
+    part, nch = ops.conv_stats(L.CONV_S2, B, L.nhwc_view(xb, co_in), Cin, wp, Cout, L.nhwc_view(y, co), BF,
+                               bias=None if bias is None else bias.to(DEV), force=force)
+    _, nq, plan = ops.conv_query(L.CONV_S2, B, GH, GW, Cin, Cout, BF, force=force)
+    assert nq == nch
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV)
+    t = torch.empty((2, Cout), device=DEV)
+    mean, rstd = ops.bn_finalize_part(part, nch, Cout, bn, t[0], t[1])
+    var = 1.0 / rstd.double() ** 2 - bn.eps
+    torch.cuda.synchronize()
+    return nchw(y[..., co:co + Cout].float()), mean.double(), var, plan
+
+
+def check(got, ref, mean, var, what, tol=1e-2):
+    scale = float(ref.abs().max()) + 1e-12
+    err = float((got - ref).abs().max())
+    assert err <= tol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+    rm = ref.double().mean(dim=(0, 2, 3))
+    rv = ref.double().var(dim=(0, 2, 3), unbiased=False)
+    sd = float(rv.max().sqrt()) + 1e-12
+    assert float((mean - rm).abs().max()) <= 2e-3 * sd, f"{what}: mean err {float((mean - rm).abs().max()):.3e}"
+    assert float(((var - rv).abs() / (rv + 1e-12)).max()) <= 8e-3, f"{what}: var err"
+
+
+CASES = [  # B, Cin, Cout, GH, GW
+    (2, 64, 128, 8, 64),     # 4 output rows per tile (e2 / D layer 2 width), two tiles per image
+    (1, 128, 256, 16, 32),   # 8 rows per tile, two 64-channel chunks, two N tiles (e3 / D layer 3)
+    (1, 256, 512, 16, 16),   # 16 rows per tile (a whole 16x16 image), 4 chunks (e4)
+    (3, 64, 96, 4, 64),      # ragged N (96 of a 128 tile), 3 images
+    (1, 192, 40, 8, 32),     # 3 chunks, N = 40
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+def test_halo_conv_s2(case):
+    B, Cin, Cout, GH, GW = case
+    x = q(rnd(B, Cin, 2 * GH, 2 * GW, seed=1, dev=DEV))
+    w = q(rnd(Cout, Cin, 4, 4, seed=2, scale=0.05, dev=DEV))
+    ref = F.conv2d(x, w, None, 2, 1)
+    y, mean, var, plan = run(B, x, w, Cin, Cout, GH, GW, HALO)
+    assert plan[4] == ops.HALO_CFG and plan[0] == 256
+    check(y, ref, mean, var, f"halo {case}")
+    # the im2col tile on the same operands: equal up to the summation order
+    y2, _, _, plan2 = run(B, x, w, Cin, Cout, GH, GW, (0, 1))
+    assert plan2[4] == 0
+    scale = float(ref.abs().max())
+    assert float((y - y2).abs().max()) <= 1e-2 * scale
+
+
+def test_halo_views_and_bias():
+    """Input from a channel slice of a wider buffer (the concat buffers), output into the second half of one,
+    with a bias epilogue."""
+    B, Cin, Cout, GH, GW = 2, 64, 128, 8, 32
+    x = q(rnd(B, Cin, 2 * GH, 2 * GW, seed=3, dev=DEV))
+    w = q(rnd(Cout, Cin, 4, 4, seed=4, scale=0.05, dev=DEV))
+    b = rnd(Cout, seed=5, dev=DEV)
+    ref = F.conv2d(x, w, b, 2, 1)
+    y, mean, var, _ = run(B, x, w, Cin, Cout, GH, GW, HALO, co_in=64, extra_in=64, co=64, extra_c=64, bias=b)
+    check(y, ref, mean, var, "halo views+bias")
+
+
+def test_halo_plan_automatic_at_train_sizes():
+    """The train step's conv-s2 layers with 64-channel chunks and enough blocks take the halo kernel; the
+    others keep their im2col plans."""
+    for (gh, cin, cout) in ((64, 64, 128), (32, 128, 256), (64, 64, 256), (32, 128, 512), (16, 256, 1024)):
+        assert ops.conv_query(L.CONV_S2, 32, gh, gh, cin, cout, BF)[2][4] == ops.HALO_CFG, (gh, cin, cout)
+    for (gh, cin, cout) in ((128, 8, 64), (16, 256, 512), (8, 512, 512)):
+        assert ops.conv_query(L.CONV_S2, 32, gh, gh, cin, cout, BF)[2][4] != ops.HALO_CFG, (gh, cin, cout)
+
+
+def test_halo_full_size_e2():
+    """G's second down conv at the bench size (bs 32, 128x128x64 -> 64x64x128) on the automatic plan, vs the
+    fp32 convolution of the same bf16 operands."""
+    B, Cin, Cout, GH = 32, 64, 128, 64
+    x = q(rnd(B, Cin, 2 * GH, 2 * GH, seed=6, dev=DEV))
+    w = q(rnd(Cout, Cin, 4, 4, seed=7, scale=0.05, dev=DEV))
+    ref = F.conv2d(x, w, None, 2, 1)
+    y, mean, var, plan = run(B, x, w, Cin, Cout, GH, GH, None)
+    assert plan[4] == ops.HALO_CFG
+    check(y, ref, mean, var, "halo e2 full size")
+
+
+class _BNT:
+    def __init__(self, C, seed):
+        g = torch.Generator().manual_seed(seed)
+        self.scale = (torch.rand(C, generator=g) + 0.5).to(DEV)
+        self.shift = (torch.randn(C, generator=g) * 0.2).to(DEV)
+        self.mean = (torch.randn(C, generator=g) * 0.1).to(DEV)
+        self.rstd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+        self.gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+
+
+@pytest.mark.parametrize("case", [(8, 64, 256, 64, 64, 128, 128), (32, 256, 1024, 16, 16, 512, 512)],
+                         ids=["d2_dgrad", "d4_dgrad"])
+def test_halo_conv_bn_backward(case):
+    """The ConvT input gradient at its train-step size (conv-s2 geometry, automatic plan = halo) with the
+    BatchNorm-backward reduction fused into the epilogue: output vs torch, sums vs the separate reduction."""
+    B, Cin, Cout, GH, GW, C, ch_off = case
+    assert ops.conv_query(L.CONV_S2, B, GH, GW, Cin, Cout, BF)[2][4] == ops.HALO_CFG
+    wt = q(rnd(Cout, Cin, 4, 4, seed=51, scale=0.05, dev=DEV))
+    w = ops.pack(L.PACK_CONV_FWD, wt, Cout, Cin, BF)
+    dy = q(rnd(B, Cin, 2 * GH, 2 * GW, seed=52, scale=0.5, dev=DEV))
+    dyb = nhwc(dy).to(BF)
+    x = torch.randn((B, GH, GW, C), generator=torch.Generator(device=DEV).manual_seed(53), device=DEV).to(BF)
+    go = torch.randn((B, GH, GW, C), generator=torch.Generator(device=DEV).manual_seed(54), device=DEV).to(BF)
+    bn = _BNT(C, 55)
+    st = (bn.scale, bn.shift, bn.mean, bn.rstd)
+    out1 = torch.zeros((B, GH, GW, Cout), device=DEV, dtype=BF)
+    dx1 = torch.empty((B, GH, GW, C), device=DEV, dtype=BF)
+    dg1, db1 = ops.conv_bn_backward(L.CONV_S2, B, L.nhwc_view(dyb), Cin, w, Cout, L.nhwc_view(out1), BF,
+                                    bn_x=L.nhwc_view(x), C=C, bn_state=st, gamma=bn.gamma, s_self=0.2, ch_off=ch_off,
+                                    g_other=L.nhwc_view(go), s_other=0.0, dxv=L.nhwc_view(dx1))
+    out2 = torch.zeros((B, GH, GW, Cout), device=DEV, dtype=BF)
+    ops.conv(L.CONV_S2, B, L.nhwc_view(dyb), Cin, w, Cout, L.nhwc_view(out2), BF)
+    dx2 = torch.empty((B, GH, GW, C), device=DEV, dtype=BF)
+    dg2, db2 = ops.bn_backward(B, L.nhwc_view(x), C, BF, L.nhwc_view(dx2), g1=L.nhwc_view(out2, ch_off), s1=0.2,
+                               g2=L.nhwc_view(go), s2=0.0, bn_state=(bn.scale, bn.shift, bn.mean, bn.rstd, bn.gamma))
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
+    ref = F.conv2d(dy, wt, None, 2, 1)
+    assert float((nchw(out1.float()) - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+    for a, b_, nm in ((dg1, dg2, "dgamma"), (db1, db2, "dbeta")):
+        err = float((a - b_).abs().max())
+        assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm} {case}: {err:.3e}"
+    err = float((dx1.float() - dx2.float()).abs().max())
+    assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx {case}: {err:.3e}"
