@@ -3,56 +3,73 @@
 // The same problem as igemm_bf16.hip's conv-s2 geometry -- the forward of STCGAN/networks.py:104-105 (U-Net
 // down convs) / :167-169,176-178 (PatchGAN convs), and the input gradient of the ConvTranspose2d layers
 // (:112-114,119-121,126-128), which has this geometry -- but the im2col tile there stages each input pixel once
-// per tap that reads it (4 of the 16 taps of a stride-2 4x4 kernel, per 128-row tile), so the L2 -> LDS stream
-// is half A bytes.  Here a block owns TH whole output rows of one image (BM = TH * GW = 256 GEMM rows) and
-// stages, per input-channel chunk of 64, kernel row ky and input-column parity, the TH input rows that this
-// (ky, parity) reads -- every staged pixel serves two taps (kx and kx + 2):
+// per tap that reads it (4 of the 16 taps of a stride-2 4x4 kernel, per 128-row tile), so half of its L2 -> LDS
+// stream is A bytes.  Here a block owns TH whole output rows of one image (BM = TH * GW = 256 GEMM rows) and
+// stages, per 32 input channels, kernel row ky and input-column parity, the TH input rows that this (ky, parity)
+// reads -- every staged pixel serves two taps (kx and kx + 2):
 //
 //   stage (ky, parity q) at LDS position P = r * GW + c holds input pixel (2 * (oy0 + r) + ky - 1, 2 * c + q);
 //   tap kx of output (r, ox) reads position P = r * GW + ox + d with
 //     kx = 0: q = 1, d = -1 (zero at ox = 0)       kx = 1: q = 0, d = 0
 //     kx = 2: q = 1, d = 0                          kx = 3: q = 0, d = +1 (zero at ox = GW - 1)
 //
-// so one stage = exactly BM pixels x 128 B in the same [row][128 B] XOR-swizzled image as the im2col A tile
-// (position = GEMM row; the fragment of 16 consecutive rows shifted by d stays conflict-free), filled by
-// LDS-DMA (input rows outside the image: an out-of-range offset, read as zeros).  The two edge cases read a
-// zero pixel instead (a per-lane address redirect on the fragments that start / end an output row).
-// A bytes per block: 8 stages x 32 KiB per 64 channels against 16 x 32 KiB (im2col, 128-row tile, per 128
-// rows): 4x fewer A bytes per GEMM row.  B (the packed weights, [N][16 taps][Cin]) is streamed per tap as in
-// igemm_bf16.hip.
+// so a stage is exactly BM pixels x 64 B (position = GEMM row), filled by LDS-DMA (input rows outside the image:
+// an out-of-range offset, read as zeros); the two edge cases zero the fragment of the lane that addressed the
+// neighbouring row's pixel.  A bytes per GEMM row and 32 channels: 8 stages x 64 B against 16 x 64 B for the
+// im2col tile -- and B (the packed weights [N][16 taps][Cin]) streams per tap as there.
 //
-// Pipeline: a super-step = one A stage (4 LDS-DMA pieces per wave) + the two B K-steps of its taps (2 x 2
-// pieces), 64 KiB; a two-slot ring (the next super-step's DMA lands under the current one's 64 MFMAs per wave),
-// one barrier per super-step; 8 waves (4 x 2) of 64 x 64, v_mfma_f32_16x16x32_bf16.  K order: chunk -> ky ->
-// parity (odd, even) -> tap (0, 2 | 1, 3): a fixed order, but not the im2col tile's tap-major one, so the fp32
-// sums differ from it by rounding only.  Epilogue: igemm_bf16.hpp (bias, BatchNorm statistics, the fused
-// BatchNorm-backward sums, 16-byte NHWC stores).
+// Block: 4 waves (2 x 2) of 128 x 64 (v_mfma_f32_16x16x32_bf16, 32 accumulator tiles per wave), 80 KiB of LDS,
+// so two blocks share a CU and one block's stage waits, epilogue and prologue overlap the other's MFMAs.  LDS
+// rows are 64 B with the 16-byte chunk XOR-ed by 2 * ((row >> 2) & 1): every ds_read_b128 lane group of a 16-row
+// fragment is conflict-free for ANY first row (the d-shifted A fragments start at odd rows).
+// Pipeline per super-step (one A stage + the two B K-steps of its taps, 64 MFMAs per wave): A is loaded two
+// super-steps ahead into a 3-slot ring (first touch comes from HBM / the memory-side cache), B one ahead into a
+// 2-pair ring (L2-resident); the 8 LDS-DMA pieces a wave issues per super-step are spread one per 8 MFMAs; one
+// barrier per super-step.  K order: 64-channel chunk -> ky -> parity (odd, even) -> 32-channel half -> tap
+// (0, 2 | 1, 3): fixed, but not the im2col tile's tap-major order, so the fp32 sums differ from it by rounding.
+// Epilogue: igemm_bf16.hpp (bias, BatchNorm statistics, the fused BatchNorm-backward sums, 16-byte NHWC stores).
 #include <type_traits>
 
 #include "igemm_bf16.hpp"
 
-#ifndef STC_HALO_IL
-#define STC_HALO_IL 1
-#endif
-
 namespace stc {
 
-constexpr int HB_BM = 256, HB_BN = 128, HB_WM = 4, HB_WN = 2, HB_NW = HB_WM * HB_WN;
-constexpr int HB_A = HB_BM * 128;             // A stage: BM pixels x 64 channels
-constexpr int HB_B = HB_BN * 128;             // one B K-step: BN rows x 64 channels
-// LDS: [B pair 0][A slot 0][A slot 1][A slot 2][B pair 1] = 160 KiB: one block (8 waves) per CU.  (The masked edge
-// lanes of A slot 0 / 2 address one pixel before / after it: inside the neighbouring B pair, never outside LDS.)
-constexpr int HB_A0 = 2 * HB_B;
-constexpr int HB_LDS = 4 * HB_B + 3 * HB_A;
-static_assert(HB_LDS <= 163840, "LDS");
+constexpr int HB_BM = 256, HB_BN = 128;  // block tile: 256 GEMM rows (whole output rows) x 128 output channels
 
-template <int GW, bool BNB>
-__global__ void __launch_bounds__(64 * HB_NW) halo_conv_s2_kernel(const GParams p) {
-  constexpr int BM = HB_BM, BN = HB_BN, WN = HB_WN, NW = HB_NW;
-  constexpr int FM = BM / HB_WM / 16, FN = BN / HB_WN / 16;  // 4 x 4 fragments of 16 x 16 per wave
-  constexpr int AG = BM / (8 * NW), BG = BN / (8 * NW);      // DMA pieces per wave: 4 (A stage), 2 (B K-step)
+// Two block shapes over one K loop (RB = bytes per LDS row = 2 x the channels of a stage):
+//   RB = 64,  2 x 2 waves of 128 x 64, 80 KiB LDS: two blocks per CU (the default when the grid has >= 512 blocks)
+//   RB = 128, 4 x 2 waves of 64 x 64, 160 KiB LDS: one 8-wave block per CU (grids of 256-511 blocks, where two
+//             4-wave blocks per CU would leave half the CUs empty)
+// LDS: [B pair 0][A slot 0][A slot 1][A slot 2][B pair 1].  The masked edge lanes of A slot 0 / 2 address one pixel
+// before / after it: inside the neighbouring B pair, never outside the block's LDS.
+template <int RB> struct HaloGeom {
+  static constexpr int A = HB_BM * RB, B = HB_BN * RB;
+  static constexpr int A0 = 2 * B, B1 = A0 + 3 * A, LDS = 4 * B + 3 * A;
+  static constexpr int CH = RB / 16;        // 16-byte chunks per row
+  static constexpr int PR = 1024 / RB;      // rows per 1 KiB DMA piece
+};
+static_assert(HaloGeom<64>::LDS <= 81920 && HaloGeom<128>::LDS <= 163840, "LDS");
+
+// chunk c of LDS row P sits in slot c ^ swz(P): RB = 128: P & 7; RB = 64: 2 * ((P >> 2) & 1) -- for both, every
+// ds_read_b128 lane group of a 16-row fragment is conflict-free for ANY first row (the d-shifted A fragments)
+template <int RB> __device__ __forceinline__ int hswz(int row) {
+  if constexpr (RB == 128) return row & 7;
+  else return ((row >> 2) & 1) << 1;
+}
+
+template <int GW, bool BNB, int RB, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kernel(const GParams p) {
+  using G = HaloGeom<RB>;
+  constexpr int BM = HB_BM, BN = HB_BN, NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;                  // wave tile: 128 x 64 / 64 x 64
+  constexpr int FM = TM / 16, FN = TN / 16;                  // fragments of 16 x 16
+  constexpr int KK = RB / 64;                                // 32-deep MFMA steps per K-step
+  constexpr int AG = BM / (G::PR * NW), BG = BN / (G::PR * NW);  // DMA pieces per wave: A stage / B K-step
+  constexpr int HALVES = 128 / RB;                           // stages per 64-channel chunk, ky and parity
   constexpr int TH = BM / GW;
-  static_assert(GW >= 16 && GW <= 64 && BM % GW == 0, "whole output rows per tile, 16-row fragments inside a row");
+  static_assert(GW % 16 == 0 && BM % GW == 0 && TM % GW == 0 && FN == 4 && FM % 2 == 0,
+                "whole output rows per tile and per wave, 16-row fragments inside an output row");
+  static_assert(2 * BG + AG == KK * FM, "one DMA piece per 8 MFMAs");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -74,14 +91,14 @@ __global__ void __launch_bounds__(64 * HB_NW) halo_conv_s2_kernel(const GParams 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, (short)0, (int)p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, (int)p.b_bytes, 0x00020000);
 
-  // ---- DMA lane roles: lane -> (pixel / row prow of its 8-row piece, LDS slot lane & 7 <- source chunk)
-  const int prow = lane >> 3;
-  const int schunk = (lane & 7) ^ prow;  // (position & 7 == prow: pieces are 8-row aligned)
+  // ---- DMA lane roles: lane -> (row prow of its piece, LDS slot lane % CH <- source chunk)
+  const int prow = lane / G::CH;
+  const int schunk = (lane % G::CH) ^ hswz<RB>(prow);  // (pieces are PR-row aligned: hswz(position) == hswz(prow))
   unsigned a_off[AG];
   unsigned top = 0, bot = 0;  // pieces whose output row is the image's first / last (ky = 0 / 3 read padding)
 #pragma unroll
   for (int g = 0; g < AG; ++g) {
-    const int pos = (wave * AG + g) * 8 + prow;
+    const int pos = (wave * AG + g) * G::PR + prow;
     const int r = pos / GW, c = pos % GW;
     const int oy = oy0 + r;
     a_off[g] = (unsigned)(img * p.a_bs + p.a_co) + (unsigned)(2 * oy) * (unsigned)p.a_rs + (unsigned)(2 * c) * (unsigned)p.a_ps +
@@ -92,34 +109,51 @@ __global__ void __launch_bounds__(64 * HB_NW) halo_conv_s2_kernel(const GParams 
   unsigned b_off[BG];
 #pragma unroll
   for (int h = 0; h < BG; ++h) {
-    const int n = n0 + (wave * BG + h) * 8 + prow;
+    const int n = n0 + (wave * BG + h) * G::PR + prow;
     b_off[h] = n < p.N ? (unsigned)(n * p.K + schunk * 8) : OOB;
   }
   const int cin = p.cin;
 
-  // super-step ss: chunk ss >> 3, ky = (ss >> 1) & 3, parity odd (taps 0, 2) for even ss, even (taps 1, 3) for
-  // odd ss.  Its A stage goes to A slot ss % 3 (issued two super-steps ahead: the input rows come from HBM / the
-  // memory-side cache on first touch), its two B K-steps to B pair ss & 1 (one super-step ahead: the weights are
-  // L2-resident).
+  // Super-step ss = ((chunk * 4 + ky) * 2 + q) * HALVES + half: parity q = 0 odd (taps 0, 2) / 1 even (taps 1, 3),
+  // half = the 32-channel half of the 64-channel chunk (RB = 64: the two halves of a pixel's 128-byte line back to
+  // back).  Its A stage goes to A slot ss % 3, its two B K-steps to B pair ss & 1.
+  auto ss_terms = [&](int ss, int& half, int& odd, int& ky, int& ch) {
+    half = HALVES == 2 ? (ss & 1) : 0;
+    const int t = HALVES == 2 ? ss >> 1 : ss;
+    odd = (t & 1) ^ 1;
+    ky = (t >> 1) & 3;
+    ch = t >> 3;
+  };
+  auto a_terms = [&](int ss, unsigned& delta, unsigned& pen) {
+    int half, odd, ky, ch;
+    ss_terms(ss, half, odd, ky, ch);
+    delta = (unsigned)((ky - 1) * p.a_rs + odd * p.a_ps + ch * 64 + half * 32);
+    pen = ky == 0 ? top : (ky == 3 ? bot : 0u);
+  };
+  auto b_k0 = [&](int ss, int j) {
+    int half, odd, ky, ch;
+    ss_terms(ss, half, odd, ky, ch);
+    const int kx = odd ? 2 * j : 2 * j + 1;
+    return (unsigned)((4 * ky + kx) * cin + ch * 64 + half * 32);
+  };
+  auto piece_a = [&](char* sA, unsigned delta, unsigned pen, int g) {
+    dma16(ra, sA + (wave * AG + g) * 1024, ((a_off[g] + delta) * 2u) | (((pen >> g) & 1u) << 31));
+  };
+  auto piece_b = [&](char* sB, unsigned k0, int j, int h) {
+    dma16(rb, sB + j * G::B + (wave * BG + h) * 1024, ((b_off[h] + k0) * 2u) | (b_off[h] & OOB));
+  };
   auto issue_a = [&](int ss, int aslot) {
-    const int ch = ss >> 3, ky = (ss >> 1) & 3, odd = (ss & 1) ^ 1;
-    char* sA = smem + HB_A0 + aslot * HB_A;
-    const unsigned delta = (unsigned)((ky - 1) * p.a_rs + odd * p.a_ps + ch * 64);
-    const unsigned pen = ky == 0 ? top : (ky == 3 ? bot : 0u);
+    unsigned delta, pen;
+    a_terms(ss, delta, pen);
 #pragma unroll
-    for (int g = 0; g < AG; ++g)
-      dma16(ra, sA + (wave * AG + g) * 1024, ((a_off[g] + delta) * 2u) | (((pen >> g) & 1u) << 31));
+    for (int g = 0; g < AG; ++g) piece_a(smem + G::A0 + aslot * G::A, delta, pen, g);
   };
   auto issue_b = [&](int ss) {
-    const int ch = ss >> 3, ky = (ss >> 1) & 3, odd = (ss & 1) ^ 1;
-    char* sB = smem + ((ss & 1) ? HB_A0 + 3 * HB_A : 0);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int kx = odd ? 2 * j : 2 * j + 1;
-      const unsigned k0 = (unsigned)((4 * ky + kx) * cin + ch * 64);
+      const unsigned k0 = b_k0(ss, j);
 #pragma unroll
-      for (int h = 0; h < BG; ++h)
-        dma16(rb, sB + j * HB_B + (wave * BG + h) * 1024, ((b_off[h] + k0) * 2u) | (b_off[h] & OOB));
+      for (int h = 0; h < BG; ++h) piece_b(smem + ((ss & 1) ? G::B1 : 0), k0, j, h);
     }
   };
 
@@ -129,30 +163,33 @@ __global__ void __launch_bounds__(64 * HB_NW) halo_conv_s2_kernel(const GParams 
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment read offsets: row (l & 15) of the fragment, chunk 4 kk + (l >> 4); A rows shifted by d
+  // fragment read offsets: row (l & 15) of the fragment, chunk KK * 4 * kk... = 4 kk + (l >> 4); A rows shifted by d
+  // (fragment i adds 16 i rows, which keeps hswz: 16 is a multiple of 8)
   const int rl = lane & 15, kq = lane >> 4;
-  int a_rd[3][2], b_rd[2];
+  int a_rd[3][KK], b_rd[KK];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
+  for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
     for (int di = 0; di < 3; ++di) {
-      const int pr = wm * 64 + rl + di - 1;  // fragment 0's row + d (fragment i adds 16 i rows)
-      a_rd[di][kk] = pr * 128 + (((4 * kk + kq) ^ ((rl + di - 1) & 7)) * 16);
+      const int pr = wm * TM + rl + di - 1;
+      a_rd[di][kk] = pr * RB + (((4 * kk + kq) ^ hswz<RB>(pr)) * 16);
     }
-    b_rd[kk] = (wn * 64 + rl) * 128 + (((4 * kk + kq) ^ (rl & 7)) * 16);
+    b_rd[kk] = (wn * TN + rl) * RB + (((4 * kk + kq) ^ hswz<RB>(rl)) * 16);
   }
   const bf16x8_t zero8 = {};
 
-  // one K-step (64 deep) from A stage sA / B K-step sBj, A rows shifted by D; with STC_HALO_IL, dma(kk, half)
-  // issues one LDS-DMA piece of the future stages after every 8 MFMAs (see below)
+  // one K-step (RB / 2 deep) from A stage sA / B K-step sBj, A rows shifted by D; dma(k) issues LDS-DMA piece k of
+  // the future stages after each 8 MFMAs
   auto kstep = [&](const char* sA, const char* sBj, auto Dc, auto dma) {
     constexpr int D = decltype(Dc)::value;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
       bf16x8_t fa[FM], fb[FN];
 #pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sBj + b_rd[kk] + j * 16 * RB);
+#pragma unroll
       for (int i = 0; i < FM; ++i) {
-        fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + a_rd[D + 1][kk] + i * 16 * 128);
+        fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + a_rd[D + 1][kk] + i * 16 * RB);
         // the fragment's first (D = -1) / last (D = +1) row is an output row's left / right edge: that lane's
         // operand is the zero padding, not the neighbouring row's pixel it addressed
         if constexpr (D == -1) {
@@ -162,85 +199,63 @@ __global__ void __launch_bounds__(64 * HB_NW) halo_conv_s2_kernel(const GParams 
         }
       }
 #pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sBj + b_rd[kk] + j * 16 * 128);
+      for (int q = 0; q < FM / 2; ++q) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int i = 2 * h; i < 2 * h + 2; ++i)
+        for (int i = 2 * q; i < 2 * q + 2; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j) acc[i][j] = exp_mfma(fa[i], fb[j], acc[i][j]);
-#if STC_HALO_IL
-        dma(kk, h);
+        dma(kk * (FM / 2) + q);
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * FN, 0);  // these 8 MFMAs, then the piece
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-#endif
       }
     }
   };
 
-  // Per super-step: wait for this wave's pieces of A(ss) and B(ss) -- A(ss + 1), issued after them, may stay
-  // in flight -- then the barrier (every wave's pieces landed; every wave done with super-step ss - 1), then
-  // refill the slots ss - 1 read: B(ss + 1), A(ss + 2).  STC_HALO_IL: the 8 pieces (per wave) of that refill are
-  // spread over the super-step, one after every 8 of its 64 MFMAs, instead of issued as a burst after the barrier
-  // (a burst of 64 one-KiB pieces per CU holds the waves at the texture unit before their first MFMA).
-  const int nss = (cin / 64) * 8;  // super-steps (even)
+  // Per super-step: wait for this wave's pieces of A(ss) and B(ss) -- A(ss + 1), issued after them, may stay in
+  // flight -- then the barrier (every wave's pieces landed; every wave done with super-step ss - 1), then refill the
+  // slots ss - 1 read, B(ss + 1) and A(ss + 2), one piece per 8 MFMAs of super-step ss (a burst of pieces after
+  // the barrier holds the waves at the texture unit before their first MFMA).
+  const int nss = (cin / 64) * 8 * HALVES;  // super-steps (a multiple of 8 / 16)
   issue_a(0, 0);
   issue_b(0);
   issue_a(1, 1);
   int aslot = 0;
-  char* const sB0 = smem;
-  char* const sB1 = smem + HB_A0 + 3 * HB_A;
-  for (int ss = 0; ss < nss; ss += 2) {
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {  // even super-step: B pair 0, odd parity (taps 0, 2); odd: B pair 1, even
-      const int s = ss + par;
-      wait_ahead<AG>(s + 1 < nss ? 1 : 0);
-      __builtin_amdgcn_s_barrier();
-      const bool nb = s + 1 < nss, na = s + 2 < nss;
-      const int na_slot = aslot == 0 ? 2 : aslot - 1;
-      const char* sA = smem + HB_A0 + aslot * HB_A;
-      const char* sB = par ? sB1 : sB0;
-#if STC_HALO_IL
-      // the refill's per-super-step terms (wave-uniform), then pieces k = 0..3 (B(s + 1)), 4..7 (A(s + 2))
-      const int nch = (s + 1) >> 3, nky = ((s + 1) >> 1) & 3, nodd = ((s + 1) & 1) ^ 1;
-      char* rB = smem + (((s + 1) & 1) ? HB_A0 + 3 * HB_A : 0);
-      const int ach = (s + 2) >> 3, aky = ((s + 2) >> 1) & 3, aodd = ((s + 2) & 1) ^ 1;
-      char* rA = smem + HB_A0 + na_slot * HB_A;
-      const unsigned adelta = (unsigned)((aky - 1) * p.a_rs + aodd * p.a_ps + ach * 64);
-      const unsigned apen = aky == 0 ? top : (aky == 3 ? bot : 0u);
-      auto piece = [&](int k) {
-        if (k < 4) {
-          if (!nb) return;
-          const int j = k >> 1, h = k & 1;
-          const int kx = nodd ? 2 * j : 2 * j + 1;
-          const unsigned k0 = (unsigned)((4 * nky + kx) * cin + nch * 64);
-          dma16(rb, rB + j * HB_B + (wave * BG + h) * 1024, ((b_off[h] + k0) * 2u) | (b_off[h] & OOB));
-        } else {
-          if (!na) return;
-          const int g = k - 4;
-          dma16(ra, rA + (wave * AG + g) * 1024, ((a_off[g] + adelta) * 2u) | (((apen >> g) & 1u) << 31));
-        }
-      };
-      if (par == 0) {
-        kstep(sA, sB, std::integral_constant<int, -1>{}, [&](int kk, int h) { piece(2 * kk + h); });
-        kstep(sA, sB + HB_B, std::integral_constant<int, 0>{}, [&](int kk, int h) { piece(4 + 2 * kk + h); });
+  // one super-step; U = q * HALVES + half (compile-time parity and B pair = U & 1)
+  auto super_step = [&](int s, auto Uc) {
+    constexpr int U = decltype(Uc)::value;
+    wait_ahead<AG>(s + 1 < nss ? 1 : 0);
+    __builtin_amdgcn_s_barrier();
+    const bool nb = s + 1 < nss, na = s + 2 < nss;
+    const char* sA = smem + G::A0 + aslot * G::A;
+    const char* sB = smem + ((U & 1) ? G::B1 : 0);
+    char* rB = smem + ((U & 1) ? 0 : G::B1);  // B(s + 1): the other pair
+    char* rA = smem + G::A0 + (aslot == 0 ? 2 : aslot - 1) * G::A;
+    const unsigned bk0 = b_k0(s + 1, 0), bk1 = b_k0(s + 1, 1);
+    unsigned adelta, apen;
+    a_terms(s + 2, adelta, apen);
+    // pieces per super-step and wave: B(s + 1) = 2 K-steps x BG, then A(s + 2) = AG
+    auto piece = [&](int k) {
+      if (k < 2 * BG) {
+        if (nb) piece_b(rB, k < BG ? bk0 : bk1, k / BG, k % BG);
       } else {
-        kstep(sA, sB, std::integral_constant<int, 0>{}, [&](int kk, int h) { piece(2 * kk + h); });
-        kstep(sA, sB + HB_B, std::integral_constant<int, 1>{}, [&](int kk, int h) { piece(4 + 2 * kk + h); });
+        if (na) piece_a(rA, adelta, apen, k - 2 * BG);
       }
-#else
-      if (nb) issue_b(s + 1);
-      if (na) issue_a(s + 2, na_slot);
-      auto none = [](int, int) {};
-      if (par == 0) {
-        kstep(sA, sB, std::integral_constant<int, -1>{}, none);
-        kstep(sA, sB + HB_B, std::integral_constant<int, 0>{}, none);
-      } else {
-        kstep(sA, sB, std::integral_constant<int, 0>{}, none);
-        kstep(sA, sB + HB_B, std::integral_constant<int, 1>{}, none);
-      }
-#endif
-      aslot = aslot == 2 ? 0 : aslot + 1;
+    };
+    if constexpr (U / HALVES == 0) {  // odd parity: taps 0 (d = -1), 2 (d = 0)
+      kstep(sA, sB, std::integral_constant<int, -1>{}, [&](int k) { piece(k); });
+      kstep(sA, sB + G::B, std::integral_constant<int, 0>{}, [&](int k) { piece(KK * FM / 2 + k); });
+    } else {  // even parity: taps 1 (d = 0), 3 (d = +1)
+      kstep(sA, sB, std::integral_constant<int, 0>{}, [&](int k) { piece(k); });
+      kstep(sA, sB + G::B, std::integral_constant<int, 1>{}, [&](int k) { piece(KK * FM / 2 + k); });
+    }
+    aslot = aslot == 2 ? 0 : aslot + 1;
+  };
+  for (int ss = 0; ss < nss; ss += 2 * HALVES) {
+    super_step(ss, std::integral_constant<int, 0>{});
+    super_step(ss + 1, std::integral_constant<int, 1>{});
+    if constexpr (HALVES == 2) {
+      super_step(ss + 2, std::integral_constant<int, 2>{});
+      super_step(ss + 3, std::integral_constant<int, 3>{});
     }
   }
 
@@ -255,7 +270,7 @@ __global__ void __launch_bounds__(64 * HB_NW) halo_conv_s2_kernel(const GParams 
     return;
   }
 #endif
-  igemm_epilogue<BM, BN, HB_WM, HB_WN, BNB>(p, acc, m0, n0, 0, mt, 0, smem);
+  igemm_epilogue<BM, BN, WM, WN, BNB>(p, acc, m0, n0, 0, mt, 0, smem);
 }
 
 // ------------------------------------------------------------------------- host
@@ -283,8 +298,9 @@ bool halo_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const 
 
 int halo_chunks(int B, int GH, int GW) { return B * GH * GW / HB_BM; }
 
-// p: filled by bf16_conv_fwd (geometry, operands, output, epilogue options; vec_out set).
-int halo_launch(GParams& p, hipStream_t st) {
+// p: filled by bf16_conv_fwd (geometry, operands, output, epilogue options; vec_out set).  shape: 0 automatic,
+// 1 the 8-wave 160 KiB block, 2 the 4-wave 80 KiB block (force_plan {HALO_CFG, shape}: tests / A/B).
+int halo_launch(GParams& p, hipStream_t st, int shape) {
   STC_REQUIRE(p.vec_out && !p.ws && p.nphase == 1 && p.M % HB_BM == 0, "halo conv: bad launch parameters");
   p.mtiles = p.M / HB_BM;
   p.ntiles = (p.N + HB_BN - 1) / HB_BN;
@@ -293,10 +309,19 @@ int halo_launch(GParams& p, hipStream_t st) {
   p.phase_major = 0;
   const dim3 grid((unsigned)(p.mtiles * p.ntiles));
   const bool bnb = p.part2 != nullptr;
-#define STC_H(GW_)                                                                                                \
-  case GW_:                                                                                                       \
-    if (bnb) hipLaunchKernelGGL((halo_conv_s2_kernel<GW_, true>), grid, dim3(64 * HB_NW), HB_LDS, st, p);       \
-    else hipLaunchKernelGGL((halo_conv_s2_kernel<GW_, false>), grid, dim3(64 * HB_NW), HB_LDS, st, p);          \
+  // >= 512 blocks: the 4-wave 80 KiB block, two per CU; fewer: the 8-wave block (one per CU, all CUs busy)
+  const bool two = shape == 2 || (shape != 1 && p.mtiles * p.ntiles >= 512);
+#define STC_HK(GW_, B_, RB_, WM_, WN_) \
+  hipLaunchKernelGGL((halo_conv_s2_kernel<GW_, B_, RB_, WM_, WN_>), grid, dim3(64 * WM_ * WN_), HaloGeom<RB_>::LDS, st, p)
+#define STC_H(GW_)                                           \
+  case GW_:                                                  \
+    if (two) {                                               \
+      if (bnb) STC_HK(GW_, true, 64, 2, 2);                  \
+      else STC_HK(GW_, false, 64, 2, 2);                     \
+    } else {                                                 \
+      if (bnb) STC_HK(GW_, true, 128, 4, 2);                 \
+      else STC_HK(GW_, false, 128, 4, 2);                    \
+    }                                                        \
     break;
   main_timer_begin(st);
   switch (p.GW) {
@@ -307,6 +332,7 @@ int halo_launch(GParams& p, hipStream_t st) {
       return fail(-1, "halo conv: output width %d", p.GW);
   }
 #undef STC_H
+#undef STC_HK
   main_timer_end(st);
   STC_CHECK_LAUNCH();
   return 0;

@@ -802,7 +802,7 @@ bool halo_geometry_ok(int kind, int B, int GH, int GW, int Cin, int Cout);
 bool halo_auto(int kind, int B, int GH, int GW, int Cin, int Cout);
 bool halo_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y);
 int halo_chunks(int B, int GH, int GW);
-int halo_launch(GParams& p, hipStream_t st);
+int halo_launch(GParams& p, hipStream_t st, int shape);
 static bool halo_plan(const int32_t* force, int kind, int B, int GH, int GW, int Cin, int Cout) {
   if (force && force[0] == HALO_CFG) return halo_geometry_ok(kind, B, GH, GW, Cin, Cout);
   return (!force || force[0] == -1) && halo_auto(kind, B, GH, GW, Cin, Cout);
@@ -892,7 +892,7 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
     if (stats || part2) STC_REQUIRE(stats_chunks >= need, "bf16 conv: stats chunks %d < %d", stats_chunks, need);
     p.stats = stats;
     p.ws = nullptr;
-    return halo_launch(p, st);
+    return halo_launch(p, st, force && force[0] == HALO_CFG ? force[1] : 0);
   }
   STC_REQUIRE(!(force && force[0] == HALO_CFG), "bf16 conv: the halo kernel does not take this shape / view");
   return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st);

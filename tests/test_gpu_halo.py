@@ -19,7 +19,8 @@ from stcgan_amd import ops
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 BF = torch.bfloat16
-HALO = (ops.HALO_CFG, 1)
+HALO = (ops.HALO_CFG, 1)   # the 8-wave block (one per CU)
+HALO2 = (ops.HALO_CFG, 2)  # the 4-wave block (two per CU)
 
 
 def nhwc(t):
@@ -77,13 +78,14 @@ CASES = [  # B, Cin, Cout, GH, GW
 ]
 
 
+@pytest.mark.parametrize("shape", [HALO, HALO2], ids=["8wave", "4wave"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
-def test_halo_conv_s2(case):
+def test_halo_conv_s2(case, shape):
     B, Cin, Cout, GH, GW = case
     x = q(rnd(B, Cin, 2 * GH, 2 * GW, seed=1, dev=DEV))
     w = q(rnd(Cout, Cin, 4, 4, seed=2, scale=0.05, dev=DEV))
     ref = F.conv2d(x, w, None, 2, 1)
-    y, mean, var, plan = run(B, x, w, Cin, Cout, GH, GW, HALO)
+    y, mean, var, plan = run(B, x, w, Cin, Cout, GH, GW, shape)
     assert plan[4] == ops.HALO_CFG and plan[0] == 256
     check(y, ref, mean, var, f"halo {case}")
     # the im2col tile on the same operands: equal up to the summation order
@@ -93,7 +95,8 @@ def test_halo_conv_s2(case):
     assert float((y - y2).abs().max()) <= 1e-2 * scale
 
 
-def test_halo_views_and_bias():
+@pytest.mark.parametrize("shape", [HALO, HALO2], ids=["8wave", "4wave"])
+def test_halo_views_and_bias(shape):
     """Input from a channel slice of a wider buffer (the concat buffers), output into the second half of one,
     with a bias epilogue."""
     B, Cin, Cout, GH, GW = 2, 64, 128, 8, 32
@@ -101,7 +104,7 @@ def test_halo_views_and_bias():
     w = q(rnd(Cout, Cin, 4, 4, seed=4, scale=0.05, dev=DEV))
     b = rnd(Cout, seed=5, dev=DEV)
     ref = F.conv2d(x, w, b, 2, 1)
-    y, mean, var, _ = run(B, x, w, Cin, Cout, GH, GW, HALO, co_in=64, extra_in=64, co=64, extra_c=64, bias=b)
+    y, mean, var, _ = run(B, x, w, Cin, Cout, GH, GW, shape, co_in=64, extra_in=64, co=64, extra_c=64, bias=b)
     check(y, ref, mean, var, "halo views+bias")
 
 
@@ -136,8 +139,9 @@ class _BNT:
         self.gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
 
 
-@pytest.mark.parametrize("case", [(8, 64, 256, 64, 64, 128, 128), (32, 256, 1024, 16, 16, 512, 512)],
-                         ids=["d2_dgrad", "d4_dgrad"])
+@pytest.mark.parametrize("case", [(8, 64, 256, 64, 64, 128, 128), (32, 256, 1024, 16, 16, 512, 512),
+                                  (32, 128, 512, 32, 32, 256, 256), (64, 256, 1024, 16, 16, 512, 512)],
+                         ids=["d2_dgrad_8wave", "d4_dgrad_8wave", "d3_dgrad_4wave", "gw16_4wave"])
 def test_halo_conv_bn_backward(case):
     """The ConvT input gradient at its train-step size (conv-s2 geometry, automatic plan = halo) with the
     BatchNorm-backward reduction fused into the epilogue: output vs torch, sums vs the separate reduction."""
