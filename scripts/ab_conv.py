@@ -13,12 +13,18 @@ from stcgan_amd import _lib as L  # noqa: E402
 from stcgan_amd import ops  # noqa: E402
 
 BF = torch.bfloat16
-SHAPES = [  # (grid, cin, cout, what)
-    (64, 64, 128, "e2 / D c2 fwd"),
-    (32, 128, 256, "e3 / D c3 fwd"),
-    (64, 64, 256, "d2 dgrad (ConvT 256->64)"),
-    (32, 128, 512, "d3 dgrad (ConvT 512->128)"),
-    (16, 256, 1024, "d4 dgrad (ConvT 1024->256)"),
+SHAPES = [  # (kind, GEMM grid, cin, cout, what)
+    (L.CONV_S2, 64, 64, 128, "e2 / D c2 fwd"),
+    (L.CONV_S2, 32, 128, 256, "e3 / D c3 fwd"),
+    (L.CONV_S2, 64, 64, 256, "d2 dgrad (ConvT 256->64)"),
+    (L.CONV_S2, 32, 128, 512, "d3 dgrad (ConvT 512->128)"),
+    (L.CONV_S2, 16, 256, 1024, "d4 dgrad (ConvT 1024->256)"),
+    (L.CONVT_S2, 64, 256, 64, "d2 fwd (ConvT 256->64)"),
+    (L.CONVT_S2, 32, 512, 128, "d3 fwd"),
+    (L.CONVT_S2, 16, 1024, 256, "d4 fwd"),
+    (L.CONVT_S2, 64, 128, 64, "e2 / D c2 dgrad"),
+    (L.CONVT_S2, 32, 256, 128, "e3 / D c3 dgrad"),
+    (L.CONVT_S2, 16, 512, 256, "e4 dgrad"),
 ]
 
 
@@ -26,23 +32,30 @@ def main():
     dev = torch.device("cuda", 0)
     B = 32
     g = torch.Generator(device=dev).manual_seed(0)
-    for gh, cin, cout, what in SHAPES:
-        x = (torch.randn((B, 2 * gh, 2 * gh, cin), generator=g, device=dev)).to(BF)
-        w = torch.randn((cout, cin, 4, 4), generator=g, device=dev) * 0.05
-        wp = ops.pack(L.PACK_CONV_FWD, w, cout, cin, BF)
+    for kind, gh, cin, cout, what in SHAPES:
+        convt = kind == L.CONVT_S2
+        ih = gh if convt else 2 * gh
+        oh = 2 * gh if convt else gh
+        x = (torch.randn((B, ih, ih, cin), generator=g, device=dev)).to(BF)
+        if convt:
+            w = torch.randn((cin, cout, 4, 4), generator=g, device=dev) * 0.05
+            wp = ops.pack(L.PACK_CONVT_FWD, w, cout, cin, BF)
+        else:
+            w = torch.randn((cout, cin, 4, 4), generator=g, device=dev) * 0.05
+            wp = ops.pack(L.PACK_CONV_FWD, w, cout, cin, BF)
         ys = {}
         times = {"halo": [], "im2col": []}
         plans = {}
         for rnd in range(5):
             for name, force in (("halo", None), ("im2col", (-2, 0))):
-                y = torch.empty((B, gh, gh, cout), device=dev, dtype=BF)
-                plans[name] = ops.conv_query(L.CONV_S2, B, gh, gh, cin, cout, BF, force=force)[2]
-                ops.conv_stats(L.CONV_S2, B, L.nhwc_view(x), cin, wp, cout, L.nhwc_view(y), BF, force=force)
+                y = torch.empty((B, oh, oh, cout), device=dev, dtype=BF)
+                plans[name] = ops.conv_query(kind, B, gh, gh, cin, cout, BF, force=force)[2]
+                ops.conv_stats(kind, B, L.nhwc_view(x), cin, wp, cout, L.nhwc_view(y), BF, force=force)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(20):
-                    ops.conv_stats(L.CONV_S2, B, L.nhwc_view(x), cin, wp, cout, L.nhwc_view(y), BF, force=force)
+                    ops.conv_stats(kind, B, L.nhwc_view(x), cin, wp, cout, L.nhwc_view(y), BF, force=force)
                 e1.record()
                 e1.synchronize()
                 times[name].append(e0.elapsed_time(e1) / 20 * 1e3)

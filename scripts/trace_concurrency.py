@@ -16,7 +16,7 @@ iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"
 t_beg, t_end = iv[0][0], max(e for _, e, _, _ in iv)
 if ":" in (sys.argv[2] if len(sys.argv) > 2 else ""):
     a, b = (int(v) for v in sys.argv[2].split(":"))
-    ad = [v for v in iv if v[2].startswith("stc::adam_pack")]
+    ad = [v for v in iv if "adam_pack" in v[2]]
     w0, w1 = ad[a][1], ad[b][1]
     iv = [v for v in iv if v[0] >= w0 and v[1] <= w1]
     print(f"window: adam #{a} .. #{b} ({(w1 - w0) / 1e6:.3f} ms)")

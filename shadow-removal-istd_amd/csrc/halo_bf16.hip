@@ -42,8 +42,8 @@ constexpr int HB_BM = 256, HB_BN = 128;  // block tile: 256 GEMM rows (whole out
 //             4-wave blocks per CU would leave half the CUs empty)
 // LDS: [B pair 0][A slot 0][A slot 1][A slot 2][B pair 1].  The masked edge lanes of A slot 0 / 2 address one pixel
 // before / after it: inside the neighbouring B pair, never outside the block's LDS.
-template <int RB> struct HaloGeom {
-  static constexpr int A = HB_BM * RB, B = HB_BN * RB;
+template <int RB, int BN = HB_BN> struct HaloGeom {
+  static constexpr int A = HB_BM * RB, B = BN * RB;
   static constexpr int A0 = 2 * B, B1 = A0 + 3 * A, LDS = 4 * B + 3 * A;
   static constexpr int CH = RB / 16;        // 16-byte chunks per row
   static constexpr int PR = 1024 / RB;      // rows per 1 KiB DMA piece
@@ -57,32 +57,41 @@ template <int RB> __device__ __forceinline__ int hswz(int row) {
   else return ((row >> 2) & 1) << 1;
 }
 
-template <int GW, bool BNB, int RB, int WM, int WN>
-__global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kernel(const GParams p) {
-  using G = HaloGeom<RB>;
-  constexpr int BM = HB_BM, BN = HB_BN, NW = WM * WN;
+// GEOM 0: Conv2d k4 s2 (GEMM grid = output grid); GEOM 1: ConvTranspose2d k4 s2, one sub-pixel phase per block
+// (GEMM grid = input grid): phase (py, px) tap (ty, tx) reads input (gy + py - ty, gx + px - tx), so the stage of
+// ty holds the input rows gy0 + r + py - ty and its two taps tx read positions r * GW + gx + d, d = px - tx.
+template <int GEOM, int GW, int BN, bool BNB, int RB, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(const GParams p) {
+  using G = HaloGeom<RB, BN>;
+  constexpr int BM = HB_BM, NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;                  // wave tile: 128 x 64 / 64 x 64
   constexpr int FM = TM / 16, FN = TN / 16;                  // fragments of 16 x 16
   constexpr int KK = RB / 64;                                // 32-deep MFMA steps per K-step
   constexpr int AG = BM / (G::PR * NW), BG = BN / (G::PR * NW);  // DMA pieces per wave: A stage / B K-step
-  constexpr int HALVES = 128 / RB;                           // stages per 64-channel chunk, ky and parity
+  constexpr int HALVES = 128 / RB;                           // stages per 64-channel chunk and (ky, parity) / ty
+  constexpr int SPC = (GEOM == 0 ? 8 : 2) * HALVES;          // super-steps per 64-channel chunk
   constexpr int TH = BM / GW;
-  static_assert(GW % 16 == 0 && BM % GW == 0 && TM % GW == 0 && FN == 4 && FM % 2 == 0,
+  constexpr int NP = 2 * BG + AG, NG = 2 * KK * FM / 2;      // DMA pieces / 8-MFMA groups per super-step and wave
+  static_assert(GW % 16 == 0 && BM % GW == 0 && TM % GW == 0 && FN == 4 && FM % 2 == 0 && BG >= 1,
                 "whole output rows per tile and per wave, 16-row fragments inside an output row");
-  static_assert(2 * BG + AG == KK * FM, "one DMA piece per 8 MFMAs");
+  static_assert(NP >= NG, "every MFMA group issues a piece");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
 
-  // XCD-aware bijective remap (blocks b, b + 8, ... share an XCD): consecutive tiles -- the N tiles of one A
-  // tile, and vertically adjacent row tiles, whose stages overlap by one input row -- run on one XCD's L2
-  const int nwg = p.mtiles * p.ntiles;
+  // XCD-aware bijective remap (blocks b, b + 8, ... share an XCD): consecutive ids -- the 4 phases of a ConvT tile
+  // (the same input rows), the N tiles of one A tile, vertically adjacent row tiles (overlapping stages) -- run on
+  // one XCD's L2
+  const int nwg = p.mtiles * p.ntiles * (GEOM == 1 ? 4 : 1);
   int bid = blockIdx.x;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
+  const int ph = GEOM == 1 ? (bid & 3) : 0;  // phase (py, px) = (ph >> 1, ph & 1)
+  if (GEOM == 1) bid >>= 2;
+  const int py = ph >> 1, px = ph & 1;
   const int mt = bid / p.ntiles, nt = bid % p.ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
   const int tiles_img = p.GH / TH;
@@ -95,46 +104,61 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kern
   const int prow = lane / G::CH;
   const int schunk = (lane % G::CH) ^ hswz<RB>(prow);  // (pieces are PR-row aligned: hswz(position) == hswz(prow))
   unsigned a_off[AG];
-  unsigned top = 0, bot = 0;  // pieces whose output row is the image's first / last (ky = 0 / 3 read padding)
+  // pieces whose grid row is the image's first / last: conv-s2 ky = 0 / 3 and ConvT row offset -1 / +1 read padding
+  unsigned top = 0, bot = 0;
 #pragma unroll
   for (int g = 0; g < AG; ++g) {
     const int pos = (wave * AG + g) * G::PR + prow;
     const int r = pos / GW, c = pos % GW;
     const int oy = oy0 + r;
-    a_off[g] = (unsigned)(img * p.a_bs + p.a_co) + (unsigned)(2 * oy) * (unsigned)p.a_rs + (unsigned)(2 * c) * (unsigned)p.a_ps +
-               (unsigned)(schunk * 8);
+    const int s_ = GEOM == 0 ? 2 : 1;  // input rows / columns per grid step
+    a_off[g] = (unsigned)(img * p.a_bs + p.a_co) + (unsigned)(s_ * oy) * (unsigned)p.a_rs +
+               (unsigned)(s_ * c) * (unsigned)p.a_ps + (unsigned)(schunk * 8);
     top |= (oy == 0 ? 1u : 0u) << g;
-    bot |= (2 * oy + 2 >= p.IH ? 1u : 0u) << g;
+    bot |= (GEOM == 0 ? 2 * oy + 2 >= p.IH : oy == p.GH - 1) ? (1u << g) : 0u;
   }
   unsigned b_off[BG];
 #pragma unroll
   for (int h = 0; h < BG; ++h) {
     const int n = n0 + (wave * BG + h) * G::PR + prow;
-    b_off[h] = n < p.N ? (unsigned)(n * p.K + schunk * 8) : OOB;
+    b_off[h] = n < p.N ? (unsigned)(ph * p.b_phase_stride + n * p.K + schunk * 8) : OOB;
   }
   const int cin = p.cin;
 
-  // Super-step ss = ((chunk * 4 + ky) * 2 + q) * HALVES + half: parity q = 0 odd (taps 0, 2) / 1 even (taps 1, 3),
-  // half = the 32-channel half of the 64-channel chunk (RB = 64: the two halves of a pixel's 128-byte line back to
-  // back).  Its A stage goes to A slot ss % 3, its two B K-steps to B pair ss & 1.
+  // GEOM 0: super-step ss = ((chunk * 4 + ky) * 2 + q) * HALVES + half: parity q = 0 odd (taps 0, 2) / 1 even
+  // (taps 1, 3); GEOM 1: ss = (chunk * 2 + ty) * HALVES + half (taps tx = 0, 1).  half = the 32-channel half of the
+  // 64-channel chunk (RB = 64: the two halves of a pixel's 128-byte line back to back).  Its A stage goes to A slot
+  // ss % 3, its two B K-steps to B pair ss & 1.
   auto ss_terms = [&](int ss, int& half, int& odd, int& ky, int& ch) {
     half = HALVES == 2 ? (ss & 1) : 0;
     const int t = HALVES == 2 ? ss >> 1 : ss;
-    odd = (t & 1) ^ 1;
-    ky = (t >> 1) & 3;
-    ch = t >> 3;
+    if constexpr (GEOM == 0) {
+      odd = (t & 1) ^ 1;
+      ky = (t >> 1) & 3;
+      ch = t >> 3;
+    } else {  // (ky = ty)
+      odd = 0;
+      ky = t & 1;
+      ch = t >> 1;
+    }
   };
   auto a_terms = [&](int ss, unsigned& delta, unsigned& pen) {
     int half, odd, ky, ch;
     ss_terms(ss, half, odd, ky, ch);
-    delta = (unsigned)((ky - 1) * p.a_rs + odd * p.a_ps + ch * 64 + half * 32);
-    pen = ky == 0 ? top : (ky == 3 ? bot : 0u);
+    if constexpr (GEOM == 0) {
+      delta = (unsigned)((ky - 1) * p.a_rs + odd * p.a_ps + ch * 64 + half * 32);
+      pen = ky == 0 ? top : (ky == 3 ? bot : 0u);
+    } else {
+      const int dy = py - ky;
+      delta = (unsigned)(dy * p.a_rs + ch * 64 + half * 32);
+      pen = dy < 0 ? top : (dy > 0 ? bot : 0u);
+    }
   };
   auto b_k0 = [&](int ss, int j) {
     int half, odd, ky, ch;
     ss_terms(ss, half, odd, ky, ch);
-    const int kx = odd ? 2 * j : 2 * j + 1;
-    return (unsigned)((4 * ky + kx) * cin + ch * 64 + half * 32);
+    const int tap = GEOM == 0 ? 4 * ky + (odd ? 2 * j : 2 * j + 1) : 2 * ky + j;
+    return (unsigned)(tap * cin + ch * 64 + half * 32);
   };
   auto piece_a = [&](char* sA, unsigned delta, unsigned pen, int g) {
     dma16(ra, sA + (wave * AG + g) * 1024, ((a_off[g] + delta) * 2u) | (((pen >> g) & 1u) << 31));
@@ -180,22 +204,28 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kern
 
   // one K-step (RB / 2 deep) from A stage sA / B K-step sBj, A rows shifted by D; dma(k) issues LDS-DMA piece k of
   // the future stages after each 8 MFMAs
-  auto kstep = [&](const char* sA, const char* sBj, auto Dc, auto dma) {
+  // D = 2: the shift is the runtime value dr (the ConvT taps: d = px - tx, block-uniform), one code path for both
+  // phase columns
+  auto kstep = [&](const char* sA, const char* sBj, auto Dc, auto dma, int dr = 0) {
     constexpr int D = decltype(Dc)::value;
+    const bool mlo = D == 2 ? (dr < 0 && rl == 0) : (D == -1 && rl == 0);   // left edge lane (d = -1)
+    const bool mhi = D == 2 ? (dr > 0 && rl == 15) : (D == 1 && rl == 15);  // right edge lane (d = +1)
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
+      const int ard = D == 2 ? (dr < 0 ? a_rd[0][kk] : (dr > 0 ? a_rd[2][kk] : a_rd[1][kk])) : a_rd[(D == 2 ? 0 : D) + 1][kk];
       bf16x8_t fa[FM], fb[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sBj + b_rd[kk] + j * 16 * RB);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + a_rd[D + 1][kk] + i * 16 * RB);
-        // the fragment's first (D = -1) / last (D = +1) row is an output row's left / right edge: that lane's
+        fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + ard + i * 16 * RB);
+        // the fragment's first (d = -1) / last (d = +1) row is an output row's left / right edge: that lane's
         // operand is the zero padding, not the neighbouring row's pixel it addressed
-        if constexpr (D == -1) {
-          if ((16 * i) % GW == 0) fa[i] = rl == 0 ? zero8 : fa[i];
-        } else if constexpr (D == 1) {
-          if ((16 * i + 16) % GW == 0) fa[i] = rl == 15 ? zero8 : fa[i];
+        if constexpr (D == -1 || D == 2) {
+          if ((16 * i) % GW == 0) fa[i] = mlo ? zero8 : fa[i];
+        }
+        if constexpr (D == 1 || D == 2) {
+          if ((16 * i + 16) % GW == 0) fa[i] = mhi ? zero8 : fa[i];
         }
       }
 #pragma unroll
@@ -205,8 +235,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kern
 #pragma unroll
           for (int j = 0; j < FN; ++j) acc[i][j] = exp_mfma(fa[i], fb[j], acc[i][j]);
         dma(kk * (FM / 2) + q);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * FN, 0);  // these 8 MFMAs, then the piece
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * FN, 0);  // these 8 MFMAs, then the group's pieces
+        __builtin_amdgcn_sched_group_barrier(0x020, (NP + NG - 1) / NG, 0);
       }
     }
   };
@@ -215,7 +245,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kern
   // flight -- then the barrier (every wave's pieces landed; every wave done with super-step ss - 1), then refill the
   // slots ss - 1 read, B(ss + 1) and A(ss + 2), one piece per 8 MFMAs of super-step ss (a burst of pieces after
   // the barrier holds the waves at the texture unit before their first MFMA).
-  const int nss = (cin / 64) * 8 * HALVES;  // super-steps (a multiple of 8 / 16)
+  const int nss = (cin / 64) * SPC;  // super-steps (even)
   issue_a(0, 0);
   issue_b(0);
   issue_a(1, 1);
@@ -233,7 +263,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kern
     const unsigned bk0 = b_k0(s + 1, 0), bk1 = b_k0(s + 1, 1);
     unsigned adelta, apen;
     a_terms(s + 2, adelta, apen);
-    // pieces per super-step and wave: B(s + 1) = 2 K-steps x BG, then A(s + 2) = AG
+    // pieces per super-step and wave: B(s + 1) = 2 K-steps x BG, then A(s + 2) = AG; MFMA group gi issues pieces
+    // [gi * NP / NG, (gi + 1) * NP / NG)
     auto piece = [&](int k) {
       if (k < 2 * BG) {
         if (nb) piece_b(rB, k < BG ? bk0 : bk1, k / BG, k % BG);
@@ -241,16 +272,28 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kern
         if (na) piece_a(rA, adelta, apen, k - 2 * BG);
       }
     };
-    if constexpr (U / HALVES == 0) {  // odd parity: taps 0 (d = -1), 2 (d = 0)
-      kstep(sA, sB, std::integral_constant<int, -1>{}, [&](int k) { piece(k); });
-      kstep(sA, sB + G::B, std::integral_constant<int, 0>{}, [&](int k) { piece(KK * FM / 2 + k); });
-    } else {  // even parity: taps 1 (d = 0), 3 (d = +1)
-      kstep(sA, sB, std::integral_constant<int, 0>{}, [&](int k) { piece(k); });
-      kstep(sA, sB + G::B, std::integral_constant<int, 1>{}, [&](int k) { piece(KK * FM / 2 + k); });
+    auto group = [&](int gi) {
+      for (int k = gi * NP / NG; k < (gi + 1) * NP / NG; ++k) piece(k);
+    };
+    using D_m1 = std::integral_constant<int, -1>;
+    using D_0 = std::integral_constant<int, 0>;
+    using D_p1 = std::integral_constant<int, 1>;
+    if constexpr (GEOM == 0) {
+      if constexpr (U / HALVES == 0) {  // odd parity: taps 0 (d = -1), 2 (d = 0)
+        kstep(sA, sB, D_m1{}, [&](int k) { group(k); });
+        kstep(sA, sB + G::B, D_0{}, [&](int k) { group(NG / 2 + k); });
+      } else {  // even parity: taps 1 (d = 0), 3 (d = +1)
+        kstep(sA, sB, D_0{}, [&](int k) { group(k); });
+        kstep(sA, sB + G::B, D_p1{}, [&](int k) { group(NG / 2 + k); });
+      }
+    } else {  // ConvT: taps tx = 0 (d = px), 1 (d = px - 1)
+      using D_rt = std::integral_constant<int, 2>;
+      kstep(sA, sB, D_rt{}, [&](int k) { group(k); }, px);
+      kstep(sA, sB + G::B, D_rt{}, [&](int k) { group(NG / 2 + k); }, px - 1);
     }
     aslot = aslot == 2 ? 0 : aslot + 1;
   };
-  for (int ss = 0; ss < nss; ss += 2 * HALVES) {
+  for (int ss = 0; ss < nss; ss += 2 * HALVES) {  // (GEOM 1: U / HALVES selects nothing; one or two ty per pass)
     super_step(ss, std::integral_constant<int, 0>{});
     super_step(ss + 1, std::integral_constant<int, 1>{});
     if constexpr (HALVES == 2) {
@@ -270,58 +313,75 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_s2_kern
     return;
   }
 #endif
-  igemm_epilogue<BM, BN, WM, WN, BNB>(p, acc, m0, n0, 0, mt, 0, smem);
+  igemm_epilogue<BM, BN, WM, WN, BNB>(p, acc, m0, n0, ph, mt, 0, smem);
 }
 
 // ------------------------------------------------------------------------- host
-// Eligible: Conv2d k4 s2 p1 geometry on an even input (IH = 2 GH, IW = 2 GW), whole-row tiles of 256 rows
-// (GW in {16, 32, 64}, GH a multiple of 256 / GW), 64-channel chunks, 16-byte NHWC bf16 views (no split K).
+// Eligible: Conv2d k4 s2 p1 on an even input (IH = 2 GH, IW = 2 GW) or ConvTranspose2d k4 s2 p1 (GEMM grid = the
+// input grid), whole-row tiles of 256 grid points (GW in {16, 32, 64}, GH a multiple of 256 / GW), 64-channel
+// chunks, 16-byte NHWC bf16 views (no split K).  N tile: 128 output channels, 64 for a ConvT with N <= 64.
+static int halo_bn(int kind, int Cout) { return kind == STC_CONVT_S2 && Cout <= 64 ? 64 : HB_BN; }
+
 bool halo_geometry_ok(int kind, int B, int GH, int GW, int Cin, int Cout) {
-  if (kind != STC_CONV_S2 || Cin % 64 != 0 || Cout % 8 != 0 || Cout > 2048) return false;
+  if ((kind != STC_CONV_S2 && kind != STC_CONVT_S2) || Cin % 64 != 0 || Cout % 8 != 0 || Cout > 2048) return false;
   if (!(GW == 16 || GW == 32 || GW == 64) || GH % (HB_BM / GW) != 0) return false;
   return 16ll * Cin * Cout * 2 < (1ll << 31);
 }
 
+static long long halo_blocks(int kind, int B, int GH, int GW, int Cout) {
+  const int bn = halo_bn(kind, Cout);
+  return (long long)B * GH * GW / HB_BM * ((Cout + bn - 1) / bn) * (kind == STC_CONVT_S2 ? 4 : 1);
+}
+
 // The automatic plan takes the halo kernel when it fills the chip: >= 256 blocks (one 8-wave block per CU).
 bool halo_auto(int kind, int B, int GH, int GW, int Cin, int Cout) {
-  if (!halo_geometry_ok(kind, B, GH, GW, Cin, Cout)) return false;
-  return (long long)B * GH * GW / HB_BM * ((Cout + HB_BN - 1) / HB_BN) >= 256;
+  return halo_geometry_ok(kind, B, GH, GW, Cin, Cout) && halo_blocks(kind, B, GH, GW, Cout) >= 256;
 }
 
 bool halo_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y) {
-  const int GH = y.H, GW = y.W;
+  const bool convt = kind == STC_CONVT_S2;
+  const int GH = convt ? x.H : y.H, GW = convt ? x.W : y.W;
   if (!halo_geometry_ok(kind, B, GH, GW, Cin, Cout)) return false;
-  if (x.H != 2 * GH || x.W != 2 * GW) return false;
+  if (!convt && (x.H != 2 * GH || x.W != 2 * GW)) return false;
   if (x.cs != 1 || x.co % 8 != 0 || x.ps % 8 != 0 || x.rs % 8 != 0 || x.bs % 8 != 0) return false;
   return (long long)B * x.bs * 2 < (1ll << 31);
 }
 
-int halo_chunks(int B, int GH, int GW) { return B * GH * GW / HB_BM; }
+int halo_chunks(int kind, int B, int GH, int GW) { return B * GH * GW / HB_BM * (kind == STC_CONVT_S2 ? 4 : 1); }
 
 // p: filled by bf16_conv_fwd (geometry, operands, output, epilogue options; vec_out set).  shape: 0 automatic,
-// 1 the 8-wave 160 KiB block, 2 the 4-wave 80 KiB block (force_plan {HALO_CFG, shape}: tests / A/B).
+// 1 the 8-wave 160 KiB block, 2 the 4-wave 80 KiB block (force_plan {HALO_CFG, shape}: tests / A/B; N <= 64
+// ConvTs always take the 4-wave 256 x 64 block).
 int halo_launch(GParams& p, hipStream_t st, int shape) {
-  STC_REQUIRE(p.vec_out && !p.ws && p.nphase == 1 && p.M % HB_BM == 0, "halo conv: bad launch parameters");
+  const bool convt = p.nphase == 4;
+  STC_REQUIRE(p.vec_out && !p.ws && (p.nphase == 1 || convt) && p.M % HB_BM == 0, "halo conv: bad launch parameters");
+  const int bn = convt && p.N <= 64 ? 64 : HB_BN;
   p.mtiles = p.M / HB_BM;
-  p.ntiles = (p.N + HB_BN - 1) / HB_BN;
+  p.ntiles = (p.N + bn - 1) / bn;
   p.ksplit = 1;
   p.kchunk = p.K;
   p.phase_major = 0;
-  const dim3 grid((unsigned)(p.mtiles * p.ntiles));
+  const int blocks = p.mtiles * p.ntiles * p.nphase;
+  const dim3 grid((unsigned)blocks);
   const bool bnb = p.part2 != nullptr;
   // >= 512 blocks: the 4-wave 80 KiB block, two per CU; fewer: the 8-wave block (one per CU, all CUs busy)
-  const bool two = shape == 2 || (shape != 1 && p.mtiles * p.ntiles >= 512);
-#define STC_HK(GW_, B_, RB_, WM_, WN_) \
-  hipLaunchKernelGGL((halo_conv_s2_kernel<GW_, B_, RB_, WM_, WN_>), grid, dim3(64 * WM_ * WN_), HaloGeom<RB_>::LDS, st, p)
-#define STC_H(GW_)                                           \
-  case GW_:                                                  \
-    if (two) {                                               \
-      if (bnb) STC_HK(GW_, true, 64, 2, 2);                  \
-      else STC_HK(GW_, false, 64, 2, 2);                     \
-    } else {                                                 \
-      if (bnb) STC_HK(GW_, true, 128, 4, 2);                 \
-      else STC_HK(GW_, false, 128, 4, 2);                    \
-    }                                                        \
+  const bool two = shape == 2 || (shape != 1 && blocks >= 512) || bn == 64;
+#define STC_HK(G_, GW_, BN_, B_, RB_, WM_, WN_)                                                               \
+  hipLaunchKernelGGL((halo_conv_kernel<G_, GW_, BN_, B_, RB_, WM_, WN_>), grid, dim3(64 * WM_ * WN_),         \
+                     (HaloGeom<RB_, BN_>::LDS), st, p)
+#define STC_HB(G_, GW_, BN_, RB_, WM_, WN_) \
+  if (bnb) STC_HK(G_, GW_, BN_, true, RB_, WM_, WN_); else STC_HK(G_, GW_, BN_, false, RB_, WM_, WN_);
+#define STC_H(GW_)                                          \
+  case GW_:                                                 \
+    if (!convt) {                                           \
+      if (two) { STC_HB(0, GW_, 128, 64, 2, 2) }            \
+      else { STC_HB(0, GW_, 128, 128, 4, 2) }               \
+    } else if (bn == 64) {                                  \
+      STC_HB(1, GW_, 64, 64, 4, 1)                          \
+    } else {                                                \
+      if (two) { STC_HB(1, GW_, 128, 64, 2, 2) }            \
+      else { STC_HB(1, GW_, 128, 128, 4, 2) }               \
+    }                                                       \
     break;
   main_timer_begin(st);
   switch (p.GW) {
@@ -329,9 +389,10 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
     STC_H(32)
     STC_H(64)
     default:
-      return fail(-1, "halo conv: output width %d", p.GW);
+      return fail(-1, "halo conv: grid width %d", p.GW);
   }
 #undef STC_H
+#undef STC_HB
 #undef STC_HK
   main_timer_end(st);
   STC_CHECK_LAUNCH();

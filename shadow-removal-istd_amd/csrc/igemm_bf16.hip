@@ -801,7 +801,7 @@ constexpr int HALO_CFG = 100;
 bool halo_geometry_ok(int kind, int B, int GH, int GW, int Cin, int Cout);
 bool halo_auto(int kind, int B, int GH, int GW, int Cin, int Cout);
 bool halo_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y);
-int halo_chunks(int B, int GH, int GW);
+int halo_chunks(int kind, int B, int GH, int GW);
 int halo_launch(GParams& p, hipStream_t st, int shape);
 static bool halo_plan(const int32_t* force, int kind, int B, int GH, int GW, int Cin, int Cout) {
   if (force && force[0] == HALO_CFG) return halo_geometry_ok(kind, B, GH, GW, Cin, Cout);
@@ -812,9 +812,10 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
                     int64_t* ws_bytes, int32_t* stats_chunks, int32_t* plan_out) {
   if (!out_f32 && halo_plan(force, kind, B, Hg, Wg, Cin, Cout)) {
     if (ws_bytes) *ws_bytes = 0;
-    if (stats_chunks) *stats_chunks = halo_chunks(B, Hg, Wg);
+    if (stats_chunks) *stats_chunks = halo_chunks(kind, B, Hg, Wg);
     if (plan_out) {
-      plan_out[0] = 256; plan_out[1] = 128; plan_out[2] = 1; plan_out[3] = 0; plan_out[4] = HALO_CFG;
+      plan_out[0] = 256; plan_out[1] = kind == STC_CONVT_S2 && Cout <= 64 ? 64 : 128; plan_out[2] = 1; plan_out[3] = 0;
+      plan_out[4] = HALO_CFG;
     }
     return 0;
   }
@@ -888,7 +889,7 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
     }
   }
   if (!act_n && p.vec_out && halo_plan(force, kind, B, p.GH, p.GW, Cin, Cout) && halo_eligible(kind, B, x, Cin, Cout, y)) {
-    const int need = halo_chunks(B, p.GH, p.GW);
+    const int need = halo_chunks(kind, B, p.GH, p.GW);
     if (stats || part2) STC_REQUIRE(stats_chunks >= need, "bf16 conv: stats chunks %d < %d", stats_chunks, need);
     p.stats = stats;
     p.ws = nullptr;

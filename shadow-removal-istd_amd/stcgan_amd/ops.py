@@ -197,8 +197,11 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
             nb = 2 if (kind == L.CONVT_S2 and 4 * cout > 16) else 1
             return f"narrow_halo_kernel<{geom}, {nb}, 8>", ws == 0
         return "narrow_tiled_kernel", True
-    if cfg == HALO_CFG:  # conv-s2 with the LDS-resident input halo (csrc/halo_bf16.hip)
-        return f"halo_conv_s2_kernel<{gw}, {str(bnb).lower()}>", True
+    if cfg == HALO_CFG:  # the LDS-resident input halo kernels (csrc/halo_bf16.hip): template as rocprof names it
+        convt = kind == L.CONVT_S2
+        blocks = B * gh * gw // 256 * ((cout + bn - 1) // bn) * (4 if convt else 1)
+        rb, wm, wn = (64, 4, 1) if bn == 64 else ((64, 2, 2) if blocks >= 512 else (128, 4, 2))
+        return (f"halo_conv_kernel<{int(convt)}, {gw}, {bn}, {str(bnb).lower()}, {rb}, {wm}, {wn}>", True)
     if cfg >= 0:
         t = _BF16_TILES[cfg]
         if len(t) > 6:  # loader-wave blocks

@@ -1,7 +1,8 @@
-"""The conv-s2 halo kernel (csrc/halo_bf16.hip) against torch fp32 references and the im2col tile.
+"""The halo kernels (csrc/halo_bf16.hip) against torch fp32 references and the im2col tile.
 
 Conv2d k4 s2 p1 (STCGAN/networks.py:104-105, 167-169, 176-178) and the ConvTranspose2d input gradient (its
-geometry, networks.py:112-128 backward) with the A operand staged as input rows in LDS.  Checked: every output
+geometry, networks.py:112-128 backward), ConvTranspose2d k4 s2 p1 (networks.py:112-128, one sub-pixel phase per
+block) and the Conv2d input gradient (its geometry), with the A operand staged as input rows in LDS.  Checked: every output
 width the kernel takes (16, 32, 64 columns: 16, 8 and 4 output rows per 256-row tile), several 64-channel
 chunks, ragged N, channel-offset input and output views (the concat buffers), bias, the BatchNorm statistics
 and the fused BatchNorm-backward sums of the epilogue, the automatic plan at the train step's sizes.
@@ -168,6 +169,93 @@ def test_halo_conv_bn_backward(case):
     torch.cuda.synchronize()
     assert torch.equal(out1, out2)
     ref = F.conv2d(dy, wt, None, 2, 1)
+    assert float((nchw(out1.float()) - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+    for a, b_, nm in ((dg1, dg2, "dgamma"), (db1, db2, "dbeta")):
+        err = float((a - b_).abs().max())
+        assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm} {case}: {err:.3e}"
+    err = float((dx1.float() - dx2.float()).abs().max())
+    assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx {case}: {err:.3e}"
+
+
+def run_t(B, x, w, Cin, Cout, GH, GW, force):
+    """ConvTranspose2d (stc_conv_fwd_ex with statistics) of NCHW fp32 x [B, Cin, GH, GW]."""
+    xb = nhwc(x).to(DEV, BF)
+    wp = ops.pack(L.PACK_CONVT_FWD, w.to(DEV), Cout, Cin, BF)
+    y = torch.full((B, 2 * GH, 2 * GW, Cout), float("nan"), device=DEV, dtype=BF)
+    part, nch = ops.conv_stats(L.CONVT_S2, B, L.nhwc_view(xb), Cin, wp, Cout, L.nhwc_view(y), BF, force=force)
+    _, nq, plan = ops.conv_query(L.CONVT_S2, B, GH, GW, Cin, Cout, BF, force=force)
+    assert nq == nch
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV)
+    t = torch.empty((2, Cout), device=DEV)
+    mean, rstd = ops.bn_finalize_part(part, nch, Cout, bn, t[0], t[1])
+    var = 1.0 / rstd.double() ** 2 - bn.eps
+    torch.cuda.synchronize()
+    return nchw(y.float()), mean.double(), var, plan
+
+
+TCASES = [  # B, Cin, Cout, GH, GW (input grid)
+    (2, 64, 128, 8, 64),
+    (1, 128, 256, 16, 32),   # two chunks, two N tiles
+    (1, 256, 512, 16, 16),
+    (3, 64, 96, 4, 64),      # ragged N
+    (2, 128, 64, 8, 64),     # N = 64: the 256 x 64 tile
+    (1, 192, 40, 8, 32),     # N = 40 on the 256 x 64 tile, 3 chunks
+]
+
+
+@pytest.mark.parametrize("shape", [HALO, HALO2], ids=["8wave", "4wave"])
+@pytest.mark.parametrize("case", TCASES, ids=lambda c: "x".join(map(str, c)))
+def test_halo_convT(case, shape):
+    B, Cin, Cout, GH, GW = case
+    x = q(rnd(B, Cin, GH, GW, seed=11, dev=DEV))
+    w = q(rnd(Cin, Cout, 4, 4, seed=12, scale=0.05, dev=DEV))
+    ref = F.conv_transpose2d(x, w, None, 2, 1)
+    y, mean, var, plan = run_t(B, x, w, Cin, Cout, GH, GW, shape)
+    assert plan[4] == ops.HALO_CFG and plan[1] == (64 if Cout <= 64 else 128)
+    check(y, ref, mean, var, f"halo convT {case}")
+    y2, _, _, plan2 = run_t(B, x, w, Cin, Cout, GH, GW, (0, 1))
+    assert plan2[4] == 0
+    assert float((y - y2).abs().max()) <= 1e-2 * float(ref.abs().max())
+
+
+def test_halo_convT_plan_automatic_at_train_sizes():
+    """The generators' ConvT layers (forward and the conv-s2 input gradients) with 64-channel chunks and whole-row
+    tiles take the halo kernel at the train-step size."""
+    for (gh, cin, cout) in ((32, 512, 128), (16, 1024, 256), (64, 256, 64), (32, 256, 128), (16, 512, 256),
+                            (64, 128, 64)):
+        assert ops.conv_query(L.CONVT_S2, 32, gh, gh, cin, cout, BF)[2][4] == ops.HALO_CFG, (gh, cin, cout)
+    for (gh, cin, cout) in ((128, 128, 1), (8, 1024, 512), (4, 1024, 512)):
+        assert ops.conv_query(L.CONVT_S2, 32, gh, gh, cin, cout, BF)[2][4] != ops.HALO_CFG, (gh, cin, cout)
+
+
+@pytest.mark.parametrize("case", [(32, 256, 128, 32, 32, 128, 0), (32, 128, 64, 64, 64, 64, 0)],
+                         ids=["e3_dgrad", "e2_dgrad_n64"])
+def test_halo_convT_bn_backward(case):
+    """The conv-s2 input gradient (ConvT geometry) at its train-step size with the fused BatchNorm-backward sums."""
+    B, Cin, Cout, GH, GW, C, ch_off = case
+    assert ops.conv_query(L.CONVT_S2, B, GH, GW, Cin, Cout, BF)[2][4] == ops.HALO_CFG
+    wt = q(rnd(Cin, Cout, 4, 4, seed=61, scale=0.05, dev=DEV))
+    w = ops.pack(L.PACK_CONVT_FWD, wt, Cout, Cin, BF)
+    dy = q(rnd(B, Cin, GH, GW, seed=62, scale=0.5, dev=DEV))
+    dyb = nhwc(dy).to(BF)
+    oh, ow = 2 * GH, 2 * GW
+    x = torch.randn((B, oh, ow, C), generator=torch.Generator(device=DEV).manual_seed(63), device=DEV).to(BF)
+    go = torch.randn((B, oh, ow, C), generator=torch.Generator(device=DEV).manual_seed(64), device=DEV).to(BF)
+    bn = _BNT(C, 65)
+    st = (bn.scale, bn.shift, bn.mean, bn.rstd)
+    out1 = torch.zeros((B, oh, ow, Cout), device=DEV, dtype=BF)
+    dx1 = torch.empty((B, oh, ow, C), device=DEV, dtype=BF)
+    dg1, db1 = ops.conv_bn_backward(L.CONVT_S2, B, L.nhwc_view(dyb), Cin, w, Cout, L.nhwc_view(out1), BF,
+                                    bn_x=L.nhwc_view(x), C=C, bn_state=st, gamma=bn.gamma, s_self=0.2, ch_off=ch_off,
+                                    g_other=L.nhwc_view(go), s_other=0.0, dxv=L.nhwc_view(dx1))
+    out2 = torch.zeros((B, oh, ow, Cout), device=DEV, dtype=BF)
+    ops.conv(L.CONVT_S2, B, L.nhwc_view(dyb), Cin, w, Cout, L.nhwc_view(out2), BF)
+    dx2 = torch.empty((B, oh, ow, C), device=DEV, dtype=BF)
+    dg2, db2 = ops.bn_backward(B, L.nhwc_view(x), C, BF, L.nhwc_view(dx2), g1=L.nhwc_view(out2, ch_off), s1=0.2,
+                               g2=L.nhwc_view(go), s2=0.0, bn_state=(bn.scale, bn.shift, bn.mean, bn.rstd, bn.gamma))
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
+    ref = F.conv_transpose2d(dy, wt, None, 2, 1)
     assert float((nchw(out1.float()) - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
     for a, b_, nm in ((dg1, dg2, "dgamma"), (db1, db2, "dbeta")):
         err = float((a - b_).abs().max())
