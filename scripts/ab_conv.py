@@ -25,6 +25,8 @@ SHAPES = [  # (kind, GEMM grid, cin, cout, what)
     (L.CONVT_S2, 64, 128, 64, "e2 / D c2 dgrad"),
     (L.CONVT_S2, 32, 256, 128, "e3 / D c3 dgrad"),
     (L.CONVT_S2, 16, 512, 256, "e4 dgrad"),
+    (L.CONV_S1, 31, 256, 512, "D c4 fwd (k4 s1)"),
+    (L.CONV_S1_DGRAD, 32, 512, 256, "D c4 dgrad"),
 ]
 
 
@@ -34,12 +36,15 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     for kind, gh, cin, cout, what in SHAPES:
         convt = kind == L.CONVT_S2
-        ih = gh if convt else 2 * gh
-        oh = 2 * gh if convt else gh
+        ih, oh = {L.CONV_S2: (2 * gh, gh), L.CONVT_S2: (gh, 2 * gh), L.CONV_S1: (gh + 1, gh),
+                  L.CONV_S1_DGRAD: (gh - 1, gh)}[kind]
         x = (torch.randn((B, ih, ih, cin), generator=g, device=dev)).to(BF)
         if convt:
             w = torch.randn((cin, cout, 4, 4), generator=g, device=dev) * 0.05
             wp = ops.pack(L.PACK_CONVT_FWD, w, cout, cin, BF)
+        elif kind == L.CONV_S1_DGRAD:
+            w = torch.randn((cin, cout, 4, 4), generator=g, device=dev) * 0.05
+            wp = ops.pack(L.PACK_CONV_S1_DGRAD, w, cout, cin, BF)
         else:
             w = torch.randn((cout, cin, 4, 4), generator=g, device=dev) * 0.05
             wp = ops.pack(L.PACK_CONV_FWD, w, cout, cin, BF)

@@ -60,6 +60,12 @@ template <int RB> __device__ __forceinline__ int hswz(int row) {
 // GEOM 0: Conv2d k4 s2 (GEMM grid = output grid); GEOM 1: ConvTranspose2d k4 s2, one sub-pixel phase per block
 // (GEMM grid = input grid): phase (py, px) tap (ty, tx) reads input (gy + py - ty, gx + px - tx), so the stage of
 // ty holds the input rows gy0 + r + py - ty and its two taps tx read positions r * GW + gx + d, d = px - tx.
+// GEOM 2: Conv2d k4 s1 p1 (the PatchGAN's stride-1 conv, STCGAN/networks.py:172-178) on the GEMM grid = its input
+// grid (32 x 32; the output is 31 x 31: the last grid row and column are computed from zero padding and masked in
+// the epilogue); GEOM 3: its input gradient (GEMM grid = the 32 x 32 output, A = the 31 x 31 output gradient).
+// Tap (ky, kx) reads A row y + SG * ky + OF, column x + SG * kx + OF (SG, OF = 1, -1 / -1, 1): the stage of ky
+// holds the rows oy0 + r + SG * ky + OF and its four taps read positions r * GW + x + d, d = SG * kx + OF, in two
+// super-steps of two taps (every staged pixel serves four taps).
 template <int GEOM, int GW, int BN, bool BNB, int RB, int WM, int WN>
 __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(const GParams p) {
   using G = HaloGeom<RB, BN>;
@@ -69,12 +75,15 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   constexpr int KK = RB / 64;                                // 32-deep MFMA steps per K-step
   constexpr int AG = BM / (G::PR * NW), BG = BN / (G::PR * NW);  // DMA pieces per wave: A stage / B K-step
   constexpr int HALVES = 128 / RB;                           // stages per 64-channel chunk and (ky, parity) / ty
-  constexpr int SPC = (GEOM == 0 ? 8 : 2) * HALVES;          // super-steps per 64-channel chunk
+  constexpr bool S1 = GEOM >= 2;
+  constexpr int SG = GEOM == 3 ? -1 : 1, OF = GEOM == 3 ? 1 : -1;
+  constexpr int SPC = (GEOM == 1 ? 2 : 8) * HALVES;          // super-steps per 64-channel chunk
   constexpr int TH = BM / GW;
-  constexpr int NP = 2 * BG + AG, NG = 2 * KK * FM / 2;      // DMA pieces / 8-MFMA groups per super-step and wave
+  constexpr int AH = S1 ? AG / 2 : AG;                       // A pieces per super-step (S1: a stage over two)
+  constexpr int NP = 2 * BG + AH, NG = 2 * KK * FM / 2;      // DMA pieces / 8-MFMA groups per super-step and wave
   static_assert(GW % 16 == 0 && BM % GW == 0 && TM % GW == 0 && FN == 4 && FM % 2 == 0 && BG >= 1,
                 "whole output rows per tile and per wave, 16-row fragments inside an output row");
-  static_assert(NP >= NG, "every MFMA group issues a piece");
+  static_assert(S1 ? AG % 2 == 0 : NP >= NG, "every MFMA group issues a piece (S1: whole halves of a stage)");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -104,8 +113,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   const int prow = lane / G::CH;
   const int schunk = (lane % G::CH) ^ hswz<RB>(prow);  // (pieces are PR-row aligned: hswz(position) == hswz(prow))
   unsigned a_off[AG];
-  // pieces whose grid row is the image's first / last: conv-s2 ky = 0 / 3 and ConvT row offset -1 / +1 read padding
-  unsigned top = 0, bot = 0;
+  // pieces whose grid row is the image's first / last: conv-s2 ky = 0 / 3 and ConvT row offset -1 / +1 read padding;
+  // S1: the piece's grid row (a piece never straddles one), tested against each stage's row offset, and (GEOM 3) the
+  // lanes of the grid column past the A image's last (read as zeros)
+  unsigned top = 0, bot = 0, colpen = 0;
+  int oyg[AG];
 #pragma unroll
   for (int g = 0; g < AG; ++g) {
     const int pos = (wave * AG + g) * G::PR + prow;
@@ -116,6 +128,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
                (unsigned)(s_ * c) * (unsigned)p.a_ps + (unsigned)(schunk * 8);
     top |= (oy == 0 ? 1u : 0u) << g;
     bot |= (GEOM == 0 ? 2 * oy + 2 >= p.IH : oy == p.GH - 1) ? (1u << g) : 0u;
+    oyg[g] = oy;
+    colpen |= (c >= p.IW ? 1u : 0u) << g;
   }
   unsigned b_off[BG];
 #pragma unroll
@@ -129,6 +143,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   // (taps 1, 3); GEOM 1: ss = (chunk * 2 + ty) * HALVES + half (taps tx = 0, 1).  half = the 32-channel half of the
   // 64-channel chunk (RB = 64: the two halves of a pixel's 128-byte line back to back).  Its A stage goes to A slot
   // ss % 3, its two B K-steps to B pair ss & 1.
+  // S1: stage st = ((chunk * 4 + ky) * HALVES + half) (super-steps 2 st, 2 st + 1: taps kx = 0, 1 | 2, 3)
   auto ss_terms = [&](int ss, int& half, int& odd, int& ky, int& ch) {
     half = HALVES == 2 ? (ss & 1) : 0;
     const int t = HALVES == 2 ? ss >> 1 : ss;
@@ -136,10 +151,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
       odd = (t & 1) ^ 1;
       ky = (t >> 1) & 3;
       ch = t >> 3;
-    } else {  // (ky = ty)
+    } else if constexpr (GEOM == 1) {  // (ky = ty)
       odd = 0;
       ky = t & 1;
       ch = t >> 1;
+    } else {  // (ss = the stage)
+      odd = 0;
+      ky = t & 3;
+      ch = t >> 2;
     }
   };
   auto a_terms = [&](int ss, unsigned& delta, unsigned& pen) {
@@ -148,16 +167,22 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
     if constexpr (GEOM == 0) {
       delta = (unsigned)((ky - 1) * p.a_rs + odd * p.a_ps + ch * 64 + half * 32);
       pen = ky == 0 ? top : (ky == 3 ? bot : 0u);
-    } else {
+    } else if constexpr (GEOM == 1) {
       const int dy = py - ky;
       delta = (unsigned)(dy * p.a_rs + ch * 64 + half * 32);
       pen = dy < 0 ? top : (dy > 0 ? bot : 0u);
+    } else {  // (ss = the stage)
+      const int dy = SG * ky + OF;
+      delta = (unsigned)(dy * p.a_rs + ch * 64 + half * 32);
+      pen = colpen;
+#pragma unroll
+      for (int g = 0; g < AG; ++g) pen |= ((unsigned)(oyg[g] + dy) >= (unsigned)p.IH ? 1u : 0u) << g;
     }
   };
   auto b_k0 = [&](int ss, int j) {
     int half, odd, ky, ch;
-    ss_terms(ss, half, odd, ky, ch);
-    const int tap = GEOM == 0 ? 4 * ky + (odd ? 2 * j : 2 * j + 1) : 2 * ky + j;
+    ss_terms(S1 ? ss >> 1 : ss, half, odd, ky, ch);
+    const int tap = GEOM == 0 ? 4 * ky + (odd ? 2 * j : 2 * j + 1) : (GEOM == 1 ? 2 * ky + j : 4 * ky + 2 * (ss & 1) + j);
     return (unsigned)(tap * cin + ch * 64 + half * 32);
   };
   auto piece_a = [&](char* sA, unsigned delta, unsigned pen, int g) {
@@ -187,32 +212,35 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment read offsets: row (l & 15) of the fragment, chunk KK * 4 * kk... = 4 kk + (l >> 4); A rows shifted by d
-  // (fragment i adds 16 i rows, which keeps hswz: 16 is a multiple of 8)
+  // fragment read offsets: row (l & 15) of the fragment, chunk KK * 4 * kk... = 4 kk + (l >> 4); A rows shifted by
+  // d = di - 2 (fragment i adds 16 i rows, which keeps hswz: 16 is a multiple of 8)
   const int rl = lane & 15, kq = lane >> 4;
-  int a_rd[3][KK], b_rd[KK];
+  int a_rd[5][KK], b_rd[KK];
 #pragma unroll
   for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
-    for (int di = 0; di < 3; ++di) {
-      const int pr = wm * TM + rl + di - 1;
+    for (int di = 0; di < 5; ++di) {
+      const int pr = wm * TM + rl + di - 2;
       a_rd[di][kk] = pr * RB + (((4 * kk + kq) ^ hswz<RB>(pr)) * 16);
     }
     b_rd[kk] = (wn * TN + rl) * RB + (((4 * kk + kq) ^ hswz<RB>(rl)) * 16);
   }
   const bf16x8_t zero8 = {};
 
-  // one K-step (RB / 2 deep) from A stage sA / B K-step sBj, A rows shifted by D; dma(k) issues LDS-DMA piece k of
-  // the future stages after each 8 MFMAs
-  // D = 2: the shift is the runtime value dr (the ConvT taps: d = px - tx, block-uniform), one code path for both
-  // phase columns
+  // one K-step (RB / 2 deep) from A stage sA / B K-step sBj, A rows shifted by D in [-2, 2]; dma(k) issues LDS-DMA
+  // piece k of the future stages after each 8 MFMAs
+  // D = DRT: the shift is the runtime value dr in [-1, 1] (the ConvT taps: d = px - tx, block-uniform), one code
+  // path for both phase columns
+  constexpr int DRT = 9;
   auto kstep = [&](const char* sA, const char* sBj, auto Dc, auto dma, int dr = 0) {
     constexpr int D = decltype(Dc)::value;
-    const bool mlo = D == 2 ? (dr < 0 && rl == 0) : (D == -1 && rl == 0);   // left edge lane (d = -1)
-    const bool mhi = D == 2 ? (dr > 0 && rl == 15) : (D == 1 && rl == 15);  // right edge lane (d = +1)
+    constexpr bool RT = D == DRT;
+    // edge lanes: the first -d (d < 0) / last d (d > 0) rows of an output row read padding
+    const bool mlo = RT ? (dr < 0 && rl == 0) : (D < 0 && rl < -D);
+    const bool mhi = RT ? (dr > 0 && rl == 15) : (D > 0 && rl >= 16 - D);
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      const int ard = D == 2 ? (dr < 0 ? a_rd[0][kk] : (dr > 0 ? a_rd[2][kk] : a_rd[1][kk])) : a_rd[(D == 2 ? 0 : D) + 1][kk];
+      const int ard = RT ? (dr < 0 ? a_rd[1][kk] : (dr > 0 ? a_rd[3][kk] : a_rd[2][kk])) : a_rd[(RT ? 0 : D) + 2][kk];
       bf16x8_t fa[FM], fb[FN];
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sBj + b_rd[kk] + j * 16 * RB);
@@ -221,10 +249,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
         fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + ard + i * 16 * RB);
         // the fragment's first (d = -1) / last (d = +1) row is an output row's left / right edge: that lane's
         // operand is the zero padding, not the neighbouring row's pixel it addressed
-        if constexpr (D == -1 || D == 2) {
+        if constexpr (RT || D < 0) {
           if ((16 * i) % GW == 0) fa[i] = mlo ? zero8 : fa[i];
         }
-        if constexpr (D == 1 || D == 2) {
+        if constexpr (RT || D > 0) {
           if ((16 * i + 16) % GW == 0) fa[i] = mhi ? zero8 : fa[i];
         }
       }
@@ -246,30 +274,36 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   // slots ss - 1 read, B(ss + 1) and A(ss + 2), one piece per 8 MFMAs of super-step ss (a burst of pieces after
   // the barrier holds the waves at the texture unit before their first MFMA).
   const int nss = (cin / 64) * SPC;  // super-steps (even)
+  const int nst = S1 ? nss >> 1 : nss;  // A stages
   issue_a(0, 0);
   issue_b(0);
   issue_a(1, 1);
   int aslot = 0;
-  // one super-step; U = q * HALVES + half (compile-time parity and B pair = U & 1)
+  // one super-step; U = q * HALVES + half (compile-time parity and B pair = U & 1); S1: U = half * 2 + tap pair
   auto super_step = [&](int s, auto Uc) {
     constexpr int U = decltype(Uc)::value;
-    wait_ahead<AG>(s + 1 < nss ? 1 : 0);
+    constexpr int TP = S1 ? (U & 1) : 0;
+    const int st = S1 ? s >> 1 : s;  // this super-step's A stage
+    if constexpr (S1)  // (the previous super-step's A pieces -- or the prologue's A(1) -- may stay in flight)
+      wait_ahead<AH>(s == 0 ? 2 : (((s - 1) >> 1) + 2 < nst ? 1 : 0));
+    else
+      wait_ahead<AG>(s + 1 < nss ? 1 : 0);
     __builtin_amdgcn_s_barrier();
-    const bool nb = s + 1 < nss, na = s + 2 < nss;
+    const bool nb = s + 1 < nss, na = st + 2 < nst;
     const char* sA = smem + G::A0 + aslot * G::A;
     const char* sB = smem + ((U & 1) ? G::B1 : 0);
     char* rB = smem + ((U & 1) ? 0 : G::B1);  // B(s + 1): the other pair
     char* rA = smem + G::A0 + (aslot == 0 ? 2 : aslot - 1) * G::A;
     const unsigned bk0 = b_k0(s + 1, 0), bk1 = b_k0(s + 1, 1);
     unsigned adelta, apen;
-    a_terms(s + 2, adelta, apen);
+    a_terms(st + 2, adelta, apen);
     // pieces per super-step and wave: B(s + 1) = 2 K-steps x BG, then A(s + 2) = AG; MFMA group gi issues pieces
     // [gi * NP / NG, (gi + 1) * NP / NG)
     auto piece = [&](int k) {
       if (k < 2 * BG) {
         if (nb) piece_b(rB, k < BG ? bk0 : bk1, k / BG, k % BG);
       } else {
-        if (na) piece_a(rA, adelta, apen, k - 2 * BG);
+        if (na) piece_a(rA, adelta, apen, TP * AH + k - 2 * BG);
       }
     };
     auto group = [&](int gi) {
@@ -286,12 +320,17 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
         kstep(sA, sB, D_0{}, [&](int k) { group(k); });
         kstep(sA, sB + G::B, D_p1{}, [&](int k) { group(NG / 2 + k); });
       }
-    } else {  // ConvT: taps tx = 0 (d = px), 1 (d = px - 1)
-      using D_rt = std::integral_constant<int, 2>;
+    } else if constexpr (GEOM == 1) {  // ConvT: taps tx = 0 (d = px), 1 (d = px - 1)
+      using D_rt = std::integral_constant<int, DRT>;
       kstep(sA, sB, D_rt{}, [&](int k) { group(k); }, px);
       kstep(sA, sB + G::B, D_rt{}, [&](int k) { group(NG / 2 + k); }, px - 1);
+    } else {  // S1: taps kx = 2 TP, 2 TP + 1
+      using D_a = std::integral_constant<int, SG * (2 * TP) + OF>;
+      using D_b = std::integral_constant<int, SG * (2 * TP + 1) + OF>;
+      kstep(sA, sB, D_a{}, [&](int k) { group(k); });
+      kstep(sA, sB + G::B, D_b{}, [&](int k) { group(NG / 2 + k); });
     }
-    aslot = aslot == 2 ? 0 : aslot + 1;
+    if (!S1 || TP == 1) aslot = aslot == 2 ? 0 : aslot + 1;
   };
   for (int ss = 0; ss < nss; ss += 2 * HALVES) {  // (GEOM 1: U / HALVES selects nothing; one or two ty per pass)
     super_step(ss, std::integral_constant<int, 0>{});
@@ -320,21 +359,33 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
 // Eligible: Conv2d k4 s2 p1 on an even input (IH = 2 GH, IW = 2 GW) or ConvTranspose2d k4 s2 p1 (GEMM grid = the
 // input grid), whole-row tiles of 256 grid points (GW in {16, 32, 64}, GH a multiple of 256 / GW), 64-channel
 // chunks, 16-byte NHWC bf16 views (no split K).  N tile: 128 output channels, 64 for a ConvT with N <= 64.
+// Conv2d k4 s1 p1 (kinds STC_CONV_S1 / STC_CONV_S1_DGRAD): a 32-wide GEMM grid only (the PatchGAN's 32 x 32 input
+// at 256 x 256); the forward's GEMM grid is its input grid (output + 1 row and column).
 static int halo_bn(int kind, int Cout) { return kind == STC_CONVT_S2 && Cout <= 64 ? 64 : HB_BN; }
+static void halo_grid(int kind, int& GH, int& GW) {
+  if (kind == STC_CONV_S1) { ++GH; ++GW; }
+}
 
 bool halo_geometry_ok(int kind, int B, int GH, int GW, int Cin, int Cout) {
-  if ((kind != STC_CONV_S2 && kind != STC_CONVT_S2) || Cin % 64 != 0 || Cout % 8 != 0 || Cout > 2048) return false;
+  if (kind != STC_CONV_S2 && kind != STC_CONVT_S2 && kind != STC_CONV_S1 && kind != STC_CONV_S1_DGRAD) return false;
+  if (Cin % 64 != 0 || Cout % 8 != 0 || Cout > 2048) return false;
+  halo_grid(kind, GH, GW);
   if (!(GW == 16 || GW == 32 || GW == 64) || GH % (HB_BM / GW) != 0) return false;
+  if ((kind == STC_CONV_S1 || kind == STC_CONV_S1_DGRAD) && GW != 32) return false;
   return 16ll * Cin * Cout * 2 < (1ll << 31);
 }
 
 static long long halo_blocks(int kind, int B, int GH, int GW, int Cout) {
   const int bn = halo_bn(kind, Cout);
+  halo_grid(kind, GH, GW);
   return (long long)B * GH * GW / HB_BM * ((Cout + bn - 1) / bn) * (kind == STC_CONVT_S2 ? 4 : 1);
 }
 
 // The automatic plan takes the halo kernel when it fills the chip: >= 256 blocks (one 8-wave block per CU).
 bool halo_auto(int kind, int B, int GH, int GW, int Cin, int Cout) {
+#if STC_EXP_NOHALO  // diagnostic builds only: the im2col tiles everywhere
+  return false;
+#endif
   return halo_geometry_ok(kind, B, GH, GW, Cin, Cout) && halo_blocks(kind, B, GH, GW, Cout) >= 256;
 }
 
@@ -342,18 +393,32 @@ bool halo_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const 
   const bool convt = kind == STC_CONVT_S2;
   const int GH = convt ? x.H : y.H, GW = convt ? x.W : y.W;
   if (!halo_geometry_ok(kind, B, GH, GW, Cin, Cout)) return false;
-  if (!convt && (x.H != 2 * GH || x.W != 2 * GW)) return false;
+  if (kind == STC_CONV_S2 && (x.H != 2 * GH || x.W != 2 * GW)) return false;
+  if (kind == STC_CONV_S1 && (x.H != GH + 1 || x.W != GW + 1)) return false;
+  if (kind == STC_CONV_S1_DGRAD && (x.H != GH - 1 || x.W != GW - 1)) return false;
   if (x.cs != 1 || x.co % 8 != 0 || x.ps % 8 != 0 || x.rs % 8 != 0 || x.bs % 8 != 0) return false;
   return (long long)B * x.bs * 2 < (1ll << 31);
 }
 
-int halo_chunks(int kind, int B, int GH, int GW) { return B * GH * GW / HB_BM * (kind == STC_CONVT_S2 ? 4 : 1); }
+int halo_chunks(int kind, int B, int GH, int GW) {
+  halo_grid(kind, GH, GW);
+  return B * GH * GW / HB_BM * (kind == STC_CONVT_S2 ? 4 : 1);
+}
 
 // p: filled by bf16_conv_fwd (geometry, operands, output, epilogue options; vec_out set).  shape: 0 automatic,
 // 1 the 8-wave 160 KiB block, 2 the 4-wave 80 KiB block (force_plan {HALO_CFG, shape}: tests / A/B; N <= 64
 // ConvTs always take the 4-wave 256 x 64 block).
 int halo_launch(GParams& p, hipStream_t st, int shape) {
   const bool convt = p.nphase == 4;
+  const int geom = convt ? 1 : (p.in_stride == 2 ? 0 : (p.stepy > 0 ? 2 : 3));
+  if (geom == 2) {  // the GEMM grid = the input grid; its last row and column (no output pixel) masked
+    const int B = p.M / (p.GH * p.GW);
+    p.vmask = 1; p.vh = p.GH; p.vw = p.GW;
+    p.GH += 1; p.GW += 1;
+    p.M = B * p.GH * p.GW;
+    p.inv_ghw = 1.0f / (float)(p.GH * p.GW);
+    p.inv_gw = 1.0f / (float)p.GW;
+  }
   STC_REQUIRE(p.vec_out && !p.ws && (p.nphase == 1 || convt) && p.M % HB_BM == 0, "halo conv: bad launch parameters");
   const int bn = convt && p.N <= 64 ? 64 : HB_BN;
   p.mtiles = p.M / HB_BM;
@@ -384,12 +449,23 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
     }                                                       \
     break;
   main_timer_begin(st);
-  switch (p.GW) {
-    STC_H(16)
-    STC_H(32)
-    STC_H(64)
-    default:
-      return fail(-1, "halo conv: grid width %d", p.GW);
+  if (geom >= 2) {
+    STC_REQUIRE(p.GW == 32, "halo conv s1: grid width %d", p.GW);
+    if (geom == 2) {
+      if (two) { STC_HB(2, 32, 128, 64, 2, 2) }
+      else { STC_HB(2, 32, 128, 128, 4, 2) }
+    } else {
+      if (two) { STC_HB(3, 32, 128, 64, 2, 2) }
+      else { STC_HB(3, 32, 128, 128, 4, 2) }
+    }
+  } else {
+    switch (p.GW) {
+      STC_H(16)
+      STC_H(32)
+      STC_H(64)
+      default:
+        return fail(-1, "halo conv: grid width %d", p.GW);
+    }
   }
 #undef STC_H
 #undef STC_HB

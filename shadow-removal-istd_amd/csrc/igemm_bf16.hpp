@@ -53,6 +53,9 @@ struct GParams {
   char* c2;
   long long c2_bs, c2_rs;
   int c2_ps, c2_co;
+  // Padded GEMM grid (halo Conv2d k4 s1: the 31 x 31 output computed on its 32 x 32 input grid): vmask = 1 keeps
+  // only the grid points y < vh, x < vw -- the others are neither stored nor counted in the statistics.
+  int vmask, vh, vw;
 };
 
 // 8 bf16 (one uint4) -> act(v, slope) per element, rounded back to bf16 (as stc_bn_apply with no table)
@@ -199,16 +202,37 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
     // BatchNorm batch statistics of the tile, one shifted pass per wave over its accumulators
     // (shift = the column's value in the wave's first row: S1 = sum(x - shift), S2 = sum((x - shift)^2)),
     // then the WM row-waves merged through LDS into the tile's {count, 0, M2, mean} (Chan).
-    const int rows_w = min(TM, max(0, p.M - (m0 + wm * TM)));
-    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][3] {S1, S2, shift}
+    int rows_w = min(TM, max(0, p.M - (m0 + wm * TM)));
+    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][4] {S1, S2, shift, rows}
     float sh[FN], s1[FN], s2[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      sh[j] = __shfl(acc[0][j][0], cl, 64);
+      sh[j] = __shfl(acc[0][j][0], cl, 64);  // (the wave's first row: a kept grid point under vmask too)
       s1[j] = 0.f;
       s2[j] = 0.f;
     }
-    if (rows_w == TM) {
+    if (p.vmask) {  // padded grid: only the kept points (the wave's rows are inside the grid: M is whole tiles)
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * TM + 16 * i + rq + r;
+          const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
+          const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+          const bool keep = y < p.vh && x < p.vw;
+          cnt += keep ? 1 : 0;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const float d = keep ? acc[i][j][r] - sh[j] : 0.f;
+            s1[j] += d;
+            s2[j] = fmaf(d, d, s2[j]);
+          }
+        }
+      cnt += __shfl_xor(cnt, 16, 64);
+      cnt += __shfl_xor(cnt, 32, 64);
+      rows_w = cnt;
+    } else if (rows_w == TM) {
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -241,8 +265,8 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
     if (lane < 16) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        float* q = red + (wm * BN + wn * TN + 16 * j + lane) * 3;
-        q[0] = s1[j]; q[1] = s2[j]; q[2] = sh[j];
+        float* q = red + (wm * BN + wn * TN + 16 * j + lane) * 4;
+        q[0] = s1[j]; q[1] = s2[j]; q[2] = sh[j]; q[3] = (float)rows_w;
       }
     }
     __syncthreads();
@@ -253,9 +277,9 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
       float cnt = 0.f, mean = 0.f, m2 = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
-        const float nw = (float)min(TM, max(0, p.M - (m0 + w * TM)));
+        const float* q = red + (w * BN + c) * 4;
+        const float nw = q[3];
         if (nw <= 0.f) continue;
-        const float* q = red + (w * BN + c) * 3;
         const float mw = q[2] + q[0] / nw, m2w = fmaxf(q[1] - q[0] * (q[0] / nw), 0.f);
         const float nt = cnt + nw, dl = mw - mean;
         mean += dl * (nw / nt);
@@ -294,7 +318,7 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
         const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
         const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
         const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
-        ok[u] = in && bnb_on && oy < p.bxH && ox < p.bxW;
+        ok[u] = in && bnb_on && oy < p.bxH && ox < p.bxW && (!p.vmask || (y < p.vh && x < p.vw));
         const int oyc = ok[u] ? oy : 0, oxc = ok[u] ? ox : 0;
         xr[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.bx) + (long long)b * p.bx_bs +
                                                 (long long)oyc * p.bx_rs + (long long)oxc * p.bx_ps + p.bx_co + nchc);
@@ -344,7 +368,9 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
         const unsigned off = (unsigned)b * (unsigned)p.c_bs + (unsigned)oy * (unsigned)p.c_rs + (unsigned)ox * (unsigned)p.c_ps +
                              cbase;
         const uint4 tv = *reinterpret_cast<const uint4*>(tl + (r0 + it * RS) * PITCH + cc * 16);
-        if (p.act_n == 0) {
+        if (p.vmask && (y >= p.vh || x >= p.vw)) {
+          // (a padding point of the grid: not stored)
+        } else if (p.act_n == 0) {
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = tv;
         } else {
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = act_bf16x8(tv, p.act_s1);
@@ -387,6 +413,7 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
         if (m < p.M && n < p.N) {
           const int b = fast_div(m, GHW, p.inv_ghw), rem = m - b * GHW;
           const int y = fast_div(rem, p.GW, p.inv_gw), x = rem - y * p.GW;
+          if (p.vmask && (y >= p.vh || x >= p.vw)) continue;
           const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
           const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = tv[u];

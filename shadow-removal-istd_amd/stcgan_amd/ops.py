@@ -199,9 +199,11 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
         return "narrow_tiled_kernel", True
     if cfg == HALO_CFG:  # the LDS-resident input halo kernels (csrc/halo_bf16.hip): template as rocprof names it
         convt = kind == L.CONVT_S2
-        blocks = B * gh * gw // 256 * ((cout + bn - 1) // bn) * (4 if convt else 1)
+        geom = {L.CONV_S2: 0, L.CONVT_S2: 1, L.CONV_S1: 2, L.CONV_S1_DGRAD: 3}[kind]
+        vh, vw = (gh + 1, gw + 1) if kind == L.CONV_S1 else (gh, gw)  # (the s1 forward: its input grid)
+        blocks = B * vh * vw // 256 * ((cout + bn - 1) // bn) * (4 if convt else 1)
         rb, wm, wn = (64, 4, 1) if bn == 64 else ((64, 2, 2) if blocks >= 512 else (128, 4, 2))
-        return (f"halo_conv_kernel<{int(convt)}, {gw}, {bn}, {str(bnb).lower()}, {rb}, {wm}, {wn}>", True)
+        return (f"halo_conv_kernel<{geom}, {vw}, {bn}, {str(bnb).lower()}, {rb}, {wm}, {wn}>", True)
     if cfg >= 0:
         t = _BF16_TILES[cfg]
         if len(t) > 6:  # loader-wave blocks

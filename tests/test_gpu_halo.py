@@ -262,3 +262,117 @@ def test_halo_convT_bn_backward(case):
         assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm} {case}: {err:.3e}"
     err = float((dx1.float() - dx2.float()).abs().max())
     assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx {case}: {err:.3e}"
+
+
+# ---- Conv2d k4 s1 p1 (the PatchGAN's stride-1 layer, STCGAN/networks.py:172-178) and its input gradient
+
+def run_s1(kind, B, x, w, Cin, Cout, out_hw, force):
+    """stc_conv_fwd_ex (with statistics) of kind CONV_S1 / CONV_S1_DGRAD on NCHW fp32 x (w: the conv weight)."""
+    pack = L.PACK_CONV_FWD if kind == L.CONV_S1 else L.PACK_CONV_S1_DGRAD
+    xb = nhwc(x).to(DEV, BF)
+    wp = ops.pack(pack, w.to(DEV), Cout, Cin, BF)
+    Ho, Wo = out_hw
+    y = torch.full((B, Ho, Wo, Cout), float("nan"), device=DEV, dtype=BF)
+    part, nch = ops.conv_stats(kind, B, L.nhwc_view(xb), Cin, wp, Cout, L.nhwc_view(y), BF, force=force)
+    _, nq, plan = ops.conv_query(kind, B, Ho, Wo, Cin, Cout, BF, force=force)
+    assert nq == nch
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV)
+    t = torch.empty((2, Cout), device=DEV)
+    mean, rstd = ops.bn_finalize_part(part, nch, Cout, bn, t[0], t[1])
+    var = 1.0 / rstd.double() ** 2 - bn.eps
+    torch.cuda.synchronize()
+    return nchw(y.float()), mean.double(), var, plan
+
+
+S1CASES = [  # B, conv Cin, conv Cout (32 x 32 -> 31 x 31)
+    (1, 64, 128),
+    (2, 128, 200),   # ragged N
+    (1, 256, 512),   # the PatchGAN layer's channels
+]
+
+
+@pytest.mark.parametrize("shape", [HALO, HALO2], ids=["8wave", "4wave"])
+@pytest.mark.parametrize("case", S1CASES, ids=lambda c: "x".join(map(str, c)))
+def test_halo_conv_s1(case, shape):
+    """Forward on the 32 x 32 grid with the last row / column masked: output, and statistics over the 31 x 31
+    pixels only."""
+    B, Cin, Cout = case
+    x = q(rnd(B, Cin, 32, 32, seed=71, dev=DEV))
+    w = q(rnd(Cout, Cin, 4, 4, seed=72, scale=0.05, dev=DEV))
+    ref = F.conv2d(x, w, None, 1, 1)
+    y, mean, var, plan = run_s1(L.CONV_S1, B, x, w, Cin, Cout, (31, 31), shape)
+    assert plan[4] == ops.HALO_CFG
+    check(y, ref, mean, var, f"halo s1 {case}")
+    y2, _, _, plan2 = run_s1(L.CONV_S1, B, x, w, Cin, Cout, (31, 31), (0, 1))
+    assert plan2[4] == 0
+    assert float((y - y2).abs().max()) <= 1e-2 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("shape", [HALO, HALO2], ids=["8wave", "4wave"])
+@pytest.mark.parametrize("case", S1CASES, ids=lambda c: "x".join(map(str, c)))
+def test_halo_conv_s1_dgrad(case, shape):
+    """Input gradient dx = conv_transpose2d(dy, w, stride 1, pad 1): 31 x 31 x Cout -> 32 x 32 x Cin."""
+    B, Cin, Cout = case
+    if Cout % 64:
+        pytest.skip("the reduction (conv Cout) needs 64-channel chunks")
+    dy = q(rnd(B, Cout, 31, 31, seed=73, dev=DEV))
+    w = q(rnd(Cout, Cin, 4, 4, seed=74, scale=0.05, dev=DEV))
+    ref = F.conv_transpose2d(dy, w, None, 1, 1)
+    y, mean, var, plan = run_s1(L.CONV_S1_DGRAD, B, dy, w, Cout, Cin, (32, 32), shape)
+    assert plan[4] == ops.HALO_CFG
+    check(y, ref, mean, var, f"halo s1 dgrad {case}")
+    y2, _, _, plan2 = run_s1(L.CONV_S1_DGRAD, B, dy, w, Cout, Cin, (32, 32), (0, 1))
+    assert plan2[4] == 0
+    assert float((y - y2).abs().max()) <= 1e-2 * float(ref.abs().max())
+
+
+def test_halo_s1_plan_automatic_at_train_size():
+    assert ops.conv_query(L.CONV_S1, 32, 31, 31, 256, 512, BF)[2][4] == ops.HALO_CFG
+    assert ops.conv_query(L.CONV_S1_DGRAD, 32, 32, 32, 512, 256, BF)[2][4] == ops.HALO_CFG
+    # other grids keep the im2col tiles
+    assert ops.conv_query(L.CONV_S1, 32, 15, 15, 256, 512, BF)[2][4] != ops.HALO_CFG
+    assert ops.conv_query(L.CONV_S1, 32, 30, 30, 512, 1, BF)[2][4] != ops.HALO_CFG
+
+
+def test_halo_conv_s1_full_size():
+    """The PatchGAN's layer 4 forward at the bench size (bs 32, 32x32x256 -> 31x31x512), automatic plan."""
+    B, Cin, Cout = 32, 256, 512
+    x = q(rnd(B, Cin, 32, 32, seed=75, dev=DEV))
+    w = q(rnd(Cout, Cin, 4, 4, seed=76, scale=0.05, dev=DEV))
+    ref = F.conv2d(x, w, None, 1, 1)
+    y, mean, var, plan = run_s1(L.CONV_S1, B, x, w, Cin, Cout, (31, 31), None)
+    assert plan[4] == ops.HALO_CFG
+    check(y, ref, mean, var, "halo s1 full size")
+
+
+def test_halo_conv_s1_dgrad_bn_backward():
+    """The stride-1 layer's input gradient at the bench size with the fused BatchNorm-backward sums of the layer
+    below (PatchGAN layer 3's BN, 256 channels)."""
+    B, Cin, Cout, C = 32, 512, 256, 256   # GEMM: 31x31x512 -> 32x32x256
+    assert ops.conv_query(L.CONV_S1_DGRAD, B, 32, 32, Cin, Cout, BF)[2][4] == ops.HALO_CFG
+    wt = q(rnd(Cin, Cout, 4, 4, seed=81, scale=0.05, dev=DEV))  # conv weight [512][256]
+    w = ops.pack(L.PACK_CONV_S1_DGRAD, wt, Cout, Cin, BF)
+    dy = q(rnd(B, Cin, 31, 31, seed=82, scale=0.5, dev=DEV))
+    dyb = nhwc(dy).to(BF)
+    x = torch.randn((B, 32, 32, C), generator=torch.Generator(device=DEV).manual_seed(83), device=DEV).to(BF)
+    bn = _BNT(C, 85)
+    st = (bn.scale, bn.shift, bn.mean, bn.rstd)
+    out1 = torch.zeros((B, 32, 32, Cout), device=DEV, dtype=BF)
+    dx1 = torch.empty((B, 32, 32, C), device=DEV, dtype=BF)
+    dg1, db1 = ops.conv_bn_backward(L.CONV_S1_DGRAD, B, L.nhwc_view(dyb), Cin, w, Cout, L.nhwc_view(out1), BF,
+                                    bn_x=L.nhwc_view(x), C=C, bn_state=st, gamma=bn.gamma, s_self=0.2,
+                                    dxv=L.nhwc_view(dx1))
+    out2 = torch.zeros((B, 32, 32, Cout), device=DEV, dtype=BF)
+    ops.conv(L.CONV_S1_DGRAD, B, L.nhwc_view(dyb), Cin, w, Cout, L.nhwc_view(out2), BF)
+    dx2 = torch.empty((B, 32, 32, C), device=DEV, dtype=BF)
+    dg2, db2 = ops.bn_backward(B, L.nhwc_view(x), C, BF, L.nhwc_view(dx2), g1=L.nhwc_view(out2), s1=0.2,
+                               bn_state=(bn.scale, bn.shift, bn.mean, bn.rstd, bn.gamma))
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
+    ref = F.conv_transpose2d(dy, wt, None, 1, 1)
+    assert float((nchw(out1.float()) - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+    for a, b_, nm in ((dg1, dg2, "dgamma"), (db1, db2, "dbeta")):
+        err = float((a - b_).abs().max())
+        assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm}: {err:.3e}"
+    err = float((dx1.float() - dx2.float()).abs().max())
+    assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx: {err:.3e}"
