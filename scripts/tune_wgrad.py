@@ -19,7 +19,7 @@ from stcgan_amd import ops  # noqa: E402
 from stcgan_amd.stcgan import STCGAN  # noqa: E402
 
 BF = torch.bfloat16
-CFGS = range(8)
+CFGS = range(10)
 SPLITS = tuple(int(v) for v in os.environ.get("WG_SPLITS", "0,1,2,4,8,16,32,64").split(","))
 MIN_P = int(os.environ.get("WG_MIN_P", "0"))
 WG_CFGS = os.environ.get("WG_CFGS")
