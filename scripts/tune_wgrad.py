@@ -19,7 +19,7 @@ from stcgan_amd import ops  # noqa: E402
 from stcgan_amd.stcgan import STCGAN  # noqa: E402
 
 BF = torch.bfloat16
-CFGS = range(10)
+CFGS = range(9)
 SPLITS = tuple(int(v) for v in os.environ.get("WG_SPLITS", "0,1,2,4,8,16,32,64").split(","))
 MIN_P = int(os.environ.get("WG_MIN_P", "0"))
 WG_CFGS = os.environ.get("WG_CFGS")
@@ -33,7 +33,8 @@ def record():
 
     def wgrad(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro=None, dslope=None, gpro=None, gslope=None, device=None,
               **kw):
-        if dt == BF and dpro is None and gpro is None and dslope is None and gslope is None and not kw.get("rows"):
+        if (dt == BF and dpro is None and gpro is None and dslope is None and gslope is None
+                and not (kw.get("rows") and kw["rows"] < R)):
             k = (B, stride, Dv.H, Dv.W, Gv.H, Gv.W, R, Cg, Cg_out)
             probs[k] = probs.get(k, 0) + 1
         return orig(B, stride, Dv, R, Gv, Cg, Cg_out, dt, dpro, dslope, gpro, gslope, device, **kw)

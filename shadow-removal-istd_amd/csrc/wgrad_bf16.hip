@@ -467,252 +467,6 @@ __global__ void __launch_bounds__(64 * (WM * WN + LD), 2) wgrad_bf16_ld_kernel(c
   wgrad_bf16_body<BM, BN, WM, WN, SWAP, FAST, LD, NST>(p);
 }
 
-// ---- v2: eight 64x64 compute waves per block (two per SIMD), every wave also issuing the LDS-DMA
-// Tiles 256x128 (4x2 waves) / 128x256 (2x4), one block per CU; 3-stage ring: step s + 2's pieces are issued
-// one or two per 8 MFMAs of step s (no burst after the barrier), a counted vmcnt leaves step s + 1's in flight,
-// one barrier per step (64 MFMAs per SIMD between barriers).  Rows = D (SWAP = false), columns = Gcol.
-template <int BM, int BN, int WM, int WN, bool FAST>
-__global__ void __launch_bounds__(64 * WM * WN, 1) wgrad_bf16_v2_kernel(const WbParams p) {
-  constexpr int NW = WM * WN, NST = 3;
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int CHA = BM / 8, CHB = BN / 8;
-  constexpr int ROWA = BM * 2, ROWB = BN * 2;
-  constexpr int PA = WB_BK * ROWA / 1024, PB = WB_BK * ROWB / 1024;
-  constexpr int TILEA = WB_BK * ROWA, TILEB = WB_BK * ROWB, STAGE = TILEA + TILEB;
-  constexpr int IA = PA / NW, IB = PB / NW, P = IA + IB;  // pieces per wave per step
-  constexpr int NG = 2 * FM / 2;                           // 8-MFMA groups per step (2 kk x FM / 2)
-  static_assert(TM == 64 && TN == 64 && IA * NW == PA && IB * NW == PB && IB >= 1, "v2 tile");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int nwg = p.mtiles * p.ntiles;
-  const int nlin = nwg * (int)gridDim.z;
-  int bid = blockIdx.x + (int)blockIdx.z * nwg;
-  {  // XCD-aware order over (split, tile), as wgrad_bf16_body
-    const int xcd = bid & 7, q = nlin >> 3, r = nlin & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  const int split = bid / nwg;
-  bid -= split * nwg;
-  const int mt = bid / p.ntiles, nt = bid % p.ntiles;
-  const int a0 = mt * BM, b0 = nt * BN;
-  const int pbeg = split * p.pchunk;
-  const int pend = min(p.P, pbeg + p.pchunk);
-  const int nsteps = (pend - pbeg + WB_BK - 1) / WB_BK;
-  const int GHW = p.GH * p.GW;
-  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)p.d, (short)0, (int)p.d_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)p.g, (short)0, (int)p.g_bytes, 0x00020000);
-  const unsigned OOBV = 0x80000000u;
-
-  // ---- per-piece lane roles (piece k of this wave: A pieces wave + NW*i, B pieces wave + NW*i)
-  struct Role { int chan_off, dy, dx; unsigned pen; };
-  auto role = [&](bool is_g, int ch_per_row, int piece, int first) -> Role {
-    const int row = piece * (64 / ch_per_row) + lane / ch_per_row;
-    const int chunk = (lane % ch_per_row) ^ wswz_rt(ch_per_row, row);
-    Role ro{};
-    if (!is_g) {
-      const int r = first + chunk * 8;
-      ro.chan_off = p.d_co + r;
-      ro.pen = r < p.R ? 0u : OOBV;
-    } else {
-      const int col = first + chunk * 8;
-      const int tap = col / p.Cg;
-      ro.chan_off = p.g_co + col - tap * p.Cg;
-      ro.dy = (tap >> 2) - 1;
-      ro.dx = (tap & 3) - 1;
-      ro.pen = col < p.Ncol ? 0u : OOBV;
-    }
-    return ro;
-  };
-  Role ra_[IA], rb_[IB];
-#pragma unroll
-  for (int i = 0; i < IA; ++i) ra_[i] = role(false, CHA, wave + NW * i, a0);
-#pragma unroll
-  for (int i = 0; i < IB; ++i) rb_[i] = role(true, CHB, wave + NW * i, b0);
-
-  // FAST (pmode 1..3): lane constants relative to a scalar step base
-  struct Lc { unsigned off; int cy, cx; unsigned pen; };
-  auto lane_const = [&](bool is_g, const Role& ro, int rows_pp, int piece) -> Lc {
-    const int d = piece * rows_pp + lane / (64 / rows_pp);
-    int db = 0, doy = 0, dox = d;
-    if (p.pmode == 2) { doy = d >> p.lg_gw; dox = d & (p.GW - 1); }
-    else if (p.pmode == 3) { db = d >> p.lg_ghw; const int r = d & (GHW - 1); doy = r >> p.lg_gw; dox = r & (p.GW - 1); }
-    Lc c;
-    if (!is_g) {
-      c.off = (unsigned)db * (unsigned)p.d_bs + (unsigned)doy * (unsigned)p.d_rs + (unsigned)dox * (unsigned)p.d_ps +
-              (unsigned)ro.chan_off;
-      c.cy = 0; c.cx = 0;
-      c.pen = ro.pen;
-    } else {
-      c.cy = doy * p.stride + ro.dy;
-      c.cx = dox * p.stride + ro.dx;
-      c.off = (unsigned)db * (unsigned)p.g_bs + (unsigned)c.cy * (unsigned)p.g_rs + (unsigned)c.cx * (unsigned)p.g_ps +
-              (unsigned)ro.chan_off;
-      if (ro.pen) c.cy = 1 << 30;
-      c.pen = 0;
-    }
-    return c;
-  };
-  Lc la_[FAST ? IA : 1], lb_[FAST ? IB : 1];
-  if constexpr (FAST) {
-#pragma unroll
-    for (int i = 0; i < IA; ++i) la_[i] = lane_const(false, ra_[i], 64 / CHA, wave + NW * i);
-#pragma unroll
-    for (int i = 0; i < IB; ++i) lb_[i] = lane_const(true, rb_[i], 64 / CHB, wave + NW * i);
-  }
-  // the step base of the next step to issue (FAST: scalar; general: its index)
-  struct Base { unsigned sd, sg, tail; int sy, sx, s; };
-  int sb0 = 0, soy0 = 0, sox0 = 0, snext = 0;
-  if constexpr (FAST) {
-    sb0 = pbeg / GHW;
-    const int r0 = pbeg - sb0 * GHW;
-    soy0 = r0 / p.GW;
-    sox0 = r0 - soy0 * p.GW;
-  }
-  auto next_base = [&]() -> Base {
-    Base b{};
-    b.s = snext++;
-    if constexpr (FAST) {
-      const int p0 = pbeg + b.s * WB_BK;
-      b.tail = p0 + WB_BK > pend ? (unsigned)(pend - p0) : 0u;
-      b.sy = soy0 * p.stride; b.sx = sox0 * p.stride;
-      b.sd = (unsigned)sb0 * (unsigned)p.d_bs + (unsigned)soy0 * (unsigned)p.d_rs + (unsigned)sox0 * (unsigned)p.d_ps;
-      b.sg = (unsigned)sb0 * (unsigned)p.g_bs + (unsigned)b.sy * (unsigned)p.g_rs + (unsigned)b.sx * (unsigned)p.g_ps;
-      if (p.pmode == 1) {
-        sox0 += WB_BK;
-        if (sox0 >= p.GW) { sox0 = 0; if (++soy0 >= p.GH) { soy0 = 0; ++sb0; } }
-      } else if (p.pmode == 2) {
-        soy0 += WB_BK >> p.lg_gw;
-        if (soy0 >= p.GH) { soy0 = 0; ++sb0; }
-      } else {
-        sb0 += WB_BK >> p.lg_ghw;
-      }
-    }
-    return b;
-  };
-  // piece k (< P) of the step with base bs into stage buffer st
-  auto piece = [&](const Base& bs, char* stg, int k) {
-    const bool is_a = k < IA;
-    const int i = is_a ? k : k - IA;
-    const int pc = wave + NW * i;
-    const int rows_pp = 64 / (is_a ? CHA : CHB);
-    char* dst = stg + (is_a ? 0 : TILEA) + pc * 1024;
-    const int d = pc * rows_pp + lane / (64 / rows_pp);
-    if constexpr (FAST) {
-      unsigned pen = 0;
-      if (bs.tail) pen = (unsigned)d < bs.tail ? 0u : OOBV;
-      if (is_a) {
-        wdma16(rd, dst, ((bs.sd + la_[i].off) * 2u) | pen | la_[i].pen);
-      } else {
-        const Lc& c = lb_[i];
-        const unsigned ipen = ((unsigned)(bs.sy + c.cy) < (unsigned)p.IH && (unsigned)(bs.sx + c.cx) < (unsigned)p.IW) ? 0u : OOBV;
-        wdma16(rg, dst, ((bs.sg + c.off) * 2u) | pen | ipen);
-      }
-    } else {
-      const int pix = pbeg + bs.s * WB_BK + d;
-      const unsigned ppen = pix < pend ? 0u : OOBV;
-      const int pp = pix < pend ? pix : pbeg;
-      const int b = fdiv(pp, GHW, p.inv_ghw);
-      const int rem = pp - b * GHW;
-      const int oy = fdiv(rem, p.GW, p.inv_gw);
-      const int ox = rem - oy * p.GW;
-      if (is_a) {
-        const Role& ro = ra_[i];
-        const unsigned off = (((unsigned)b * (unsigned)p.d_bs + (unsigned)oy * (unsigned)p.d_rs + (unsigned)ox * (unsigned)p.d_ps +
-                               (unsigned)ro.chan_off) * 2u) | ppen | ro.pen;
-        wdma16(rd, dst, off);
-      } else {
-        const Role& ro = rb_[i];
-        const int iy = oy * p.stride + ro.dy, ix = ox * p.stride + ro.dx;
-        const unsigned ipen = ((unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW) ? 0u : OOBV;
-        const unsigned off = (((unsigned)b * (unsigned)p.g_bs + (unsigned)iy * (unsigned)p.g_rs + (unsigned)ix * (unsigned)p.g_ps +
-                               (unsigned)ro.chan_off) * 2u) | ppen | ro.pen | ipen;
-        wdma16(rg, dst, off);
-      }
-    }
-  };
-
-  floatx4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int kq = lane >> 4, q = (lane & 15) >> 2, pcol = lane & 3;
-  auto tr_off = [&](int row, int colbase, int rowbytes, int ch) {
-    const int col = colbase + 4 * pcol;
-    return row * rowbytes + 16 * ((col >> 3) ^ wswz_rt(ch, row)) + 2 * (col & 7);
-  };
-
-  // prologue: steps 0 and 1
-  if (nsteps > 0) {
-    const Base b = next_base();
-#pragma unroll
-    for (int k = 0; k < P; ++k) piece(b, smem, k);
-  }
-  if (nsteps > 1) {
-    const Base b = next_base();
-#pragma unroll
-    for (int k = 0; k < P; ++k) piece(b, smem + STAGE, k);
-  }
-  int cur = 0;
-  for (int s = 0; s < nsteps; ++s) {
-    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const bool refill = s + 2 < nsteps;
-    Base nb{};
-    if (refill) nb = next_base();
-    char* rst = smem + (cur == 0 ? 2 : cur - 1) * STAGE;  // stage of step s + 2 (= step s - 1's)
-    const char* sA = smem + cur * STAGE;
-    const char* sB = sA + TILEA;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int rowa = kk * 32 + 8 * kq + q;
-      wbf16x8 fa[FM], fb[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int cb = wm * TM + 16 * i;
-        const w4i16 v8[2] = {wtr16(sA + tr_off(rowa, cb, ROWA, CHA)), wtr16(sA + tr_off(rowa + 4, cb, ROWA, CHA))};
-        fa[i] = __builtin_bit_cast(wbf16x8, v8);
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int cb = wn * TN + 16 * j;
-        const w4i16 v8[2] = {wtr16(sB + tr_off(rowa, cb, ROWB, CHB)), wtr16(sB + tr_off(rowa + 4, cb, ROWB, CHB))};
-        fb[j] = __builtin_bit_cast(wbf16x8, v8);
-      }
-#pragma unroll
-      for (int h = 0; h < FM / 2; ++h) {
-#pragma unroll
-        for (int i = 2 * h; i < 2 * h + 2; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = exp_mfma(fa[i], fb[j], acc[i][j]);
-        const int gi = kk * (FM / 2) + h;
-        if (refill) {
-#pragma unroll
-          for (int k = gi * P / NG; k < (gi + 1) * P / NG; ++k) piece(nb, rst, k);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * FN, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, (P + NG - 1) / NG, 0);
-      }
-    }
-    cur = cur == NST - 1 ? 0 : cur + 1;
-  }
-#if STC_EXP_NOEPI
-  {
-    float s_ = 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) s_ += acc[i][j][0] + acc[i][j][3];
-    if (s_ == 1.2345f) p.ws[threadIdx.x] = s_;
-    return;
-  }
-#endif
-  wgrad_store<BM, BN, WM, WN, false>(p, acc, a0, b0, split);
-}
-
 // ---- halo weight gradient of the stride-2 geometry (Conv2d k4 s2: D = dy on the output grid, G = x; the
 // ConvTranspose2d k4 s2 layers: D = x on the input grid, G = dy): dW[r][tap][ci] = sum_p D[p][r] * G[2p + tap offset][ci]
 // with tap (ky, kx) at G row 2y + ky - 1, column 2x + kx - 1.  The im2col column operand stages every G pixel once per
@@ -724,12 +478,16 @@ __global__ void __launch_bounds__(64 * WM * WN, 1) wgrad_bf16_v2_kernel(const Wb
 // the transposed reads of K rows q and q + 8 hit different banks.  Per K-step: D 64 px x 128 channels (16 KB) +
 // the patch (<= 20 KB) against 128 x 256 x 64 MACs -- 2x the MACs per staged byte of the 128 x 128 im2col tile.
 // Block: 4 compute waves (2 x 2, 64 x 128 each: 4 row x 8 tap fragments) + 4 loader waves, 4-stage ring (144 KiB).
-template <int TC>
+// S1: the PatchGAN's Conv2d k4 s1 p1 (D = dy 31 x 31, G = x 32 x 32; STCGAN/networks.py:172-178) on a virtual 32 x 32
+// D grid whose last row and column read as zeros: tap (ky, kx) at G row y + ky - 1, column x + kx - 1, one plane of
+// patch columns x0 - 1 .. x0 + TC + 1, patch rows y0 - 1 .. y0 + TR + 1.
+template <int TC, bool S1 = false>
 struct WhGeom {
   static constexpr int TR = 64 / TC;                 // grid rows per K-step
-  static constexpr int NR = 2 * TR + 2;              // patch rows
-  static constexpr int NPOS = TC + 16;               // positions per plane line (>= TC + 1, whole 16-groups)
-  static constexpr int SLOTS = NR * 2 * NPOS;        // 32-B slots
+  static constexpr int NR = S1 ? TR + 3 : 2 * TR + 2;  // patch rows
+  static constexpr int NPL = S1 ? 1 : 2;             // column planes
+  static constexpr int NPOS = TC + 16;               // positions per plane line (>= TC + 3, whole 16-groups)
+  static constexpr int SLOTS = NR * NPL * NPOS;      // 32-B slots
   static constexpr int PBR = (SLOTS + 31) / 32;      // 1 KiB pieces of the patch
   static constexpr int PB = (PBR + 3) / 4 * 4;       // padded to whole pieces per loader wave
   static constexpr int TILEA = 64 * 128 * 2, TILEB = PB * 1024, STAGE = TILEA + TILEB;
@@ -738,9 +496,11 @@ static_assert(4 * WhGeom<64>::STAGE <= 163840 && 4 * WhGeom<32>::STAGE <= 163840
               "halo wgrad LDS");
 __device__ __forceinline__ int wh_perm(int pos) { return pos ^ (((pos >> 3) & 1) << 2); }
 
-template <int TC>
+template <int TC, bool S1>
 __global__ void __launch_bounds__(512, 1) wgrad_halo_kernel(const WbParams p) {
-  using G = WhGeom<TC>;
+  using G = WhGeom<TC, S1>;
+  // (S1: p.GH / p.GW are the virtual grid, p.IH / p.IW the G image; D pixels outside D.H = GH - 1, D.W = GW - 1
+  // are zeros)
   constexpr int BM = 128, NW = 4, NL = 4, NST = 4;
   constexpr int FM = 4, FN = 8;                      // compute wave tile 64 x 128 (8 taps x 16 channels)
   constexpr int CHA = 16, ROWA = 256;
@@ -776,7 +536,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_kernel(const WbParams p) {
       const int chunk = (lane % CHA) ^ wswz<16>(d);
       const int r = a0 + chunk * 8;
       aoff[i] = (unsigned)((d / TC) * p.d_rs + (d % TC) * p.d_ps + p.d_co + r);
-      apen[i] = r < p.R ? 0u : OOBV;
+      apen[i] = r < p.R && (!S1 || d % TC < p.GW - 1) ? 0u : OOBV;
     }
     // B (patch) pieces: slot -> (line = row * 2 + plane, position); lane & 1 = the 16-byte half of the 32-B slot
     unsigned boff[IB];
@@ -786,10 +546,10 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_kernel(const WbParams p) {
       const int pc = lw + NL * i;
       const int slot = pc * 32 + (lane >> 1);
       const int line = slot / G::NPOS, pos = wh_perm(slot % G::NPOS);
-      const int r = line >> 1, plane = line & 1;
-      const bool ok = line < 2 * G::NR && pos <= TC;
+      const int r = line / G::NPL, plane = line % G::NPL;
+      const bool ok = line < G::NPL * G::NR && pos <= (S1 ? TC + 2 : TC);
       brow[i] = ok ? r - 1 : (1 << 20);
-      bcol[i] = 2 * pos + plane - 1;
+      bcol[i] = S1 ? pos - 1 : 2 * pos + plane - 1;
       boff[i] = (unsigned)(brow[i] * p.g_rs + bcol[i] * p.g_ps + p.g_co + c0 + 8 * (lane & 1));
     }
     // step base (b, y0, x0), advanced by 64 pixels per issued step
@@ -802,19 +562,21 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_kernel(const WbParams p) {
       char* sB = sA + G::TILEA;
       const int p0 = pbeg + s * 64;
       const unsigned tail = p0 + 64 > pend ? (unsigned)(pend - p0) : 64u;
+      constexpr int SG = S1 ? 1 : 2;  // G pixels per grid step
       const unsigned bd = (unsigned)sb * (unsigned)p.d_bs + (unsigned)sy * (unsigned)p.d_rs + (unsigned)sx * (unsigned)p.d_ps;
-      const unsigned bg = (unsigned)sb * (unsigned)p.g_bs + (unsigned)(2 * sy) * (unsigned)p.g_rs +
-                          (unsigned)(2 * sx) * (unsigned)p.g_ps;
+      const unsigned bg = (unsigned)sb * (unsigned)p.g_bs + (unsigned)(SG * sy) * (unsigned)p.g_rs +
+                          (unsigned)(SG * sx) * (unsigned)p.g_ps;
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
         const int pc = lw + NL * i;
         const unsigned d = (unsigned)(pc * 4 + lane / CHA);
-        wdma16(rd, sA + pc * 1024, ((bd + aoff[i]) * 2u) | apen[i] | (d < tail ? 0u : OOBV));
+        const bool rowok = !S1 || sy + (int)d / TC < p.GH - 1;  // (S1: the virtual last grid row)
+        wdma16(rd, sA + pc * 1024, ((bd + aoff[i]) * 2u) | apen[i] | (d < tail && rowok ? 0u : OOBV));
       }
 #pragma unroll
       for (int i = 0; i < IB; ++i) {
         const int pc = lw + NL * i;
-        const bool in = (unsigned)(2 * sy + brow[i]) < (unsigned)p.IH && (unsigned)(2 * sx + bcol[i]) < (unsigned)p.IW;
+        const bool in = (unsigned)(SG * sy + brow[i]) < (unsigned)p.IH && (unsigned)(SG * sx + bcol[i]) < (unsigned)p.IW;
         wdma16(rg, sB + pc * 1024, ((bg + boff[i]) * 2u) | (in ? 0u : OOBV));
       }
       sx += TC;
@@ -849,18 +611,20 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_kernel(const WbParams p) {
     const int col = wm * 64 + 16 * i + 4 * pcol;
     return row * ROWA + 16 * ((col >> 3) ^ wswz<16>(row)) + 2 * (col & 7);
   };
-  // B (patch) fragment offsets of K row d for the taps with kx / 2 = h: patch row 2 ty (+ ky), position tx + h
+  // B (patch) fragment offsets of K row d for the taps with column shift h (kx / 2; S1: kx): patch row 2 ty (+ ky)
+  // (S1: ty + ky), position tx + h
+  constexpr int NH = S1 ? 4 : 2;
   auto b_base = [&](int d, int h) {
     const int ty = d / TC, tx = d % TC;
-    return (2 * ty * 2 * G::NPOS + wh_perm(tx + h)) * 32 + 8 * pcol;
+    return ((S1 ? ty : 2 * ty) * G::NPL * G::NPOS + wh_perm(tx + h)) * 32 + 8 * pcol;
   };
-  int bb[2][2][2];  // [kk][lo/hi][h]
+  int bb[2][2][NH];  // [kk][lo/hi][h]
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) bb[kk][u][h] = b_base(kk * 32 + 8 * kq + q + 4 * u, h);
+      for (int h = 0; h < NH; ++h) bb[kk][u][h] = b_base(kk * 32 + 8 * kq + q + 4 * u, h);
   int cur = 0;
   for (int s = 0; s < nsteps; ++s) {
     __builtin_amdgcn_s_barrier();
@@ -879,8 +643,9 @@ __global__ void __launch_bounds__(512, 1) wgrad_halo_kernel(const WbParams p) {
       for (int j = 0; j < FN; ++j) {  // tap t = wn * 8 + j: ky = t >> 2, kx = t & 3
         const int t = wn * 8 + j;      // (wn is wave-uniform: the two taps rows of this wave)
         const int ky = t >> 2, kx = t & 3;
-        const int lineoff = (ky * 2 + (kx & 1)) * G::NPOS * 32;
-        const w4i16 v8[2] = {wtr16(sB + bb[kk][0][kx >> 1] + lineoff), wtr16(sB + bb[kk][1][kx >> 1] + lineoff)};
+        const int lineoff = (S1 ? ky : ky * 2 + (kx & 1)) * G::NPOS * 32;
+        const int h = S1 ? kx : kx >> 1;
+        const w4i16 v8[2] = {wtr16(sB + bb[kk][0][h] + lineoff), wtr16(sB + bb[kk][1][h] + lineoff)};
         fb[j] = __builtin_bit_cast(wbf16x8, v8);
       }
 #pragma unroll
@@ -946,11 +711,9 @@ constexpr WbCfg kWbCfg[] = {
     {128, 256, 8, false},        // 5
     {128, 128, 4, false, 4, 4},  // 6: + 4 loader waves, 4-stage ring
     {128, 128, 4, false, 3, 4},  // 7: + 4 loader waves, 3-stage ring
-    {256, 128, 8, false, 3, -1}, // 8: v2 (eight compute waves that also load, 3-stage ring)
-    {128, 256, 8, false, 3, -1}, // 9: v2
-    {128, 256, 8, false, 4, -2}, // 10: halo (stride 2, 16 channels x 16 taps per tile; wgrad_halo_kernel)
+    {128, 256, 8, false, 4, 4},  // 8: halo (stride 2, 16 channels x 16 taps per tile; wgrad_halo_kernel)
 };
-constexpr int WB_HALO = 10;
+constexpr int WB_HALO = 8;
 constexpr int kNumWbCfg = sizeof(kWbCfg) / sizeof(kWbCfg[0]);
 
 
@@ -962,8 +725,12 @@ struct WbPlan {
 // The halo tile (cfg WB_HALO) takes the stride-2 geometry on a D grid of width 16..128 (power of two; a K-step
 // = whole grid rows or half a 128-wide row), 16-channel G groups and >= 96 D rows.  stride 0 = unknown (the
 // query, which has no stride argument: it plans as stride 2 and sizes the workspace for either).
+// Stride 1: a 31-wide D grid (the PatchGAN layer 4 at 256 x 256), run on the virtual 32 x 32 grid.
+static bool wb_halo_s1(int GH, int GW, int stride) { return (stride == 1 || stride == 0) && GW == 31 && (GH + 1) % 2 == 0; }
 static bool wb_halo_ok(int GH, int GW, int stride, int R, int Cg) {
-  if (!(stride == 2 || stride == 0) || Cg % 16 != 0 || R < 96) return false;
+  if (Cg % 16 != 0 || R < 96) return false;
+  if (wb_halo_s1(GH, GW, stride)) return true;
+  if (!(stride == 2 || stride == 0)) return false;
   if (!(GW == 16 || GW == 32 || GW == 64 || GW == 128)) return false;
   return GH % (64 / std::min(GW, 64)) == 0;
 }
@@ -972,19 +739,22 @@ static bool wb_halo_ok(int GH, int GW, int stride, int R, int Cg) {
 // NULL or an unknown config = the automatic plan (also the halo config where the geometry does not allow it)
 static WbPlan wb_plan(int B, int GH, int GW, int stride, int R, int Cg, const int32_t* force) {
   WbPlan pl{};
-  const int P = B * GH * GW;
   const long long ncol = 16LL * Cg;
-  const int steps = cdiv(P, WB_BK);
   const bool halo = wb_halo_ok(GH, GW, stride, R, Cg);
   int cfg = force ? force[0] : -1;
   int force_ns = force ? std::max(force[1], 0) : 0;
   if (cfg == WB_HALO && !halo) cfg = -1;
+  const bool s1v = halo && wb_halo_s1(GH, GW, stride) && (cfg < 0 || cfg >= kNumWbCfg || cfg == WB_HALO);
+  const int P = s1v ? B * (GH + 1) * (GW + 1) : B * GH * GW;  // (the stride-1 halo: its virtual grid)
+  const int steps = cdiv(P, WB_BK);
   if (cfg < 0 || cfg >= kNumWbCfg) {
     force_ns = 0;
     // (fitted to scripts/tune_wgrad.py over one train step: the 8-wave tiles pay off once each
     // split still has a long pixel loop; 128x128 stays best for the shorter reductions)
     if (R <= 16) cfg = 2;
-    else if (R <= 64) cfg = 1;
+    // (R <= 64: the 128 x 128 loader tile beats the 64 x 128 tile on the first layers' 524288-pixel problems even
+    // with half its rows idle, 32-38 us against 40-45: profiles/r04/wgrad/tune_s1.log)
+    else if (R <= 64 && P < 65536) cfg = 1;
     else if (halo && P >= 4096) cfg = WB_HALO;
     else if (ncol >= 1024 && ((R >= 512 && P >= 16384) || (R >= 256 && P >= 65536))) cfg = 3;
     // 128x128 + 4 loader waves, 3-stage ring (96 KiB: a 64 KiB conv block still fits beside it): 5-13 % under
@@ -1060,14 +830,20 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
     p.lg_gw = lgw < 0 ? 0 : lgw;
     p.lg_ghw = lghw < 0 ? 0 : lghw;
   }
-  // (the halo tile needs G on exactly the doubled grid)
-  const bool g2x = G.H == 2 * D.H && G.W == 2 * D.W;
-  const WbPlan pl = wb_plan(B, D.H, D.W, stride == 2 && g2x ? 2 : 1, R, Cg, force);
+  // (the stride-2 halo tile needs G on exactly the doubled grid, the stride-1 one on the grid + 1)
+  const bool g2x = G.H == 2 * D.H && G.W == 2 * D.W, g1x = G.H == D.H + 1 && G.W == D.W + 1;
+  const WbPlan pl = wb_plan(B, D.H, D.W, stride == 2 ? (g2x ? 2 : -1) : (g1x ? 1 : -1), R, Cg, force);
+  const bool hs1 = pl.cfg == WB_HALO && stride == 1;
+  if (hs1) {  // the virtual grid
+    p.GH = D.H + 1; p.GW = D.W + 1;
+    p.P = B * p.GH * p.GW;
+  }
   p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.nsplit = pl.nsplit; p.pchunk = pl.pchunk;
   dim3 grid(pl.mtiles * pl.ntiles, 1, pl.nsplit);
-  const int htc = std::min(D.W, 64);
+  const int htc = std::min(p.GW, 64);
   const size_t lds = pl.cfg == WB_HALO
-                         ? (size_t)4 * (htc == 64 ? WhGeom<64>::STAGE : htc == 32 ? WhGeom<32>::STAGE : WhGeom<16>::STAGE)
+                         ? (size_t)4 * (hs1 ? WhGeom<32, true>::STAGE : htc == 64 ? WhGeom<64>::STAGE
+                                                                       : htc == 32 ? WhGeom<32>::STAGE : WhGeom<16>::STAGE)
                          : (size_t)kWbCfg[pl.cfg].stages * WB_BK * (pl.BM + pl.BN) * 2;
   if (!pl.slab) {
     p.dW = dW;
@@ -1094,18 +870,11 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
       if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_ld_kernel<128, 128, 2, 2, false, true, 4, 4>), grid, dim3(512), lds, st, p);
       else hipLaunchKernelGGL((wgrad_bf16_ld_kernel<128, 128, 2, 2, false, false, 4, 4>), grid, dim3(512), lds, st, p);
       break;
-    case 8:
-      if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_v2_kernel<256, 128, 4, 2, true>), grid, dim3(512), lds, st, p);
-      else hipLaunchKernelGGL((wgrad_bf16_v2_kernel<256, 128, 4, 2, false>), grid, dim3(512), lds, st, p);
-      break;
-    case 9:
-      if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_v2_kernel<128, 256, 2, 4, true>), grid, dim3(512), lds, st, p);
-      else hipLaunchKernelGGL((wgrad_bf16_v2_kernel<128, 256, 2, 4, false>), grid, dim3(512), lds, st, p);
-      break;
     case WB_HALO:
-      if (htc == 64) hipLaunchKernelGGL((wgrad_halo_kernel<64>), grid, dim3(512), lds, st, p);
-      else if (htc == 32) hipLaunchKernelGGL((wgrad_halo_kernel<32>), grid, dim3(512), lds, st, p);
-      else hipLaunchKernelGGL((wgrad_halo_kernel<16>), grid, dim3(512), lds, st, p);
+      if (hs1) hipLaunchKernelGGL((wgrad_halo_kernel<32, true>), grid, dim3(512), lds, st, p);
+      else if (htc == 64) hipLaunchKernelGGL((wgrad_halo_kernel<64, false>), grid, dim3(512), lds, st, p);
+      else if (htc == 32) hipLaunchKernelGGL((wgrad_halo_kernel<32, false>), grid, dim3(512), lds, st, p);
+      else hipLaunchKernelGGL((wgrad_halo_kernel<16, false>), grid, dim3(512), lds, st, p);
       break;
     default:
       if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_ld_kernel<128, 128, 2, 2, false, true, 4, 3>), grid, dim3(512), lds, st, p);

@@ -278,9 +278,8 @@ def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True
 # bf16 weight-gradient tile configurations (csrc/wgrad_bf16.hip kWbCfg): cfg -> (BM, BN, WM, WN, swapped)
 _WB_TILES = [(128, 128, 2, 2, "false"), (64, 128, 1, 4, "false"), (128, 16, 4, 1, "true"), (256, 256, 2, 4, "false"),
              (256, 128, 4, 2, "false"), (128, 256, 2, 4, "false"), (128, 128, 2, 2, "false", 4, 4),
-             (128, 128, 2, 2, "false", 4, 3), (256, 128, 4, 2, "false", -1, 3),
-             (128, 256, 2, 4, "false", -1, 3),
-             (128, 256, 2, 2, "false", -2, 4)]  # (BM, BN, WM, WN, swapped[, loader waves (-1: v2, -2: halo), stages])
+             (128, 128, 2, 2, "false", 4, 3),
+             (128, 256, 2, 2, "false", -2, 4)]  # (BM, BN, WM, WN, swapped[, loader waves (-2: halo), stages])
 
 
 def wgrad_query(B, Hd, Wd, R, Cg, dt, force=None):
@@ -303,10 +302,8 @@ def _wgrad_kernel_name(plan, Hd, Wd):
     pow2 = lambda v: v > 0 and (v & (v - 1)) == 0  # noqa: E731
     fast = Wd % 64 == 0 or (pow2(Wd) and ghw % 64 == 0) or (pow2(ghw) and pow2(Wd) and 64 % ghw == 0)
     fast = fast and cfg != 3  # the 256x256 tile keeps the general addressing (register budget)
-    if ld == -2:
-        return f"wgrad_halo_kernel<{min(Wd, 64)}>"
-    if ld < 0:
-        return f"wgrad_bf16_v2_kernel<{bm}, {bn}, {wm}, {wn}, {str(fast).lower()}>"
+    if ld == -2:  # (the stride-1 halo tile: a 31-wide grid run as 32 x 32)
+        return "wgrad_halo_kernel<32, true>" if Wd == 31 else f"wgrad_halo_kernel<{min(Wd, 64)}, false>"
     if ld:
         return f"wgrad_bf16_ld_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}, {ld}, {nst}>"
     return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}>"

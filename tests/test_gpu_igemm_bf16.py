@@ -314,31 +314,21 @@ WGRAD_FORCED = [  # (case, tile config, pixel splits): the 8-wave tiles on ragge
     (("conv", 2, 1, 16, 128, 128, 128), 6, 3),
     (("conv", 2, 5, 16, 64, 8, 8), 7, 2),
     (("conv", 1, 2, 512, 8, 17, 17), 6, 4),
-    # v2 tiles (eight compute waves that also load, 3-stage ring): every pixel mode, ragged, split / unsplit
-    (("conv", 2, 2, 64, 256, 32, 32), 8, 0),
-    (("conv", 2, 2, 64, 256, 32, 32), 9, 1),
-    (("conv", 1, 2, 256, 512, 17, 17), 8, 0),
-    (("conv", 1, 2, 256, 512, 17, 17), 9, 3),
-    (("conv", 2, 3, 32, 96, 10, 14), 8, 3),
-    (("conv", 2, 3, 32, 96, 10, 14), 9, 0),
-    (("convT", 2, 2, 128, 64, 16, 16), 8, 2),
-    (("convT", 2, 2, 1024, 512, 2, 2), 9, 1),
-    (("conv", 2, 1, 16, 128, 128, 128), 9, 3),
-    (("conv", 2, 5, 16, 64, 8, 8), 8, 2),
-    (("conv", 2, 2, 8, 64, 64, 64), 9, 0),
-    (("conv", 1, 2, 512, 8, 17, 17), 8, 4),
-    (("conv", 2, 2, 32, 64, 256, 16), 9, 2),
     # halo tile (stride 2, 16 channels x 16 taps per tile): K-step widths 16 / 32 / 64 (+ a 128-wide grid: two steps
     # per row), both roles (conv: D = dy; convT: D = x), ragged R, several channel groups, splits across images
-    (("conv", 2, 2, 64, 128, 32, 32), 10, 0),
-    (("conv", 2, 2, 64, 128, 32, 32), 10, 3),
-    (("conv", 2, 1, 32, 256, 64, 64), 10, 2),
-    (("conv", 2, 1, 16, 128, 128, 128), 10, 1),
-    (("conv", 2, 1, 48, 96, 256, 64), 10, 5),
-    (("conv", 2, 1, 16, 128, 64, 256), 10, 2),
-    (("convT", 2, 2, 128, 64, 16, 16), 10, 0),
-    (("convT", 2, 3, 256, 32, 32, 32), 10, 4),
-    (("convT", 2, 1, 128, 16, 64, 64), 10, 1),
+    (("conv", 2, 2, 64, 128, 32, 32), 8, 0),
+    (("conv", 2, 2, 64, 128, 32, 32), 8, 3),
+    (("conv", 2, 1, 32, 256, 64, 64), 8, 2),
+    (("conv", 2, 1, 16, 128, 128, 128), 8, 1),
+    (("conv", 2, 1, 48, 96, 256, 64), 8, 5),
+    (("conv", 2, 1, 16, 128, 64, 256), 8, 2),
+    (("convT", 2, 2, 128, 64, 16, 16), 8, 0),
+    (("convT", 2, 3, 256, 32, 32, 32), 8, 4),
+    (("convT", 2, 1, 128, 16, 64, 64), 8, 1),
+    # the stride-1 halo tile (PatchGAN layer 4: D = dy 31 x 31 run as 32 x 32, G = x 32 x 32)
+    (("conv", 1, 2, 64, 128, 32, 32), 8, 0),
+    (("conv", 1, 1, 256, 512, 32, 32), 8, 3),
+    (("conv", 1, 3, 32, 96, 32, 32), 8, 2),
 ]
 
 
@@ -372,9 +362,9 @@ def test_wgrad_rows_narrow_s1(B, Cin, H, W, rows, dt):
 
 def test_wgrad_halo_plan_automatic():
     """The train step's stride-2 weight gradients with a 16..128-wide grid and 16-channel groups take the halo tile
-    (plan config 10); the narrow first layers (Cg = 8) and the deep 8x8 .. 1x1 grids keep the im2col tiles."""
+    (plan config 8); the narrow first layers (Cg = 8) and the deep 8x8 .. 1x1 grids keep the im2col tiles."""
     for (B, gh, R, Cg) in ((32, 64, 128, 64), (32, 32, 256, 128), (32, 16, 512, 256), (32, 64, 256, 64),
-                           (32, 32, 512, 128), (32, 16, 1024, 256)):
-        assert ops.wgrad_query(B, gh, gh, R, Cg, BF)[1][0] == 10, (B, gh, R, Cg)
+                           (32, 32, 512, 128), (32, 16, 1024, 256), (32, 31, 512, 256)):
+        assert ops.wgrad_query(B, gh, gh, R, Cg, BF)[1][0] == 8, (B, gh, R, Cg)
     for (B, gh, R, Cg) in ((32, 128, 64, 8), (32, 8, 512, 512), (32, 2, 512, 512)):
-        assert ops.wgrad_query(B, gh, gh, R, Cg, BF)[1][0] != 10, (B, gh, R, Cg)
+        assert ops.wgrad_query(B, gh, gh, R, Cg, BF)[1][0] != 8, (B, gh, R, Cg)
