@@ -65,6 +65,19 @@ def _disarm():
     lib().stc_time_next_main_kernel(None, None)
 
 
+# Plan / workspace answers of the library are pure functions of their arguments (no environment, no device
+# state), and the step asks the same few dozen questions every iteration: memoised, ~5 us of host time per call.
+_MEMO = {}
+
+
+def _conv_ws_bytes(kind, B, gh, gw, cin, cout, dt):
+    key = ("cws", kind, B, gh, gw, cin, cout, dt)
+    v = _MEMO.get(key)
+    if v is None:
+        v = _MEMO[key] = lib().stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
+    return v
+
+
 def plan_of(kind, B, gh, gw, cin, cout, dt):
     out = (ctypes.c_int32 * 4)()
     check(lib().stc_conv_fwd_plan(L.dtype_code(dt), kind, B, gh, gw, cin, cout, out), "stc_conv_fwd_plan")
@@ -79,7 +92,7 @@ def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=No
     else:
         gh, gw = yv.H, yv.W
     l = lib()
-    nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
+    nbytes = _conv_ws_bytes(kind, B, gh, gw, cin, cout, dt)
     ws, nb = _ws(nbytes, dev)
     sc, sh = _pro(pro)
     timer = _timer
@@ -97,13 +110,18 @@ def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=No
 
 def conv_query(kind, B, gh, gw, cin, cout, dt, out_f32=False, force=None):
     """(workspace bytes, stats chunks, plan (BM, BN, ksplit, narrow, cfg)) of stc_conv_fwd_ex."""
+    key = ("cq", kind, B, gh, gw, cin, cout, dt, bool(out_f32), None if force is None else tuple(force))
+    r = _MEMO.get(key)
+    if r is not None:
+        return r
     ws = ctypes.c_int64()
     nch = ctypes.c_int32()
     po = (ctypes.c_int32 * 5)()
     fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
     check(lib().stc_conv_fwd_query(L.dtype_code(dt), kind, B, gh, gw, cin, cout, int(out_f32), fp, ctypes.byref(ws),
                                    ctypes.byref(nch), po), "stc_conv_fwd_query")
-    return ws.value, nch.value, tuple(po)
+    r = _MEMO[key] = (ws.value, nch.value, tuple(po))
+    return r
 
 
 # Tuning hooks (scripts/train_steps.py --ab-plans): per-shape plan overrides of the forward convs with
@@ -130,7 +148,7 @@ def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bi
         return False
     gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (y1v.H, y1v.W)
     dev = w_packed.device
-    nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
+    nbytes = _conv_ws_bytes(kind, B, gh, gw, cin, cout, dt)
     ws, nb = _ws(nbytes, dev)
     timer = _timer
     if timer is not None:
@@ -231,9 +249,12 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
     dev = w_packed.device
     l = lib()
     gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
-    nbytes = l.stc_conv_fwd_workspace(L.dtype_code(dt), kind, B, gh, gw, cin, cout)
+    nbytes = _conv_ws_bytes(kind, B, gh, gw, cin, cout, dt)
     ws, nb = _ws(nbytes, dev)
-    nch = l.stc_conv_bwd_bn_chunks(L.dtype_code(dt), kind, B, gh, gw, cin, cout, bn_x.H, bn_x.W)
+    key = ("bnbch", kind, B, gh, gw, cin, cout, dt, bn_x.H, bn_x.W)
+    nch = _MEMO.get(key)
+    if nch is None:
+        nch = _MEMO[key] = l.stc_conv_bwd_bn_chunks(L.dtype_code(dt), kind, B, gh, gw, cin, cout, bn_x.H, bn_x.W)
     part = torch.empty((nch, C, 2), dtype=torch.float32, device=dev)
     scale, shift, mean, rstd = bn_state
     fuse = L.BnbFuse(bn_x, g_other if g_other is not None else L.NULL_VIEW, scale.data_ptr(), shift.data_ptr(),
@@ -284,12 +305,17 @@ _WB_TILES = [(128, 128, 2, 2, "false"), (64, 128, 1, 4, "false"), (128, 16, 4, 1
 
 def wgrad_query(B, Hd, Wd, R, Cg, dt, force=None):
     """(workspace bytes, plan (cfg, BM, BN, splits, slab)) of stc_conv_wgrad_ex for these arguments."""
+    key = ("wq", B, Hd, Wd, R, Cg, dt, None if force is None else tuple(force))
+    r = _MEMO.get(key)
+    if r is not None:
+        return r
     ws = ctypes.c_int64()
     po = (ctypes.c_int32 * 5)()
     fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
     check(lib().stc_conv_wgrad_query(L.dtype_code(dt), B, Hd, Wd, R, Cg, fp, ctypes.byref(ws), po),
           "stc_conv_wgrad_query")
-    return ws.value, tuple(po)
+    r = _MEMO[key] = (ws.value, tuple(po))
+    return r
 
 
 def _wgrad_kernel_name(plan, Hd, Wd):
