@@ -159,7 +159,11 @@ def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bi
         _disarm()
     check(rc, "stc_conv_fwd_act")
     if timer is not None:
-        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1)
+        # the 8-channel first layers run the streaming stem kernel (csrc/stem_bf16.hip, stem_eligible)
+        stem = (kind == L.CONV_S2 and cin == 8 and cout == 64 and xv.W in (256, 512) and xv.co == 0 and xv.ps == 8
+                and xv.H == 2 * gh and gh % 8 == 0)
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1,
+                    name=f"stem_conv_kernel<{xv.W}, {2 if y2v is not None else 1}>" if stem else None)
     return True
 
 
