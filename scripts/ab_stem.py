@@ -43,3 +43,18 @@ for nout in (1, 2):
     byt = B * W * W * 8 * 2 + nout * B * Ho * Ho * 64 * 2
     print(f"outputs {nout}: stem {t_stem:6.1f} us ({byt / t_stem / 1e6:.2f} TB/s)  im2col conv alone {t_conv:6.1f} us  "
           f"conv + bn_apply {t_two:6.1f} us", flush=True)
+
+# the output layer's input gradient with the fused BN-backward sums (G: dq 8 ch -> 128 ch, BN on channels 64..127)
+Cout, C = 128, 64
+wt = torch.randn((8, Cout, 4, 4), device=dev) * 0.05
+wd = ops.pack(L.PACK_CONVT_DGRAD, wt, Cout, 8, BF)
+dq = torch.randn((B, W, W, 8), device=dev).to(BF)
+bx = torch.randn((B, Ho, Ho, C), device=dev).to(BF)
+out = torch.empty((B, Ho, Ho, Cout), device=dev, dtype=BF)
+dx = torch.empty((B, Ho, Ho, C), device=dev, dtype=BF)
+tabs = [torch.rand(C, device=dev) + 0.5 for _ in range(5)]
+t_f = timed(lambda: ops.conv_bn_backward(L.CONV_S2, B, L.nhwc_view(dq), 8, wd, Cout, L.nhwc_view(out), BF,
+                                         bn_x=L.nhwc_view(bx), C=C, bn_state=tuple(tabs[:4]), gamma=tabs[4], s_self=0.0,
+                                         ch_off=64, dxv=L.nhwc_view(dx)))
+byt = B * W * W * 8 * 2 + B * Ho * Ho * (Cout + C) * 2
+print(f"BN-backward input gradient (stem + BN apply): {t_f:6.1f} us  (conv part compulsory {byt / 1e6:.0f} MB)", flush=True)

@@ -851,8 +851,13 @@ static bool bnb_fused_path(int dtype, int kind, int B, const stc_view& dy, int C
   return bf16_path(dtype, kind, Cin, Cout) && vec && bf16_conv_eligible(kind, B, dy, Cin, Cout);
 }
 
+namespace stc {
+int stem_bnb_chunks(int kind, int B, int Hg, int Wg, int Cin, int Cout);
+}
+
 extern "C" int stc_conv_bwd_bn_chunks(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int xH, int xW) {
   if (bf16_path(dtype, kind, Cin, Cout)) {
+    if (const int sn = stem_bnb_chunks(kind, B, Hg, Wg, Cin, Cout)) return sn;  // (the streaming Cin = 8 kernel)
     int32_t nch = 0;
     bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &nch, nullptr);
     return nch;  // (NHWC 16-byte aligned views assumed: the fused path)
@@ -868,8 +873,13 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
   if (bnb_fused_path(dtype, kind, B, dy, Cin, Cout, out)) {
     const Geometry g = geometry(kind);
     const int Hg = kind == STC_CONVT_S2 ? dy.H : out.H, Wg = kind == STC_CONVT_S2 ? dy.W : out.W;
-    int32_t need = 0;
-    bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &need, nullptr);
+    int32_t need = stem_bnb_chunks(kind, B, Hg, Wg, Cin, Cout);
+    if (need) {  // the streaming Cin = 8 kernel: a dense 8-channel input view
+      STC_REQUIRE(dy.cs == 1 && dy.ps == 8 && dy.co == 0 && out.H * 2 == dy.H && out.W * 2 == dy.W,
+                  "stc_conv_bwd_bn: the 8-channel input of this shape must be a dense NHWC tensor");
+    } else {
+      bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &need, nullptr);
+    }
     (void)g;
     STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks)", nchunks, need);
     return bf16_conv_fwd(kind, B, dy, Cin, w_packed, Cout, out, nullptr, 0, 0, nullptr, need, nullptr, workspace,

@@ -804,7 +804,7 @@ bool halo_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const 
 int halo_chunks(int kind, int B, int GH, int GW);
 int halo_launch(GParams& p, hipStream_t st, int shape);
 // the Cin = 8 first layers with the activation epilogue (stem_bf16.hip)
-bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y);
+bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y, bool bnb);
 int stem_launch(GParams& p, hipStream_t st);
 static bool halo_plan(const int32_t* force, int kind, int B, int GH, int GW, int Cin, int Cout) {
   if (force && force[0] == HALO_CFG) return halo_geometry_ok(kind, B, GH, GW, Cin, Cout);
@@ -891,7 +891,10 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
       p.c2 = (char*)act2->p; p.c2_bs = act2->bs; p.c2_rs = act2->rs; p.c2_ps = act2->ps; p.c2_co = act2->co;
     }
   }
-  if (act_n && p.vec_out && !force && stem_eligible(kind, B, x, Cin, Cout, y)) return stem_launch(p, st);
+  if (p.vec_out && !force && !stats && (act_n || bnb) && stem_eligible(kind, B, x, Cin, Cout, y, bnb != nullptr)) {
+    p.ws = nullptr;
+    return stem_launch(p, st);
+  }
   if (!act_n && p.vec_out && halo_plan(force, kind, B, p.GH, p.GW, Cin, Cout) && halo_eligible(kind, B, x, Cin, Cout, y)) {
     const int need = halo_chunks(kind, B, p.GH, p.GW);
     if (stats || part2) STC_REQUIRE(stats_chunks >= need, "bf16 conv: stats chunks %d < %d", stats_chunks, need);

@@ -1,19 +1,23 @@
-// bf16 first-layer Conv2d k4 s2 p1 with 8 (padded) input channels and 64 outputs + activation epilogue
-// (G's outermost down conv, STCGAN/networks.py:99, and D's first conv, :165-166; no BatchNorm after either).
-//
-// The layer is HBM-bound: K = 16 taps x 8 channels = 128, so its MFMA work is 4 % of the time it takes to read
-// the 16-byte input pixels once and write the 128-byte output pixels once or twice (the LeakyReLU copy for the next
-// conv and, in G, the ReLU copy for the skip concat).  The im2col GEMM tile re-stages every input pixel 4 times per
-// 128-row tile and pays a load latency per tile; here a block owns a strip of 8 output rows of one image and streams
-// its input rows through an 8-slot LDS ring by LDS-DMA (an input row = W x 16 B; output row oy reads input rows
-// 2oy-1 .. 2oy+2, so each output row brings 2 new input rows), two output rows of loads ahead of the MFMAs.  Padding
-// rows are out-of-range DMA offsets (zeros); the padding columns are zeroed in registers.
-//
+// bf16 Conv2d k4 s2 p1 with 8 (padded) input channels: the K = 128 layers at the full-resolution edge of the
+// generator and the discriminators, which are HBM-bound (their MFMA work is a few % of the time it takes to read the
+// 16-byte input pixels once and write the output pixels once).
+//   * forward of G's outermost down conv and D's first conv (STCGAN/networks.py:99, :165-166; 64 outputs, no
+//     BatchNorm): the activation epilogue -- act(s1) [and act(s2)] of the bf16-rounded output, exactly as
+//     stc_bn_apply with no table (MODE 1 / 2);
+//   * the input gradient of G's output ConvTranspose2d (networks.py:112-116; dq, 8 channels -> the 128-channel
+//     concat gradient) with the BatchNorm-backward sums of the up-path BN on its second half fused in (MODE 3, the
+//     stc_conv_bwd_bn contract of igemm_bf16.hpp's BNB epilogue; one partial per block).
+// The im2col GEMM tile re-stages every input pixel 4 times per 128-row tile and pays a load latency per tile; here a
+// block owns a strip of 8 output rows of one image and streams its input rows through an 8-slot LDS ring by LDS-DMA
+// (an input row = W x 16 B; output row oy reads input rows 2oy-1 .. 2oy+2, so each output row brings 2 new input
+// rows), two output rows of loads ahead of the MFMAs.  Padding rows are out-of-range DMA offsets (zeros); the
+// padding columns are zeroed in registers.
 // MFMA v_mfma_f32_16x16x32_bf16, K-step = kernel row ky: a lane's 8 K values (tap (ky, kx = lane >> 4), 8 channels)
-// are one input pixel, one ds_read_b128 (conflict-free: the 16 lanes of a group read 16 distinct pixels mod 16);
-// the 64 x 128 weights live in registers (16 fragments).  A wave computes 16 output pixels x 64 channels per chunk;
-// the epilogue adds the bias, rounds to bf16, applies act(s1) [and act(s2)] to the rounded value exactly as
-// stc_bn_apply with no table does, and writes 16-byte NHWC rows through a per-wave LDS transpose.
+// are one input pixel, one ds_read_b128 (conflict-free: the 16 lanes of a group read 16 distinct pixels mod 16); the
+// N x 128 weights live in registers.  A wave computes 16 output pixels x N channels per chunk and writes 16-byte NHWC
+// rows through a per-wave LDS transpose.  Results equal the im2col tile's bit for bit (same K order, same MFMA).
+#include <algorithm>
+
 #include "igemm_bf16.hpp"
 
 namespace stc {
@@ -21,14 +25,21 @@ namespace stc {
 constexpr int STEM_RB = 8;   // output rows per block
 constexpr int STEM_NS = 8;   // input-row slots in the LDS ring
 
-template <int WIN, int NOUT>
+template <int WIN, int N, int MODE>
 __global__ void __launch_bounds__(256) stem_conv_kernel(const GParams p) {
   constexpr int WOUT = WIN / 2;
   constexpr int ROWB = WIN * 16;              // bytes of one input row (8 bf16 channels per pixel)
   constexpr int PPW = WIN / 256;              // 1 KiB DMA pieces per wave per input row
   constexpr int NCH = WOUT / 64;              // 64-pixel chunks per output row (16 per wave)
-  constexpr int SPW = NCH * 2 * NOUT;         // 16-byte stores per lane per output row
-  constexpr int PITCH = 64 * 2 + 16;          // output staging row (64 bf16 + pad)
+  constexpr int NF = N / 16;                  // MFMA N fragments
+  constexpr int CPX = N / 8;                  // 16-byte chunks per output pixel
+  constexpr int PXS = 64 / CPX;               // pixels per store pass of a wave
+  constexpr int NPASS = 16 / PXS;             // store passes per chunk
+  constexpr bool BNB = MODE == 3;
+  // other VMEM ops per output row and wave: the stores, and (MODE 3) the BN input + second-gradient loads
+  constexpr int OPW = NCH * NPASS * (MODE == 2 ? 2 : 1) + (BNB ? 2 * NCH * NPASS : 0);
+  constexpr int PITCH = N * 2 + 16;           // output staging row (N bf16 + pad)
+  static_assert(NPASS >= 1 && 4 * PPW <= 63 && 2 * PPW + 2 * OPW <= 63, "stem tile: vmcnt immediates");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ring = smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -53,32 +64,46 @@ __global__ void __launch_bounds__(256) stem_conv_kernel(const GParams p) {
   };
 
   // weights: B fragment (n-frag j, K-step ky) of lane (rl, kq) = w[16 j + rl][tap 4 ky + kq][0..7]
-  bf16x8_t wf[4][4];
+  bf16x8_t wf[NF][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < NF; ++j)
 #pragma unroll
     for (int ky = 0; ky < 4; ++ky)
       wf[j][ky] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(p.b) + (16 * j + rl) * 128 +
                                                      (4 * ky + kq) * 8);
-  float bz[4];
+  float bz[NF];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bz[j] = p.bias ? p.bias[16 * j + rl] : 0.f;
+  for (int j = 0; j < NF; ++j) bz[j] = p.bias ? p.bias[16 * j + rl] : 0.f;
   const bf16x8_t zero8 = {};
+
+  // store / BN-backward lane role: 16-byte chunk sc of pixels spx + PXS * h
+  const int sc = lane % CPX, spx = lane / CPX;
+  const int nb = sc * 8 - p.bch_off;  // BN channel of the chunk (MODE 3)
+  const bool bn_lane = BNB && nb >= 0 && nb < p.bC;
+  const int nbc = bn_lane ? nb : 0;
+  float bsc[8], bsh[8], bmu[8], brs[8], sa[8], sb[8];
+  if constexpr (BNB) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bsc[e] = p.bsc[nbc + e]; bsh[e] = p.bsh[nbc + e]; bmu[e] = p.bmu[nbc + e]; brs[e] = p.brs[nbc + e];
+      sa[e] = 0.f; sb[e] = 0.f;
+    }
+  }
 
   // prologue: the 4 rows of output row 0 and the 2 new rows of output rows 1 and 2
 #pragma unroll
   for (int r = 0; r < 8; ++r) load_row(r);
   for (int t = 0; t < STEM_RB; ++t) {
-    // rows 2t .. 2t+3 must have landed; younger: this wave's stores of rows t-2 / t-1 and the loads of rows 2t+4.. 2t+7
-    // issued between them (t = 0: the loads of rows 4..7; t = 1: rows 6, 7 after the stores of row 0)
+    // rows 2t .. 2t+3 must have landed; younger: this wave's other VMEM ops (stores, BN loads) of output rows t-2 and
+    // t-1 and the loads of rows 2t+4 .. 2t+7 issued between them (t = 0: the loads of rows 4..7; t = 1: rows 6, 7
+    // before the ops of row 0)
     if (t == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PPW) : "memory");
-    else if (t == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + SPW) : "memory");
-    else if (t + 1 < STEM_RB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + 2 * SPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * SPW) : "memory");
+    else if (t == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + OPW) : "memory");
+    else if (t + 1 < STEM_RB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + 2 * OPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPW) : "memory");
     __builtin_amdgcn_s_barrier();
-    // refill: rows 2t + 8, 2t + 9 into the slots of rows 2t, 2t + 1 ... read by THIS output row: so the refill for
-    // output row t + 3 waits for the next barrier; here: rows 2t + 6, 2t + 7 (slots of rows 2t - 2, 2t - 1, last read
-    // by output row t - 1, which every wave finished before this barrier)
+    // refill rows 2t + 6, 2t + 7 into the slots of rows 2t - 2, 2t - 1, last read by output row t - 1, which every
+    // wave finished before this barrier (the slots of rows 2t .. 2t + 3 are this row's)
     if (t >= 1 && 2 * t + 7 < 2 * STEM_RB + 2) {
       load_row(2 * t + 6);
       load_row(2 * t + 7);
@@ -89,69 +114,143 @@ __global__ void __launch_bounds__(256) stem_conv_kernel(const GParams p) {
     for (int ky = 0; ky < 4; ++ky) rows[ky] = ring + ((2 * t + ky) % STEM_NS) * ROWB;
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
+      // MODE 3: this chunk's BN inputs, loaded before the MFMAs
+      uint4 bxv[NPASS], bgv[NPASS];
+      if constexpr (BNB) {  // (the second gradient's loads always issue -- from the BN input when there is none --
+                            // so that every wave's VMEM count per row is the compile-time OPW)
+#pragma unroll
+        for (int h = 0; h < NPASS; ++h) {
+          const int oxs = ch * 64 + wave * 16 + spx + PXS * h;
+          const bool in = oy < p.bxH && oxs < p.bxW;
+          const int oyc = in ? oy : 0, oxc = in ? oxs : 0;
+          const bf16* xq = reinterpret_cast<const bf16*>(p.bx) + (long long)img * p.bx_bs + (long long)oyc * p.bx_rs +
+                           (long long)oxc * p.bx_ps + p.bx_co + nbc;
+          const bf16* gq = p.bg ? reinterpret_cast<const bf16*>(p.bg) + (long long)img * p.bg_bs + (long long)oyc * p.bg_rs +
+                                      (long long)oxc * p.bg_ps + p.bg_co + nbc
+                                : xq;
+          bxv[h] = *reinterpret_cast<const uint4*>(xq);
+          bgv[h] = *reinterpret_cast<const uint4*>(gq);
+        }
+      }
       const int ox = ch * 64 + wave * 16 + rl;  // this lane's output pixel
       const int col = 2 * ox + kq - 1;          // input column of tap kx = kq
       const bool cok = (unsigned)col < (unsigned)WIN;
-      floatx4 acc[4];
+      floatx4 acc[NF];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NF; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ky = 0; ky < 4; ++ky) {
         bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(rows[ky] + (cok ? col : 0) * 16);
         a = cok ? a : zero8;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = exp_mfma(a, wf[j][ky], acc[j]);
+        for (int j = 0; j < NF; ++j) acc[j] = exp_mfma(a, wf[j][ky], acc[j]);
       }
-      // acc[j][e] = out[pixel ch*64 + wave*16 + 4 kq + e][channel 16 j + rl]: + bias, bf16, staged [pixel][64 ch]
+      // acc[j][e] = out[pixel ch*64 + wave*16 + 4 kq + e][channel 16 j + rl]: + bias, bf16, staged [pixel][N]
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NF; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float v = acc[j][e] + bz[j];
-          const unsigned u = pack_bf16x2(v, 0.f) & 0xffffu;
+          const unsigned u = pack_bf16x2(acc[j][e] + bz[j], 0.f) & 0xffffu;
           *reinterpret_cast<unsigned short*>(stg + (4 * kq + e) * PITCH + (16 * j + rl) * 2) = (unsigned short)u;
         }
       __builtin_amdgcn_wave_barrier();
-      // 16 pixels x 8 chunks of 16 B: lane -> chunk lane & 7, pixels lane >> 3 and + 8
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int px = (lane >> 3) + 8 * h, c8 = lane & 7;
-        const uint4 tv = *reinterpret_cast<const uint4*>(stg + px * PITCH + c8 * 16);
+      for (int h = 0; h < NPASS; ++h) {
+        const int px = spx + PXS * h;
+        const uint4 tv = *reinterpret_cast<const uint4*>(stg + px * PITCH + sc * 16);
         const int oxs = ch * 64 + wave * 16 + px;
-        const long long o1 = (long long)img * p.c_bs + (long long)oy * p.c_rs + (long long)oxs * p.c_ps + p.c_co + c8 * 8;
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + o1) = act_bf16x8(tv, p.act_s1);
-        if constexpr (NOUT == 2) {
-          const long long o2 = (long long)img * p.c2_bs + (long long)oy * p.c2_rs + (long long)oxs * p.c2_ps + p.c2_co + c8 * 8;
-          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c2) + o2) = act_bf16x8(tv, p.act_s2);
+        const long long o1 = (long long)img * p.c_bs + (long long)oy * p.c_rs + (long long)oxs * p.c_ps + p.c_co + sc * 8;
+        if constexpr (BNB) {
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + o1) = tv;
+          // {sum dn, sum dn * xhat} of the chunk's BN channels at this pixel (igemm_epilogue's BNB arithmetic)
+          if (bn_lane && oy < p.bxH && oxs < p.bxW) {
+            const unsigned wt[4] = {tv.x, tv.y, tv.z, tv.w};
+            const unsigned wx[4] = {bxv[h].x, bxv[h].y, bxv[h].z, bxv[h].w};
+            const unsigned wg[4] = {bgv[h].x, bgv[h].y, bgv[h].z, bgv[h].w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float v = __uint_as_float((e & 1) ? (wt[e >> 1] & 0xffff0000u) : (wt[e >> 1] << 16));
+              const float xv = __uint_as_float((e & 1) ? (wx[e >> 1] & 0xffff0000u) : (wx[e >> 1] << 16));
+              const float gv = __uint_as_float((e & 1) ? (wg[e >> 1] & 0xffff0000u) : (wg[e >> 1] << 16));
+              const float nn = fmaf(xv, bsc[e], bsh[e]);
+              float dn = v * (nn > 0.f ? 1.f : p.bs_self);
+              if (p.bg) dn += gv * (nn > 0.f ? 1.f : p.bs_other);
+              sa[e] += dn;
+              sb[e] += dn * (xv - bmu[e]) * brs[e];
+            }
+          }
+        } else {
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + o1) = act_bf16x8(tv, p.act_s1);
+          if constexpr (MODE == 2) {
+            const long long o2 = (long long)img * p.c2_bs + (long long)oy * p.c2_rs + (long long)oxs * p.c2_ps + p.c2_co +
+                                 sc * 8;
+            *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c2) + o2) = act_bf16x8(tv, p.act_s2);
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();
     }
   }
+  if constexpr (BNB) {
+    // the block's partial: threads sharing a chunk summed in thread order (fixed), through the ring's LDS
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [256][16]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sa[e]; red[tid * 16 + 8 + e] = sb[e]; }
+    __syncthreads();
+    if (tid < CPX) {
+      const int ch0 = tid * 8 - p.bch_off;
+      if (ch0 >= 0 && ch0 < p.bC) {
+        float ta[8], tb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { ta[e] = 0.f; tb[e] = 0.f; }
+        for (int q = tid; q < 256; q += CPX)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { ta[e] += red[q * 16 + e]; tb[e] += red[q * 16 + 8 + e]; }
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          *reinterpret_cast<float2*>(p.part2 + ((long long)blockIdx.x * p.bC + ch0 + e) * 2) = make_float2(ta[e], tb[e]);
+      }
+    }
+  }
 }
 
-// Eligible: Conv2d k4 s2 p1, 8 input channels (a 16-byte bf16 pixel, channel offset 0 of a dense pixel), 64 outputs,
-// input width 256 or 512, output rows a multiple of 8, the activation epilogue (no statistics, no split), 16-byte
-// NHWC output views.
-bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y) {
-  if (kind != STC_CONV_S2 || Cin != 8 || Cout != 64) return false;
-  if (!(x.W == 256 || x.W == 512) || x.H % 2 != 0 || y.H * 2 != x.H || y.W * 2 != x.W || y.H % STEM_RB != 0) return false;
+// Eligible: Conv2d k4 s2 p1, 8 input channels (a dense 16-byte bf16 pixel at channel offset 0), input width 256 or
+// 512, output rows a multiple of 8, 16-byte NHWC output views; 64 outputs with the activation epilogue, or 128
+// outputs with the fused BN-backward sums (input width 256).
+static bool stem_sizes(int kind, int Cin, int Cout, int Hg, int Wg, bool bnb) {
+  return kind == STC_CONV_S2 && Cin == 8 && Cout == (bnb ? 128 : 64) && (Wg == 128 || (Wg == 256 && !bnb)) &&
+         Hg % STEM_RB == 0;
+}
+
+bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y, bool bnb) {
+  if (!stem_sizes(kind, Cin, Cout, y.H, y.W, bnb) || y.H * 2 != x.H || y.W * 2 != x.W) return false;
   if (x.cs != 1 || x.ps != 8 || x.co != 0) return false;
   return (long long)B * x.bs * 2 < (1ll << 31);
+}
+
+// BN-backward partial count of the fused input gradient when it takes this kernel (0: it does not)
+int stem_bnb_chunks(int kind, int B, int Hg, int Wg, int Cin, int Cout) {
+  return stem_sizes(kind, Cin, Cout, Hg, Wg, true) ? B * (Hg / STEM_RB) : 0;
 }
 
 int stem_launch(GParams& p, hipStream_t st) {
   const int B = p.M / (p.GH * p.GW);
   const dim3 grid((unsigned)(B * (p.GH / STEM_RB)));
-  const size_t lds = (size_t)STEM_NS * p.IW * 16 + 4 * 16 * (64 * 2 + 16);
+  const bool bnb = p.part2 != nullptr;
+  const int n = bnb ? 128 : 64;
+  const size_t lds = std::max((size_t)STEM_NS * p.IW * 16 + 4 * 16 * (n * 2 + 16), (size_t)256 * 16 * 4);
   main_timer_begin(st);
+#define STEM_K(W_, N_, M_) hipLaunchKernelGGL((stem_conv_kernel<W_, N_, M_>), grid, dim3(256), lds, st, p)
   if (p.IW == 256) {
-    if (p.act_n == 2) hipLaunchKernelGGL((stem_conv_kernel<256, 2>), grid, dim3(256), lds, st, p);
-    else hipLaunchKernelGGL((stem_conv_kernel<256, 1>), grid, dim3(256), lds, st, p);
+    if (bnb) STEM_K(256, 128, 3);
+    else if (p.act_n == 2) STEM_K(256, 64, 2);
+    else STEM_K(256, 64, 1);
   } else {
-    if (p.act_n == 2) hipLaunchKernelGGL((stem_conv_kernel<512, 2>), grid, dim3(256), lds, st, p);
-    else hipLaunchKernelGGL((stem_conv_kernel<512, 1>), grid, dim3(256), lds, st, p);
+    if (p.act_n == 2) STEM_K(512, 64, 2);
+    else STEM_K(512, 64, 1);
   }
+#undef STEM_K
   main_timer_end(st);
   STC_CHECK_LAUNCH();
   return 0;

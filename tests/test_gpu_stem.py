@@ -45,3 +45,49 @@ def test_stem_conv_act(case):
     got = F.leaky_relu(ref, 0.2)
     err = float((y1.permute(0, 3, 1, 2).float() - got).abs().max())
     assert err <= 1e-2 * float(got.abs().max())
+
+
+class _BNT:
+    def __init__(self, C, seed):
+        g = torch.Generator().manual_seed(seed)
+        self.scale = (torch.rand(C, generator=g) + 0.5).to(DEV)
+        self.shift = (torch.randn(C, generator=g) * 0.2).to(DEV)
+        self.mean = (torch.randn(C, generator=g) * 0.1).to(DEV)
+        self.rstd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+        self.gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+
+
+@pytest.mark.parametrize("with_other", [False, True], ids=["no_other", "g_other"])
+def test_stem_bn_backward(with_other):
+    """G's output-layer input gradient (dq 256x256x8 -> the 128-channel concat gradient at 128x128) with the
+    up-path BN's backward sums on channels 64..127: the streaming kernel against the im2col tile + the separate BN
+    backward (same outputs bit for bit, sums within fp32 reordering)."""
+    B, Cin, Cout, C, ch_off = 4, 8, 128, 64, 64
+    g = torch.Generator(device=DEV).manual_seed(7 + with_other)
+    wt = torch.randn((Cin, Cout, 4, 4), generator=g, device=DEV) * 0.05  # the ConvT weight [8][128]
+    w = ops.pack(L.PACK_CONVT_DGRAD, wt, Cout, Cin, BF)
+    dq = (torch.randn((B, 256, 256, Cin), generator=g, device=DEV) * 0.5).to(BF)
+    x = torch.randn((B, 128, 128, C), generator=g, device=DEV).to(BF)
+    go = torch.randn((B, 128, 128, C), generator=g, device=DEV).to(BF) if with_other else None
+    bn = _BNT(C, 55)
+    st = (bn.scale, bn.shift, bn.mean, bn.rstd)
+    assert ops.conv_query(L.CONV_S2, B, 128, 128, Cin, Cout, BF)[2][4] != ops.HALO_CFG
+    out1 = torch.zeros((B, 128, 128, Cout), device=DEV, dtype=BF)
+    dx1 = torch.empty((B, 128, 128, C), device=DEV, dtype=BF)
+    dg1, db1 = ops.conv_bn_backward(L.CONV_S2, B, L.nhwc_view(dq), Cin, w, Cout, L.nhwc_view(out1), BF,
+                                    bn_x=L.nhwc_view(x), C=C, bn_state=st, gamma=bn.gamma, s_self=0.0, ch_off=ch_off,
+                                    g_other=None if go is None else L.nhwc_view(go), s_other=0.2,
+                                    dxv=L.nhwc_view(dx1))
+    out2 = torch.zeros((B, 128, 128, Cout), device=DEV, dtype=BF)
+    ops.conv(L.CONV_S2, B, L.nhwc_view(dq), Cin, w, Cout, L.nhwc_view(out2), BF)
+    dx2 = torch.empty((B, 128, 128, C), device=DEV, dtype=BF)
+    dg2, db2 = ops.bn_backward(B, L.nhwc_view(x), C, BF, L.nhwc_view(dx2), g1=L.nhwc_view(out2, ch_off), s1=0.0,
+                               g2=None if go is None else L.nhwc_view(go), s2=0.2,
+                               bn_state=(bn.scale, bn.shift, bn.mean, bn.rstd, bn.gamma))
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
+    for a, b_, nm in ((dg1, dg2, "dgamma"), (db1, db2, "dbeta")):
+        err = float((a - b_).abs().max())
+        assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm}: {err:.3e}"
+    err = float((dx1.float() - dx2.float()).abs().max())
+    assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx: {err:.3e}"
