@@ -58,3 +58,18 @@ t_f = timed(lambda: ops.conv_bn_backward(L.CONV_S2, B, L.nhwc_view(dq), 8, wd, C
                                          ch_off=64, dxv=L.nhwc_view(dx)))
 byt = B * W * W * 8 * 2 + B * Ho * Ho * (Cout + C) * 2
 print(f"BN-backward input gradient (stem + BN apply): {t_f:6.1f} us  (conv part compulsory {byt / 1e6:.0f} MB)", flush=True)
+
+# the PatchGAN logits layer's input gradient with layer 4's BN-backward sums (dy 30x30x8 -> 31x31x512)
+wt = torch.randn((8, 512, 4, 4), device=dev) * 0.05
+ws1 = ops.pack(L.PACK_CONV_S1_DGRAD, wt, 512, 8, BF)
+dy = torch.randn((B, 30, 30, 8), device=dev).to(BF)
+bx = torch.randn((B, 31, 31, 512), device=dev).to(BF)
+out = torch.empty((B, 31, 31, 512), device=dev, dtype=BF)
+dx = torch.empty((B, 31, 31, 512), device=dev, dtype=BF)
+tabs = [torch.rand(512, device=dev) + 0.5 for _ in range(5)]
+t_l = timed(lambda: ops.conv_bn_backward(L.CONV_S1_DGRAD, B, L.nhwc_view(dy), 8, ws1, 512, L.nhwc_view(out), BF,
+                                         bn_x=L.nhwc_view(bx), C=512, bn_state=tuple(tabs[:4]), gamma=tabs[4],
+                                         s_self=0.2, dxv=L.nhwc_view(dx)))
+t_a = timed(lambda: ops.bn_backward(B, L.nhwc_view(bx), 512, BF, L.nhwc_view(dx), g1=L.nhwc_view(out), s1=0.2,
+                                    bn_state=tuple(tabs)))
+print(f"logits-layer input gradient + BN backward: {t_l:6.1f} us (the BN-backward pair alone {t_a:6.1f} us)", flush=True)

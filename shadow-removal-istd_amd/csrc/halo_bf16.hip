@@ -430,7 +430,10 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
   const dim3 grid((unsigned)blocks);
   const bool bnb = p.part2 != nullptr;
   // >= 512 blocks: the 4-wave 80 KiB block, two per CU; fewer: the 8-wave block (one per CU, all CUs busy)
-  const bool two = shape == 2 || (shape != 1 && blocks >= 512) || bn == 64;
+#ifndef STC_EXP_TWO_MIN
+#define STC_EXP_TWO_MIN 512
+#endif
+  const bool two = shape == 2 || (shape != 1 && blocks >= STC_EXP_TWO_MIN) || bn == 64;
 #define STC_HK(G_, GW_, BN_, B_, RB_, WM_, WN_)                                                               \
   hipLaunchKernelGGL((halo_conv_kernel<G_, GW_, BN_, B_, RB_, WM_, WN_>), grid, dim3(64 * WM_ * WN_),         \
                      (HaloGeom<RB_, BN_>::LDS), st, p)

@@ -874,9 +874,12 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
     const Geometry g = geometry(kind);
     const int Hg = kind == STC_CONVT_S2 ? dy.H : out.H, Wg = kind == STC_CONVT_S2 ? dy.W : out.W;
     int32_t need = stem_bnb_chunks(kind, B, Hg, Wg, Cin, Cout);
-    if (need) {  // the streaming Cin = 8 kernel: a dense 8-channel input view
+    if (need && kind == STC_CONV_S2) {  // the streaming Cin = 8 kernel: a dense 8-channel input view
       STC_REQUIRE(dy.cs == 1 && dy.ps == 8 && dy.co == 0 && out.H * 2 == dy.H && out.W * 2 == dy.W,
                   "stc_conv_bwd_bn: the 8-channel input of this shape must be a dense NHWC tensor");
+    } else if (need) {  // the logits layer's input gradient: no second gradient
+      STC_REQUIRE(!bnb->g_other.p && dy.cs == 1 && dy.ps % 8 == 0 && dy.co % 8 == 0,
+                  "stc_conv_bwd_bn: the 31x31 logits-layer input gradient takes no second gradient");
     } else {
       bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &need, nullptr);
     }

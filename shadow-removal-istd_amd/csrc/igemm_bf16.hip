@@ -806,6 +806,8 @@ int halo_launch(GParams& p, hipStream_t st, int shape);
 // the Cin = 8 first layers with the activation epilogue (stem_bf16.hip)
 bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y, bool bnb);
 int stem_launch(GParams& p, hipStream_t st);
+bool stem_s1d_eligible(int kind, int B, const stc_view& dy, int Cin, int Cout, const stc_view& y);
+int stem_s1d_launch(GParams& p, hipStream_t st);
 static bool halo_plan(const int32_t* force, int kind, int B, int GH, int GW, int Cin, int Cout) {
   if (force && force[0] == HALO_CFG) return halo_geometry_ok(kind, B, GH, GW, Cin, Cout);
   return (!force || force[0] == -1) && halo_auto(kind, B, GH, GW, Cin, Cout);
@@ -890,6 +892,10 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
     if (act_n == 2) {
       p.c2 = (char*)act2->p; p.c2_bs = act2->bs; p.c2_rs = act2->rs; p.c2_ps = act2->ps; p.c2_co = act2->co;
     }
+  }
+  if (p.vec_out && !force && !stats && bnb && !bnb->g_other.p && stem_s1d_eligible(kind, B, x, Cin, Cout, y)) {
+    p.ws = nullptr;
+    return stem_s1d_launch(p, st);
   }
   if (p.vec_out && !force && !stats && (act_n || bnb) && stem_eligible(kind, B, x, Cin, Cout, y, bnb != nullptr)) {
     p.ws = nullptr;

@@ -215,6 +215,144 @@ __global__ void __launch_bounds__(256) stem_conv_kernel(const GParams p) {
   }
 }
 
+// ---- the PatchGAN logits layer's input gradient (Conv2d k4 s1 p1, 512 -> 1 at 31 -> 30; STCGAN/networks.py:183-184):
+// dy (30 x 30, the 1 real channel padded to 8) -> 31 x 31 x 512 with the layer-4 BatchNorm's backward sums fused in
+// (stc_conv_bwd_bn, kind STC_CONV_S1_DGRAD).  out(y, x) = sum_{ky,kx} dy[y + 1 - ky][x + 1 - kx] w[ky][kx]: K = 128, so
+// the launch is the 31.5 MB output + the 31.5 MB BN input.  A block = (image, 8-row strip, 128 output channels); the
+// strip's 11 dy rows (5 KiB) are staged once; its 16 tasks (output row x 16-pixel half) go round-robin to the 4 waves,
+// each task's BN-input loads issued one task ahead.
+constexpr int S1D_W = 31, S1D_PAD = 32;
+__global__ void __launch_bounds__(256) stem_s1d_kernel(const GParams p) {
+  constexpr int NF = 8, CPX = 16, PXS = 4, NPASS = 4;  // 128 channels: 16-byte chunks per pixel, store passes
+  constexpr int PITCH = 128 * 2 + 16;
+  constexpr int NRW = STEM_RB + 3;                     // staged dy rows
+  __shared__ __attribute__((aligned(16))) char dys[NRW * S1D_PAD * 16];
+  __shared__ __attribute__((aligned(16))) char stgs[4 * 16 * PITCH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* stg = stgs + wave * 16 * PITCH;
+  const int nslices = p.N / 128, strips = (p.GH + STEM_RB - 1) / STEM_RB;
+  int bid = blockIdx.x;
+  const int ns = bid % nslices;
+  bid /= nslices;
+  const int strip = bid % strips, img = bid / strips;
+  const int y0 = strip * STEM_RB, n0 = ns * 128;
+  const int rl = lane & 15, kq = lane >> 4;
+  // dy rows y0 - 2 .. y0 + 8 (local r), columns 0 .. 31 (>= IW: zero)
+  for (int i = tid; i < NRW * S1D_PAD; i += 256) {
+    const int r = i / S1D_PAD, c = i % S1D_PAD, gy = y0 - 2 + r;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if ((unsigned)gy < (unsigned)p.IH && c < p.IW)
+      v = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.a) + (long long)img * p.a_bs +
+                                          (long long)gy * p.a_rs + (long long)c * p.a_ps + p.a_co);
+    *reinterpret_cast<uint4*>(dys + i * 16) = v;
+  }
+  bf16x8_t wf[NF][4];
+#pragma unroll
+  for (int j = 0; j < NF; ++j)
+#pragma unroll
+    for (int ky = 0; ky < 4; ++ky)
+      wf[j][ky] = *reinterpret_cast<const bf16x8_t*>(reinterpret_cast<const bf16*>(p.b) + (n0 + 16 * j + rl) * 128 +
+                                                     (4 * ky + kq) * 8);
+  const int sc = lane % CPX, spx = lane / CPX;
+  const int nb = n0 + sc * 8 - p.bch_off;
+  const bool bn_lane = nb >= 0 && nb < p.bC;
+  const int nbc = bn_lane ? nb : 0;
+  float bsc[8], bsh[8], bmu[8], brs[8], sa[8], sb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bsc[e] = p.bsc[nbc + e]; bsh[e] = p.bsh[nbc + e]; bmu[e] = p.bmu[nbc + e]; brs[e] = p.brs[nbc + e];
+    sa[e] = 0.f; sb[e] = 0.f;
+  }
+  const bf16x8_t zero8 = {};
+  __syncthreads();
+  // task k of this wave: output row y0 + (k >> 1) within the image, pixels 16 (k & 1) .. + 15
+  const int ntask = 2 * min(STEM_RB, p.GH - y0);
+  auto bn_load = [&](int k, uint4 (&v)[NPASS]) {
+    const int y = y0 + (k >> 1);
+#pragma unroll
+    for (int h = 0; h < NPASS; ++h) {
+      const int x = 16 * (k & 1) + spx + PXS * h;
+      const bool in = k < ntask && y < p.bxH && x < p.bxW;
+      v[h] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.bx) + (long long)img * p.bx_bs +
+                                             (long long)(in ? y : 0) * p.bx_rs + (long long)(in ? x : 0) * p.bx_ps +
+                                             p.bx_co + nbc);
+    }
+  };
+  uint4 cur[NPASS], nxt[NPASS];
+  bn_load(wave, cur);
+  for (int k = wave; k < ntask; k += 4) {
+    bn_load(k + 4, nxt);
+    const int yl = k >> 1, y = y0 + yl;
+    const int px = 16 * (k & 1) + rl;
+    floatx4 acc[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ky = 0; ky < 4; ++ky) {
+      const int col = px + 1 - kq;  // dy column of tap kx = kq; dy row y + 1 - ky = local row yl + 3 - ky
+      const bool cok = (unsigned)col < (unsigned)S1D_PAD;
+      bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(dys + ((yl + 3 - ky) * S1D_PAD + (cok ? col : 0)) * 16);
+      a = cok ? a : zero8;
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[j] = exp_mfma(a, wf[j][ky], acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned u = pack_bf16x2(acc[j][e], 0.f) & 0xffffu;
+        *reinterpret_cast<unsigned short*>(stg + (4 * kq + e) * PITCH + (16 * j + rl) * 2) = (unsigned short)u;
+      }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < NPASS; ++h) {
+      const int spix = spx + PXS * h;
+      const int x = 16 * (k & 1) + spix;
+      if (x >= p.GW) continue;  // (pixel 31 of the 32-wide task)
+      const uint4 tv = *reinterpret_cast<const uint4*>(stg + spix * PITCH + sc * 16);
+      const long long o = (long long)img * p.c_bs + (long long)y * p.c_rs + (long long)x * p.c_ps + p.c_co + n0 + sc * 8;
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + o) = tv;
+      if (bn_lane && y < p.bxH && x < p.bxW) {
+        const unsigned wt[4] = {tv.x, tv.y, tv.z, tv.w};
+        const unsigned wx[4] = {cur[h].x, cur[h].y, cur[h].z, cur[h].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = __uint_as_float((e & 1) ? (wt[e >> 1] & 0xffff0000u) : (wt[e >> 1] << 16));
+          const float xv = __uint_as_float((e & 1) ? (wx[e >> 1] & 0xffff0000u) : (wx[e >> 1] << 16));
+          const float nn = fmaf(xv, bsc[e], bsh[e]);
+          const float dn = v * (nn > 0.f ? 1.f : p.bs_self);
+          sa[e] += dn;
+          sb[e] += dn * (xv - bmu[e]) * brs[e];
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < NPASS; ++h) cur[h] = nxt[h];
+  }
+  // block partial of this slice's channels (threads sharing a chunk, thread order), through the staging LDS
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(stgs);  // [256][16] = 16 KiB <= 17 KiB
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[tid * 16 + e] = sa[e]; red[tid * 16 + 8 + e] = sb[e]; }
+  __syncthreads();
+  if (tid < CPX) {
+    const int ch0 = n0 + tid * 8 - p.bch_off;
+    if (ch0 >= 0 && ch0 < p.bC) {
+      float ta[8], tb[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { ta[e] = 0.f; tb[e] = 0.f; }
+      for (int q = tid; q < 256; q += CPX)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { ta[e] += red[q * 16 + e]; tb[e] += red[q * 16 + 8 + e]; }
+      const long long tile = (long long)img * strips + strip;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        *reinterpret_cast<float2*>(p.part2 + (tile * p.bC + ch0 + e) * 2) = make_float2(ta[e], tb[e]);
+    }
+  }
+}
+
 // Eligible: Conv2d k4 s2 p1, 8 input channels (a dense 16-byte bf16 pixel at channel offset 0), input width 256 or
 // 512, output rows a multiple of 8, 16-byte NHWC output views; 64 outputs with the activation epilogue, or 128
 // outputs with the fused BN-backward sums (input width 256).
@@ -229,9 +367,30 @@ bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const 
   return (long long)B * x.bs * 2 < (1ll << 31);
 }
 
-// BN-backward partial count of the fused input gradient when it takes this kernel (0: it does not)
+// the logits layer's input gradient: 8 (padded) dy channels, 128-channel slices, the 31 x 31 grid
+static bool s1d_sizes(int kind, int Cin, int Cout, int Hg, int Wg) {
+  return kind == STC_CONV_S1_DGRAD && Cin == 8 && Cout % 128 == 0 && Hg == S1D_W && Wg == S1D_W;
+}
+
+// BN-backward partial count of the fused input gradient when it takes one of these kernels (0: it does not)
 int stem_bnb_chunks(int kind, int B, int Hg, int Wg, int Cin, int Cout) {
+  if (s1d_sizes(kind, Cin, Cout, Hg, Wg)) return B * ((Hg + STEM_RB - 1) / STEM_RB);
   return stem_sizes(kind, Cin, Cout, Hg, Wg, true) ? B * (Hg / STEM_RB) : 0;
+}
+
+bool stem_s1d_eligible(int kind, int B, const stc_view& dy, int Cin, int Cout, const stc_view& y) {
+  return s1d_sizes(kind, Cin, Cout, y.H, y.W) && dy.H == y.H - 1 && dy.W == y.W - 1 && dy.cs == 1 && dy.ps % 8 == 0 &&
+         dy.co % 8 == 0;
+}
+
+int stem_s1d_launch(GParams& p, hipStream_t st) {
+  const int B = p.M / (p.GH * p.GW);
+  const dim3 grid((unsigned)(B * ((p.GH + STEM_RB - 1) / STEM_RB) * (p.N / 128)));
+  main_timer_begin(st);
+  hipLaunchKernelGGL(stem_s1d_kernel, grid, dim3(256), 0, st, p);
+  main_timer_end(st);
+  STC_CHECK_LAUNCH();
+  return 0;
 }
 
 int stem_launch(GParams& p, hipStream_t st) {

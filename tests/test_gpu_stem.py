@@ -91,3 +91,38 @@ def test_stem_bn_backward(with_other):
         assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm}: {err:.3e}"
     err = float((dx1.float() - dx2.float()).abs().max())
     assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx: {err:.3e}"
+
+
+@pytest.mark.parametrize("B", [32, 3])
+def test_stem_logits_dgrad_bn_backward(B):
+    """The PatchGAN logits layer's input gradient (dy 30x30, 1 channel padded to 8 -> 31x31x512) with layer 4's
+    BatchNorm-backward sums: the streaming kernel against the im2col conv + the separate BN backward."""
+    Cin, Cout, C = 8, 512, 512
+    g = torch.Generator(device=DEV).manual_seed(11 + B)
+    wt = torch.zeros((Cin, Cout, 4, 4), device=DEV)
+    wt[:1] = torch.randn((1, Cout, 4, 4), generator=g, device=DEV) * 0.05  # conv weight [1 (padded 8)][512]
+    w = ops.pack(L.PACK_CONV_S1_DGRAD, wt, Cout, Cin, BF)
+    dy = torch.zeros((B, 30, 30, Cin), device=DEV, dtype=BF)
+    dy[..., :1] = (torch.randn((B, 30, 30, 1), generator=g, device=DEV) * 0.5).to(BF)
+    x = torch.randn((B, 31, 31, C), generator=g, device=DEV).to(BF)
+    bn = _BNT(C, 57)
+    st = (bn.scale, bn.shift, bn.mean, bn.rstd)
+    out1 = torch.zeros((B, 31, 31, Cout), device=DEV, dtype=BF)
+    dx1 = torch.empty((B, 31, 31, C), device=DEV, dtype=BF)
+    dg1, db1 = ops.conv_bn_backward(L.CONV_S1_DGRAD, B, L.nhwc_view(dy), Cin, w, Cout, L.nhwc_view(out1), BF,
+                                    bn_x=L.nhwc_view(x), C=C, bn_state=st, gamma=bn.gamma, s_self=0.2,
+                                    dxv=L.nhwc_view(dx1))
+    out2 = torch.zeros((B, 31, 31, Cout), device=DEV, dtype=BF)
+    ops.conv(L.CONV_S1_DGRAD, B, L.nhwc_view(dy), Cin, w, Cout, L.nhwc_view(out2), BF)
+    dx2 = torch.empty((B, 31, 31, C), device=DEV, dtype=BF)
+    dg2, db2 = ops.bn_backward(B, L.nhwc_view(x), C, BF, L.nhwc_view(dx2), g1=L.nhwc_view(out2), s1=0.2,
+                               bn_state=(bn.scale, bn.shift, bn.mean, bn.rstd, bn.gamma))
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
+    ref = torch.nn.functional.conv_transpose2d(dy.permute(0, 3, 1, 2).float(), wt.to(BF).float(), None, 1, 1)
+    assert float((out1.permute(0, 3, 1, 2).float() - ref).abs().max()) <= 1e-2 * float(ref.abs().max())
+    for a, b_, nm in ((dg1, dg2, "dgamma"), (db1, db2, "dbeta")):
+        err = float((a - b_).abs().max())
+        assert err <= 1e-4 * float(b_.abs().max()) + 1e-5, f"{nm}: {err:.3e}"
+    err = float((dx1.float() - dx2.float()).abs().max())
+    assert err <= 1e-2 * float(dx2.float().abs().max()), f"dx: {err:.3e}"
