@@ -18,6 +18,8 @@
 // every B fragment), narrow_wk_kernel (the default) splits the K dimension over them (each fragment
 // loaded once per block), sums the waves' partials through LDS in a fixed order and stores the output
 // tile from LDS with row / pixel vector stores.
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace stc {
@@ -40,13 +42,16 @@ struct HParams {
   float* ws;  // [split][Mtot][NP] when nsplit > 1
   long long Mtot;  // B * GH * GW
   const char* frag;  // B fragment table (narrow_bfrag_kernel), in the workspace
+  int smode;         // narrow_stream_kernel output stores: 0 scalar, 1 NHWC 16-byte pixels, 2 NCHW fp32 rows
 };
 
 typedef __bf16 bf16x8_h __attribute__((ext_vector_type(8)));
 using lds_vptr_h = __attribute__((address_space(3))) void*;
 
 __device__ __forceinline__ void hdma16(__amdgpu_buffer_rsrc_t r, char* lds_dst, unsigned voff) {
+#if !STC_EXP_NODMA  // diagnostic builds only (common.hpp)
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr_h)lds_dst, 16, voff, 0, 0, 0);
+#endif
 }
 
 __device__ __forceinline__ void store_out(const HParams& p, long long off, float v) {
@@ -444,6 +449,201 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) n
   }
 }
 
+// ---- streaming ConvT (GEOM 0) for the HBM-bound full-resolution edges: the generator output layer (CIN 128, N 1|3)
+// and the first convs' input gradients (CIN 64, N 8).  A block owns one image's strip of SR grid rows x 64 grid
+// columns (16 per wave, all CIN channels); its SR + 2 input rows (66 pixels each: one halo column either side) flow
+// through an NS-slot LDS ring by LDS-DMA, NS - 1 rows ahead of the MFMAs, so each input pixel crosses HBM once per
+// strip (+2/SR for the halo rows) and ~50 KiB per block are in flight.  Grid row gy reads input rows gy-1, gy, gy+1:
+// each staged row's A fragments (3 column shifts x CIN/32 K-steps) are read once and feed the three output rows it
+// touches, accumulated in three rotating register tiles; a row is complete (and stored, + bias, tanh) two input rows
+// after it started.  The whole CIN x 9 x N' B-fragment table lives in registers.  LDS rows: pixel-major, 16-byte
+// channel chunks XOR-swizzled by pixel (conflict-free A reads).  Every wave's VMEM count per iteration is known
+// (its DMA pieces per row + 4 NB stores per output row), so the ring waits are exact counted vmcnt.
+constexpr int NS_SR = 16;  // grid rows per block strip
+constexpr int NS_TW = 64;  // grid columns per block
+
+__device__ __forceinline__ void vm_wait_dyn(int n) {
+  switch (n) {
+#define STC_VW(k) case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(k) : "memory"); return;
+#define STC_VW8(k) STC_VW(k) STC_VW(k + 1) STC_VW(k + 2) STC_VW(k + 3) STC_VW(k + 4) STC_VW(k + 5) STC_VW(k + 6) STC_VW(k + 7)
+    STC_VW8(0) STC_VW8(8) STC_VW8(16) STC_VW8(24) STC_VW8(32) STC_VW8(40) STC_VW8(48) STC_VW8(56)
+#undef STC_VW8
+#undef STC_VW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); return;
+  }
+}
+
+template <int CIN, int NB, int NS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) narrow_stream_kernel(const HParams p) {
+  constexpr int PXB = CIN * 2;                       // bytes per staged pixel
+  constexpr int CH = CIN / 8;                        // 16-byte chunks per pixel
+  constexpr int SH = CIN == 64 ? 1 : 0;              // swizzle: chunk ^ ((pixel >> SH) & (CH - 1))
+  constexpr int RPX = NS_TW + 2;                     // staged pixels per row
+  constexpr int PIECES = (RPX * PXB + 1023) / 1024;  // 1 KiB DMA pieces per row
+  constexpr int SLOT = PIECES * 1024;
+  constexpr int KK = CIN / 32;                       // MFMA K-steps per pixel
+  constexpr int PD = NS - 1;                         // rows of DMA ahead
+  constexpr int NROW = NS_SR + 2;                    // input rows per strip
+  constexpr int PWMAX = (PIECES + 3) / 4;
+  static_assert((PD - 1) * PWMAX + PD * 4 * NB <= 63, "narrow stream: vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int strips = p.GH / NS_SR, cols = p.GW / NS_TW;
+  int bid = blockIdx.x;
+  const int cb = bid % cols;
+  bid /= cols;
+  const int strip = bid % strips, img = bid / strips;
+  const int y0 = strip * NS_SR, x0 = cb * NS_TW;
+  const int pw = (PIECES - wave + 3) / 4;  // this wave's DMA pieces per row
+  char* stg = smem + NS * SLOT + wave * 2048;  // the wave's output staging (smode 1 / 2)
+  const int spr = STC_EXP_NOEPI ? 0 : (p.smode == 0 ? 4 * NB : 1);  // store instructions per output row
+
+  // B fragments (K-step k = 64-channel chunk * 2 + half, neighbour nb = (dy+1)*3 + (dx+1), column block j)
+  const uint4* frag = reinterpret_cast<const uint4*>(p.frag);
+  bf16x8_h bfr[KK][9][NB];
+#pragma unroll
+  for (int k = 0; k < KK; ++k)
+#pragma unroll
+    for (int nb = 0; nb < 9; ++nb)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) bfr[k][nb][j] = __builtin_bit_cast(bf16x8_h, frag[((k * 9 + nb) * NB + j) * 64 + lane]);
+  // this lane's output column n' = 16 j + (lane & 15) -> (phase, channel), and its bias
+  int ph[NB], nn[NB];
+  float bz[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int np = 16 * j + (lane & 15);
+    ph[j] = np / p.N;
+    nn[j] = np - ph[j] * p.N;
+    bz[j] = (p.bias && np < p.NP) ? p.bias[nn[j]] : 0.f;
+  }
+
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, (short)0, (int)p.a_bytes, 0x00020000);
+  const unsigned OOBV = 0x80000000u;
+  auto issue = [&](int t) {  // input row y0 - 1 + t -> slot t % NS
+    const int iy = y0 - 1 + t;
+    const bool rok = (unsigned)iy < (unsigned)p.IH;
+    char* dst = smem + (t % NS) * SLOT;
+#pragma unroll
+    for (int k = 0; k < PWMAX; ++k) {
+      const int pc = wave + 4 * k;
+      if (pc >= PIECES) break;
+      const int o = pc * 1024 + lane * 16;
+      const int pix = o / PXB, s = (o % PXB) >> 4;
+      const int c = s ^ ((pix >> SH) & (CH - 1));
+      const int ix = x0 - 1 + pix;
+      const bool ok = rok && pix < RPX && (unsigned)ix < (unsigned)p.IW;
+      const unsigned off = (((unsigned)(img * p.a_bs + iy * p.a_rs + ix * p.a_ps + p.a_co + 8 * c)) * 2u) |
+                           (ok ? 0u : OOBV);
+      hdma16(ra, dst + pc * 1024, ok ? off : OOBV);
+    }
+  };
+
+  floatx4 acc[3][NB];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[q][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < PD; ++t) issue(t);
+
+  const int rl = lane & 15, cq = lane >> 4;
+  auto step = [&](int t, auto tm3) {
+    constexpr int T3 = decltype(tm3)::value;  // t % 3
+    // VMEM ops this wave issued after row t's DMA: rows t+1 .. t+PD-1 (those that exist) and the stores of the
+    // iterations from row t's issue on (iterations >= 2 store)
+    const int nrows = min(PD - 1, NROW - 1 - t);
+    const int s0 = t < PD ? 0 : t - PD;
+    const int nst = max(0, t - max(2, s0));
+    vm_wait_dyn(nrows * pw + nst * spr);
+    __builtin_amdgcn_s_barrier();
+    if (t + PD < NROW) issue(t + PD);  // into the slot of row t - 1, which every wave finished before the barrier
+    // row t: output rows q = t - 1 - dy (dy = -1, 0, 1) -> register tiles (t - 1 - dy) % 3
+    constexpr int QA = T3, QB = (T3 + 2) % 3, QC = (T3 + 1) % 3;  // dy = -1, 0, +1
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[QA][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const char* row = smem + (t % NS) * SLOT;
+#pragma unroll
+    for (int k = 0; k < KK; ++k) {
+      const int c = 4 * k + cq;
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int pix = 16 * wave + rl + dx;
+        const bf16x8_h a = *reinterpret_cast<const bf16x8_h*>(row + pix * PXB + ((c ^ ((pix >> SH) & (CH - 1))) << 4));
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          acc[QA][j] = exp_mfma(a, bfr[k][0 * 3 + dx][j], acc[QA][j]);
+          acc[QB][j] = exp_mfma(a, bfr[k][1 * 3 + dx][j], acc[QB][j]);
+          acc[QC][j] = exp_mfma(a, bfr[k][2 * 3 + dx][j], acc[QC][j]);
+        }
+      }
+    }
+    // output row q = t - 2 is complete: acc[QC][j][e] = grid point (y0 + q, x0 + 16 wave + 4 cq + e), column n'
+    if (!STC_EXP_NOEPI && t >= 2) {
+      const int gy = y0 + t - 2;
+      if (p.smode == 0) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const bool on = 16 * j + rl < p.NP;
+          const int oy = 2 * gy + (ph[j] >> 1);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int gx = x0 + 16 * wave + 4 * cq + e;
+            float v = acc[QC][j][e] + bz[j];
+            if (p.tanh_) v = tanhf(v);
+            const long long off = (long long)img * p.c_bs + (long long)oy * p.c_rs +
+                                  (long long)(2 * gx + (ph[j] & 1)) * p.c_ps + (long long)(p.c_co + nn[j]) * p.c_cs;
+            if (on) store_out(p, off, v);
+          }
+        }
+      } else {
+        // the wave's 2 x 32 output pixels x N channels through its LDS staging area, then one 16-byte store per
+        // lane: smode 1 = [row][pixel][N] (a pixel's N channels are 16 bytes), smode 2 = [n][row][pixel] fp32
+        const int esz = p.out_f32 ? 4 : 2;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if (16 * j + rl >= p.NP) continue;
+          const int row = ph[j] >> 1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int px = 2 * (4 * cq + e) + (ph[j] & 1);
+            float v = acc[QC][j][e] + bz[j];
+            if (p.tanh_) v = tanhf(v);
+            const int o = p.smode == 1 ? ((row * 32 + px) * p.N + nn[j]) * esz : ((nn[j] * 2 + row) * 32 + px) * 4;
+            if (p.out_f32) *reinterpret_cast<float*>(stg + o) = v;
+            else *reinterpret_cast<unsigned short*>(stg + o) = (unsigned short)(pack_bf16x2(v, 0.f) & 0xffffu);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int ox0 = 2 * (x0 + 16 * wave);
+        if (p.smode == 1) {  // lane = (row, pixel)
+          const int row = lane >> 5, px = lane & 31;
+          const uint4 v = *reinterpret_cast<const uint4*>(stg + (row * 32 + px) * 16);
+          const long long off = (long long)img * p.c_bs + (long long)(2 * gy + row) * p.c_rs +
+                                (long long)(ox0 + px) * p.c_ps + p.c_co;
+          *reinterpret_cast<uint4*>(p.c + off * esz) = v;
+        } else if (lane < 16 * p.N) {  // lane = (n, row, 4-pixel quad)
+          const int n = lane >> 4, row = (lane >> 3) & 1, qd = lane & 7;
+          const uint4 v = *reinterpret_cast<const uint4*>(stg + ((n * 2 + row) * 32 + 4 * qd) * 4);
+          const long long off = (long long)img * p.c_bs + (long long)(2 * gy + row) * p.c_rs + (ox0 + 4 * qd) +
+                                (long long)(p.c_co + n) * p.c_cs;
+          *reinterpret_cast<uint4*>(p.c + off * 4) = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  };
+  // NROW = 18 = 6 x 3 iterations, unrolled by 3 so the register tiles rotate at compile time
+  static_assert(NROW % 3 == 0, "narrow stream: strip rows + 2 must be a multiple of 3");
+  for (int t = 0; t < NROW; t += 3) {
+    step(t, std::integral_constant<int, 0>{});
+    step(t + 1, std::integral_constant<int, 1>{});
+    step(t + 2, std::integral_constant<int, 2>{});
+  }
+}
+
 // split-K combine: out = epi(sum_s ws[s][m][n'])
 template <int GEOM>
 __global__ void narrow_reduce_kernel(const HParams p, int B) {
@@ -485,17 +685,54 @@ static size_t wk_lds(int geom, int ty, int txb, int n_out, int nch) {
   return std::max(img * (size_t)nch, red + stage);
 }
 
-// Narrow plan: {ty, txb, nsplit, kernel}.  Taller / wider tiles reuse each register-held B fragment over
+// the streaming ConvT kernel's shapes: CIN 128 with N' <= 16 (the generator output layer) or CIN 64 with
+// 16 < N' <= 32 (the N = 8 first-layer input gradients); whole strips and 64-column blocks
+static bool narrow_stream_ok(int geom, int cin, int np_cols, int GH, int GW) {
+  return geom == 0 && GH % NS_SR == 0 && GW % NS_TW == 0 &&
+         ((cin == 128 && np_cols <= 16) || (cin == 64 && np_cols > 16 && np_cols <= 32));
+}
+
+// ring slots: 3 (CIN 128) / 4 (CIN 64), two blocks per CU (VGPR-bound); force {NS, 32} picks another depth (tuning).
+// Measured (scripts/ab_narrow.py, bs=32 128^2 grids): 128 -> 1|3 37.7-38.2 us at NS 3, 40 us at 4, ~60 us at 6 / 8
+// (one block per CU); 64 -> 8 32.4 us at 4, 35.4 at 6; the tiled K-split kernel 44.8 / 46.2 / 34.6 us.
+static int stream_ns(int cin, const int32_t* force) {
+  if (force && (force[1] & 32) && force[0] > 0) return force[0];
+  return cin == 128 ? 3 : 4;
+}
+
+static size_t stream_lds(int cin, int ns) {
+  const int pieces = ((NS_TW + 2) * cin * 2 + 1023) / 1024;
+  return (size_t)ns * pieces * 1024 + 4 * 2048;  // + the waves' output staging
+}
+
+// store mode of the streaming kernel's output (HParams::smode): 16-byte NHWC pixels (N x element = 16 B, 16-byte
+// aligned views), NCHW fp32 rows (unit pixel stride, 16-byte aligned rows and planes), else scalar stores
+static int stream_smode(const stc_view& y, int N, int out_f32) {
+  const int esz = out_f32 ? 4 : 2;
+  const int a = 16 / esz;  // elements per 16 bytes
+  if (y.cs == 1 && N * esz == 16 && y.ps % a == 0 && y.co % a == 0 && y.rs % a == 0 && y.bs % a == 0) return 1;
+  if (out_f32 && y.ps == 1 && N <= 4 && y.rs % 4 == 0 && y.cs % 4 == 0 && y.bs % 4 == 0 && (y.co * y.cs) % 4 == 0)
+    return 2;
+  return 0;
+}
+
+// Narrow plan: {ty, txb, nsplit, kernel}.  Kernel 2 (default where it applies): narrow_stream_kernel (force
+// {0, 32} selects it explicitly; any other forced tile takes the tiled kernels).  Taller / wider tiles reuse each register-held B fragment over
 // more MFMAs; the split over channel chunks keeps >= 1024 blocks on the long reductions.  Kernel 1 (default):
 // narrow_wk_kernel, whose block stages all its chunks at once -- the split also keeps that under 56 KiB
 // (3 blocks per CU).  force = {ty, txb (+16: the row-split narrow_halo_kernel)}.
 static void narrow_plan(int geom, int B, int GH, int GW, int cin, int np_cols, const int32_t* force, int* ty,
-                        int* txb, int* nsplit, int* kern) {
+                        int* txb, int* nsplit, int* kern, bool allow_stream = true) {
   // K-split kernel: 4 x 16 tiles (scripts/narrow_sweep.py, round 3: G output ConvT 128->1|3 41.6|43.7 us,
   // N = 8 input gradient 33.6 us, logits 21.1 us vs 60.7|60.3, 60.4, 24.7 us for the best row-split tiles)
   *ty = 4;
   *txb = 1;
   *kern = 1;
+  if (allow_stream && narrow_stream_ok(geom, cin, np_cols, GH, GW) && (!force || (force[0] == 0 && force[1] == 0) || (force[1] & 32))) {
+    *kern = 2;  // the streaming ConvT kernel: one strip per block, no split
+    *nsplit = 1;
+    return;
+  }
   if (force && force[0] > 0) {
     *ty = force[0];
     *txb = (force[1] & 15) > 0 ? (force[1] & 15) : 1;
@@ -533,7 +770,7 @@ int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout
   const int geom = kind == STC_CONVT_S2 ? 0 : 1;
   int ty, txb, ns, kern;
   const int np = geom == 0 ? 4 * Cout : Cout;
-  narrow_plan(geom, B, GH, GW, Cin, np, nullptr, &ty, &txb, &ns, &kern);
+  narrow_plan(geom, B, GH, GW, Cin, np, nullptr, &ty, &txb, &ns, &kern, false);  // (a forced tiled plan's slab)
   return (ns <= 1 ? 0 : (int64_t)ns * B * GH * GW * np * 4) + narrow_frag_bytes(geom, Cin, Cout);
 }
 
@@ -582,6 +819,25 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
       hipLaunchKernelGGL((narrow_bfrag_kernel<1, 1>), dim3(nfrag), dim3(64), 0, st, p, (uint4*)p.frag);
     }
     STC_CHECK_LAUNCH();
+  }
+  if (kern == 2) {
+    STC_REQUIRE(p.nsplit == 1 && narrow_stream_ok(geom, Cin, p.NP, p.GH, p.GW), "narrow bf16: stream plan");
+    const dim3 sgrid((unsigned)(B * (p.GH / NS_SR) * (p.GW / NS_TW)));
+    p.smode = stream_smode(y, Cout, out_f32);
+    STC_REQUIRE(p.smode == 0 || ((uintptr_t)y.p & 15) == 0, "narrow bf16: unaligned output");
+    const int nsl = stream_ns(Cin, force);
+    const size_t slds = stream_lds(Cin, nsl);
+    main_timer_begin(st);
+#define STC_NS(C_, NB_, S_) \
+  else if (Cin == C_ && nsl == S_) hipLaunchKernelGGL((narrow_stream_kernel<C_, NB_, S_>), sgrid, dim3(256), slds, st, p)
+    if (false) {}
+    STC_NS(128, 1, 4); STC_NS(128, 1, 3); STC_NS(128, 1, 6); STC_NS(128, 1, 8);
+    STC_NS(64, 2, 6); STC_NS(64, 2, 4);
+    else return fail(-1, "narrow bf16: no stream kernel with %d slots", nsl);
+#undef STC_NS
+    main_timer_end(st);
+    STC_CHECK_LAUNCH();
+    return 0;
   }
   dim3 grid((unsigned)(B * p.tiles_per_img), (unsigned)p.nsplit);
   const size_t lds = kern == 1 ? wk_lds(geom, ty, txb, Cout, p.chunks_per_split)

@@ -84,8 +84,9 @@ def plan_of(kind, B, gh, gw, cin, cout, dt):
     return tuple(out)
 
 
-def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=None, tanh=False, out_f32=False):
-    """Implicit-GEMM conv family (stc_conv_fwd)."""
+def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=None, tanh=False, out_f32=False,
+         force=None):
+    """Implicit-GEMM conv family (stc_conv_fwd; force: a forced narrow-N tile through stc_conv_fwd_ex, tests)."""
     dev = w_packed.device
     if kind == L.CONVT_S2:
         gh, gw = xv.H, xv.W
@@ -98,9 +99,14 @@ def conv(kind, B, xv, cin, w_packed, cout, yv, dt, pro=None, slope=None, bias=No
     timer = _timer
     if timer is not None:
         e0, e1 = _main_events()
-    rc = l.stc_conv_fwd(L.dtype_code(dt), kind, B, xv, cin, sc, sh, 0 if slope is None else 1,
-                        0.0 if slope is None else float(slope), ptr(w_packed), cout, yv, ptr(bias), int(tanh),
-                        int(out_f32), ptr(ws), nb, stream())
+    if force is not None:
+        assert pro is None and slope is None
+        rc = l.stc_conv_fwd_ex(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ptr(bias), int(tanh),
+                               int(out_f32), None, 0, (ctypes.c_int32 * 2)(*force), ptr(ws), nb, stream())
+    else:
+        rc = l.stc_conv_fwd(L.dtype_code(dt), kind, B, xv, cin, sc, sh, 0 if slope is None else 1,
+                            0.0 if slope is None else float(slope), ptr(w_packed), cout, yv, ptr(bias), int(tanh),
+                            int(out_f32), ptr(ws), nb, stream())
     if timer is not None:
         _disarm()
     check(rc, "stc_conv_fwd")
@@ -216,8 +222,13 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
     if narrow:
         if dt == torch.bfloat16 and cin % 64 == 0:
             geom = 0 if kind == L.CONVT_S2 else 1
-            nb = 2 if (kind == L.CONVT_S2 and 4 * cout > 16) else 1
-            return f"narrow_halo_kernel<{geom}, {nb}, 8>", ws == 0
+            npc = 4 * cout if geom == 0 else cout
+            nb = 2 if npc > 16 else 1
+            # csrc/narrow_bf16.hip narrow_plan: the streaming ConvT kernel where it applies, else the 4x16 K-split tile
+            if geom == 0 and gh % 16 == 0 and gw % 64 == 0 and ((cin == 128 and npc <= 16) or
+                                                               (cin == 64 and 16 < npc <= 32)):
+                return f"narrow_stream_kernel<{cin}, {nb}, {3 if cin == 128 else 4}>", True
+            return f"narrow_wk_kernel<{geom}, {nb}, 4, 1>", ws == 0
         return "narrow_tiled_kernel", True
     if cfg == HALO_CFG:  # the LDS-resident input halo kernels (csrc/halo_bf16.hip): template as rocprof names it
         convt = kind == L.CONVT_S2

@@ -184,6 +184,69 @@ def test_narrow_halo(case, out):
     assert err <= tol * max(scale, 1.0) * (1 if tanh else 1) + (1e-5 if tanh else 0), f"narrow {case} {out}: {err:.3e}"
 
 
+NARROW_STREAM = [  # B, Cin, N, grid H, grid W: the streaming ConvT kernel's shapes (16-row strips, 64-column blocks)
+    (2, 128, 3, 32, 64),     # generator output layer (G2: 3 channels)
+    (3, 128, 1, 16, 128),    # G1: 1 channel, two column blocks
+    (2, 64, 8, 32, 64),      # first-layer input gradient (N = 8 padded channels)
+    (1, 64, 8, 48, 192),
+    (32, 128, 3, 128, 128),  # full size (bench workload)
+    (32, 64, 8, 128, 128),
+]
+
+
+@pytest.mark.parametrize("out", ["nchw_f32", "nhwc_bf16"])
+@pytest.mark.parametrize("case", NARROW_STREAM, ids=lambda c: "_".join(map(str, c)))
+def test_narrow_stream(case, out):
+    """The streaming ConvT kernel (csrc/narrow_bf16.hip narrow_stream_kernel, the default for these shapes) vs torch
+    fp32 and vs the tiled K-split kernel forced on the same inputs (same MFMA products, another summation order)."""
+    B, Cin, N, GH, GW = case
+    assert ops.kernel_name(L.CONVT_S2, B, GH, GW, Cin, N, BF)[0].startswith("narrow_stream_kernel")
+    x = q(rnd(B, Cin, GH, GW, seed=41))
+    b = rnd(N, seed=42)
+    w = q(rnd(Cin, N, 4, 4, seed=43, scale=0.05))
+    ref = F.conv_transpose2d(x, w, b, 2, 1)
+    wp = ops.pack(L.PACK_CONVT_FWD, w.to(DEV), N, Cin, BF)
+    xg = nhwc(x).to(DEV, BF)
+    tanh = out == "nchw_f32"
+    outs = []
+    for force in (None, (4, 1)):
+        if tanh:
+            y = torch.full((B, N, 2 * GH, 2 * GW), float("nan"), device=DEV)
+            ops.conv(L.CONVT_S2, B, L.nhwc_view(xg), Cin, wp, N, L.nchw_view(y), BF, bias=b.to(DEV), tanh=True,
+                     out_f32=True, force=force)
+            outs.append(y.cpu())
+        else:
+            y = torch.full((B, 2 * GH, 2 * GW, N), float("nan"), device=DEV, dtype=BF)
+            ops.conv(L.CONVT_S2, B, L.nhwc_view(xg), Cin, wp, N, L.nhwc_view(y), BF, bias=b.to(DEV), force=force)
+            outs.append(nchw(y.float()).cpu())
+    if tanh:
+        ref = torch.tanh(ref)
+    scale = max(float(ref.abs().max()), 1.0)
+    tol = 2e-5 if tanh else 8e-3
+    for got, what in zip(outs, ("stream", "tiled")):
+        assert not torch.isnan(got).any(), f"{what}: unwritten outputs"
+        err = float((got - ref).abs().max())
+        assert err <= tol * scale + (1e-5 if tanh else 0), f"narrow {what} {case} {out}: {err:.3e}"
+    # the two kernels differ only in fp32 summation order (bf16 outputs: at most one rounding step apart)
+    d = float((outs[0] - outs[1]).abs().max())
+    assert d <= (1e-5 if tanh else 8e-3 * scale), f"stream vs tiled {case} {out}: {d:.3e}"
+
+
+def test_narrow_stream_offset_view():
+    """G2's output layer writing into a channel-offset NHWC view (the cat / objective buffers), NaN guard around it."""
+    B, Cin, N, GH, GW = 2, 128, 3, 16, 64
+    x = q(rnd(B, Cin, GH, GW, seed=44))
+    w = q(rnd(Cin, N, 4, 4, seed=45, scale=0.05))
+    ref = F.conv_transpose2d(x, w, None, 2, 1)
+    wp = ops.pack(L.PACK_CONVT_FWD, w.to(DEV), N, Cin, BF)
+    buf = torch.full((B, 2 * GH, 2 * GW, 8), float("nan"), device=DEV, dtype=BF)
+    yv = L.nhwc_view(buf, c0=4)
+    ops.conv(L.CONVT_S2, B, L.nhwc_view(nhwc(x).to(DEV, BF)), Cin, wp, N, yv, BF)
+    got = nchw(buf[..., 4:4 + N].float()).cpu()
+    assert torch.isnan(buf[..., :4].float()).all() and torch.isnan(buf[..., 4 + N:].float()).all()
+    assert float((got - ref).abs().max()) <= 8e-3 * max(float(ref.abs().max()), 1.0)
+
+
 WGRAD = [  # kind, stride, B, Cin, Cout, H, W (input grid of the forward layer)
     ("conv", 2, 2, 64, 128, 32, 32),
     ("conv", 2, 2, 8, 64, 64, 64),     # first layer: Cg = 8, 16 taps per 128-column tile
