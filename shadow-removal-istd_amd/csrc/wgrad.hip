@@ -539,13 +539,19 @@ __global__ void __launch_bounds__(256) wgrad_rows_kernel(const char* __restrict_
 
 // ---- the same weight gradient on MFMA (bf16): C[tap][ci] = sum_q Dpad[q - tap shift][r] * G[q][ci] is a 16-row
 // GEMM (M = the 16 taps of one real D row, N = channels, K = the image's pixels), so v_mfma_f32_16x16x32_bf16 takes
-// it whole: A (16 taps x 32 pixels) = lookups in the image's zero-bordered D plane (bf16 in LDS, exact), B (32 pixels
-// x 16 channels) = ds_read_b64_tr_b16 of the staged input.  Block = (image, 64-channel chunk, pixel part of <= 512):
-// its input part (<= 64 KiB, [pixel][64 ch], 16-byte chunk c of pixel p in slot c ^ 2((p >> 1) & 3): the 16 lanes of a
-// transposed read -- 4 pixels x 32 bytes -- hit 16 distinct 8-byte bank groups) is LDS-DMA'd in one go; wave w owns channels 16w .. +15.  Partial sums go to the slab
+// it whole.  K is laid out as image rows of 32 pixel slots (the input is <= 32 wide; slots past it are zero), so a
+// K-step of 32 = one input row qy and a lane's 8 K values = 8 consecutive columns of one row:
+//   A (16 taps x 32 slots): lane (tap = (kh, kw), kq) = D[qy - kh + 1][8 kq - kw + 1 ..] -- one 16-byte LDS read from
+//     the kw-shifted copy of the zero-bordered D plane (4 copies, [row][40] bf16, built once per block);
+//   B (32 slots x 16 channels): ds_read_b64_tr_b16 of the staged input.
+// Block = (image, 64-channel chunk, 16-row part): its input part ([16 rows x 32 slots][64 ch] = 64 KiB, 16-byte chunk
+// c of slot p in position c ^ 2((p >> 1) & 3): the 16 lanes of a transposed read hit 16 distinct 8-byte bank
+// groups) is LDS-DMA'd in one go; wave w owns channels 16w .. +15.  Partial sums go to the slab
 // [image * parts + part][RO][16 * Cg] (column tap * Cg + ci) for the ordered reduce, as in wgrad_rows_kernel.
-constexpr int WRM_PIX = 512;  // input pixels per block (part)
-constexpr int WRM_DPL = 12;   // D-plane elements per thread (RO x (OH + 4) x (OW + 4) <= 3072)
+constexpr int WRM_ROWS = 16;  // input rows per block (part)
+constexpr int WRM_W = 32;     // pixel slots per input row
+constexpr int WRM_PITCH = 40; // D-copy row pitch (bf16): 32 columns + pad, 16-byte rows
+constexpr int WRM_DPT = 8;    // D values per thread (RO x OH x OW <= 2048)
 
 template <int RO>
 __global__ void __launch_bounds__(256) wgrad_rows_mfma_kernel(const char* __restrict__ dp, long long d_bs, long long d_rs,
@@ -554,83 +560,83 @@ __global__ void __launch_bounds__(256) wgrad_rows_mfma_kernel(const char* __rest
                                                               int IH, int IW, int Cg, int parts, float* __restrict__ ws,
                                                               float* __restrict__ zdst, long long nzero) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* gs = smem;                                                        // [512 px][128 B]
-  unsigned short* dl = reinterpret_cast<unsigned short*>(smem + WRM_PIX * 128);  // [RO][OH + 4][OW + 4] bf16
+  char* gs = smem;                                                          // [16 x 32 slots][128 B]
+  unsigned short* dc = reinterpret_cast<unsigned short*>(smem + WRM_ROWS * WRM_W * 128);  // [RO][4 kw][OH + 5][40]
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nchunk = Cg / 64;
   int bid = blockIdx.x;
   const int part = bid % parts;
   bid /= parts;
   const int cc = bid % nchunk, b = bid / nchunk;
-  const int Q = IH * IW, q0 = part * WRM_PIX, qn = min(WRM_PIX, Q - q0);
-  // the input part by LDS-DMA: piece k (1 KiB) = pixels 8k .. 8k+7, lane -> (pixel 8k + (lane >> 3), slot lane & 7)
+  const int y0 = part * WRM_ROWS;
+  const int crow = OH + 5, cplane = crow * WRM_PITCH, ncopy = RO * 4 * cplane;
+  // 1. the D plane's loads (RO x OH x OW <= 4 x 256 values), issued before the input DMA so that waiting for them
+  //    does not wait for the DMA (VMEM completes in order)
+  const unsigned short* D = reinterpret_cast<const unsigned short*>(dp);
+  const int npl = OH * OW;
+  unsigned short dv[WRM_DPT];
+#pragma unroll
+  for (int u = 0; u < WRM_DPT; ++u) {
+    const int i = tid + 256 * u, r = i / npl, rem = i - r * npl, oy = rem / OW, ox = rem - oy * OW;
+    const bool in = i < RO * npl;
+    dv[u] = D[in ? (long long)b * d_bs + (long long)oy * d_rs + (long long)ox * d_ps + d_co + r : 0];
+  }
+  // 2. the input part by LDS-DMA: piece k (1 KiB) = slots 8k .. 8k+7, lane -> (slot 8k + (lane >> 3), position lane & 7)
   {
     const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)gp, (short)0, (int)g_bytes, 0x00020000);
     using lds_t = __attribute__((address_space(3))) void*;
 #pragma unroll
-    for (int k = 0; k < WRM_PIX / 8 / 4; ++k) {
+    for (int k = 0; k < WRM_ROWS * WRM_W / 8 / 4; ++k) {
       const int pc = wave + 4 * k;
-      const int px = 8 * pc + (lane >> 3), slot = lane & 7;
-      const int c8 = slot ^ (((px >> 1) & 3) << 1);  // the 16-byte chunk stored in this slot
-      const int q = q0 + px, qy = q / IW, qx = q - qy * IW;
-      const bool ok = px < qn;
+      const int px = 8 * pc + (lane >> 3), pos = lane & 7;
+      const int c8 = pos ^ (((px >> 1) & 3) << 1);  // the 16-byte chunk stored in this position
+      const int qy = y0 + px / WRM_W, qx = px % WRM_W;
+      const bool ok = qy < IH && qx < IW;
       const unsigned off = (unsigned)(b * g_bs + qy * g_rs + qx * g_ps + g_co + cc * 64 + 8 * c8) * 2u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rg, (lds_t)(gs + pc * 1024), 16, ok ? off : 0x80000000u, 0, 0, 0);
     }
   }
-  // the D plane (real rows 0 .. RO-1) with a 2-wide zero border: all of a thread's loads issued before any is
-  // stored (one load latency, not one per element)
-  const int prow = OW + 4, plane = (OH + 4) * prow;
-  const unsigned short* D = reinterpret_cast<const unsigned short*>(dp);
-  unsigned short dv[WRM_DPL];
-#pragma unroll
-  for (int u = 0; u < WRM_DPL; ++u) {
-    const int i = tid + 256 * u;
-    const int r = i / plane, rem = i - r * plane, yy = rem / prow, xx = rem - yy * prow;
-    const int oy = yy - 2, ox = xx - 2;
-    const bool in = i < RO * plane && oy >= 0 && oy < OH && ox >= 0 && ox < OW;
-    dv[u] = D[in ? (long long)b * d_bs + (long long)oy * d_rs + (long long)ox * d_ps + d_co + r : 0];
-    if (!in) dv[u] = 0;
-  }
+  // 3. the kw-shifted D copies: copy[r][kw][row][x] = D[row - 2][x - kw + 1][r] (0 outside), x < 32 -- zeroed, then
+  //    each D value written to its 4 positions
+  for (int i = tid; i < ncopy / 8; i += 256) *reinterpret_cast<uint4*>(dc + 8 * i) = make_uint4(0u, 0u, 0u, 0u);
   // the padded D rows' weight gradient is zero: this block's share of dW[R_out .. R)
   for (long long z = (long long)blockIdx.x * 256 + tid; z < nzero; z += (long long)gridDim.x * 256) zdst[z] = 0.f;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int u = 0; u < WRM_DPL; ++u)
-    if (tid + 256 * u < RO * plane) dl[tid + 256 * u] = dv[u];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  for (int u = 0; u < WRM_DPT; ++u) {
+    const int i = tid + 256 * u, r = i / npl, rem = i - r * npl, oy = rem / OW, ox = rem - oy * OW;
+    if (i < RO * npl) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int x = ox + k - 1;
+        if (x >= 0 && x < WRM_W) dc[(r * 4 + k) * cplane + (oy + 2) * WRM_PITCH + x] = dv[u];
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
+  // 3. K-steps = the part's input rows
   const int tap = lane & 15, kq = lane >> 4, kh = tap >> 2, kw = tap & 3;
   const int q4 = (lane & 15) >> 2, pcol = lane & 3;
+  const int nrow = STC_EXP_NOEPI ? 0 : min(WRM_ROWS, IH - y0);  // (diagnostic builds: the loads alone)
   floatx4 acc[RO];
 #pragma unroll
   for (int r = 0; r < RO; ++r) acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int nstep = STC_EXP_NOEPI ? 0 : (qn + 31) / 32;  // (diagnostic builds: the loads alone)
-  for (int s = 0; s < nstep; ++s) {
-    // A: taps x pixels 32 s + 8 kq .. + 7 of the part -> D[qy - kh + 1][qx - kw + 1] = plane (qy - kh + 3, qx - kw + 3)
-    int q = q0 + 32 * s + 8 * kq;
-    int qy = q / IW, qx = q - qy * IW;
-    unsigned short av[RO][8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const bool ok = 32 * s + 8 * kq + i < qn;
-      const int o = (qy - kh + 3) * prow + (qx - kw + 3);
-#pragma unroll
-      for (int r = 0; r < RO; ++r) av[r][i] = ok ? dl[r * plane + o] : (unsigned short)0;
-      if (++qx == IW) { qx = 0; ++qy; }
-    }
-    // B: pixels (rows) 32 s + 8 kq + q4 (+4) x channels 16 wave + 4 pcol .. + 3 (columns), transposed by the LDS
-    const int col = 16 * wave + 4 * pcol;
-    auto boff = [&](int px) { return px * 128 + 16 * ((col >> 3) ^ (((px >> 1) & 3) << 1)) + 2 * (col & 7); };
-    const int pr = 32 * s + 8 * kq + q4;
+  const int col = 16 * wave + 4 * pcol;
+  auto boff = [&](int px) { return px * 128 + 16 * ((col >> 3) ^ (((px >> 1) & 3) << 1)) + 2 * (col & 7); };
+  const unsigned short* arow = dc + kw * cplane + 8 * kq;
+  for (int s = 0; s < nrow; ++s) {
+    const int pr = WRM_W * s + 8 * kq + q4;
     const v4i16 lo = lds_tr16(gs + boff(pr)), hi = lds_tr16(gs + boff(pr + 4));
     const v4i16 bv[2] = {lo, hi};
     const stc_bf16x8 bf = __builtin_bit_cast(stc_bf16x8, bv);
+    const int arw = (y0 + s - kh + 3) * WRM_PITCH;
 #pragma unroll
     for (int r = 0; r < RO; ++r) {
-      const shortx8 a8 = {(short)av[r][0], (short)av[r][1], (short)av[r][2], (short)av[r][3],
-                          (short)av[r][4], (short)av[r][5], (short)av[r][6], (short)av[r][7]};
-      acc[r] = exp_mfma(__builtin_bit_cast(stc_bf16x8, a8), bf, acc[r]);
+      const stc_bf16x8 a = *reinterpret_cast<const stc_bf16x8*>(arow + r * 4 * cplane + arw);
+      acc[r] = exp_mfma(a, bf, acc[r]);
     }
   }
   // acc[r][e] = C[tap 4 kq + e][channel cc*64 + 16 wave + (lane & 15)] -> slab column tap * Cg + ci
@@ -661,13 +667,13 @@ extern "C" int stc_conv_wgrad_rows(int dtype, int B, stc_view D, int R, int R_ou
               D.H, D.W, G.H, G.W);
   hipStream_t st = (hipStream_t)stream;
   const int64_t need = stc_conv_wgrad_rows_workspace(B, G.H, R_out, Cg);
-  // bf16 on MFMA (wgrad_rows_mfma_kernel): 16-byte aligned input channels, <= 4 parts of 512 pixels per image
-  const int parts = (G.H * G.W + WRM_PIX - 1) / WRM_PIX;
-  const size_t lds_m = (size_t)WRM_PIX * 128 + (size_t)R_out * (D.H + 4) * (D.W + 4) * 2;
+  // bf16 on MFMA (wgrad_rows_mfma_kernel): input <= 32 x 32 (rows of 32 slots), 16-byte aligned input channels
+  const int parts = (G.H + WRM_ROWS - 1) / WRM_ROWS;
+  const size_t lds_m = (size_t)WRM_ROWS * WRM_W * 128 + (size_t)R_out * 4 * (D.H + 5) * WRM_PITCH * 2;
   const long long g_bytes = (long long)B * G.bs * 2;
-  if (dtype == STC_BF16 && G.ps % 8 == 0 && G.co % 8 == 0 && parts <= 4 && lds_m <= 80 * 1024 &&
-      (long long)R_out * (D.H + 4) * (D.W + 4) <= 256 * WRM_DPL &&
-      g_bytes < (1ll << 31) && G.bs < (1ll << 31) && G.rs < (1ll << 31)) {
+  if (dtype == STC_BF16 && G.ps % 8 == 0 && G.co % 8 == 0 && G.W <= WRM_W && G.H <= 32 && parts <= 4 &&
+      R_out * D.H * D.W <= 256 * WRM_DPT &&
+      lds_m <= 96 * 1024 && g_bytes < (1ll << 31)) {
     STC_REQUIRE(workspace && workspace_bytes >= need, "stc_conv_wgrad_rows: workspace %lld < %lld",
                 (long long)workspace_bytes, (long long)need);
     float* ws = (float*)workspace;
