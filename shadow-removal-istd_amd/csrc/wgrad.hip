@@ -386,11 +386,62 @@ __global__ void __launch_bounds__(256) wgrad_reduce_v4_kernel(const float* __res
   }
 }
 
+// The same sum for small outputs over many slabs (the first layers' 256 splits of a 64|128 x 128 dW, the logits
+// layer's 64 image parts): a block = one row r x 64 slab columns, thread = (float4 column cq, slab lane sl < 16): lane
+// sl sums slabs sl, sl + 16, ... in order with 8 loads in flight, then the 16 lanes' partials are added in lane order
+// through LDS; the wave-per-unit kernel above kept only 4 scalar loads per lane in flight (11-20 us for 256 slabs; this
+// one 5-6 us, a 512-thread variant with 32 slab lanes no faster).
+__global__ void __launch_bounds__(256) wgrad_reduce_many_kernel(const float* __restrict__ ws, int nsplit, int R, int Cg,
+                                                                int Cg_out, float* __restrict__ dW) {
+  __shared__ float4 part[16][16];
+  const int tid = threadIdx.x, cq = tid & 15, sl = tid >> 4;
+  const long long Ncol = 16LL * Cg;
+  const int nchk = (int)((Ncol + 63) / 64);
+  const int r = blockIdx.x / nchk;
+  const long long c = (long long)(blockIdx.x - r * nchk) * 64 + 4 * cq;
+  const long long slab = (long long)R * Ncol;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < Ncol) {  // (Ncol = 16 Cg is a multiple of 4: a float4 never straddles the end)
+    const float* src = ws + (long long)r * Ncol + c;
+    int sp = sl;
+    for (; sp + 16 * 7 < nsplit; sp += 16 * 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(src + (long long)(sp + 16 * u) * slab);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+    }
+    for (; sp < nsplit; sp += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (long long)sp * slab);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  part[sl][cq] = acc;
+  __syncthreads();
+  if (tid < 64) {  // column c0 + tid: the 16 lanes' partials in lane order
+    const int q = tid >> 2, e = tid & 3;
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) {
+      const float4 v = part[l][q];
+      t += e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+    }
+    const long long col = (long long)(blockIdx.x - r * nchk) * 64 + tid;
+    if (col < Ncol) {
+      const int tap = (int)(col / Cg), ci = (int)(col - (long long)tap * Cg);
+      if (ci < Cg_out) dW[((long long)r * Cg_out + ci) * 16 + tap] = t;
+    }
+  }
+}
+
 void wgrad_reduce_launch(const float* ws, int nsplit, int R, int Cg, int Cg_out, float* dW, hipStream_t st) {
   const long long units = (long long)R * Cg_out * 4;
   if (Cg % 4 == 0 && Cg_out >= 64 && !(units < 8192 && nsplit >= 16))
     hipLaunchKernelGGL(wgrad_reduce_v4_kernel, dim3((unsigned)(R * ((Cg_out + 63) / 64))), dim3(256), 0, st, ws, nsplit,
                        R, Cg, Cg_out, dW);
+  else if (units < 8192 && nsplit >= 16 && Cg % 4 == 0)
+    hipLaunchKernelGGL(wgrad_reduce_many_kernel, dim3((unsigned)(R * ((16LL * Cg + 63) / 64))), dim3(256), 0, st, ws,
+                       nsplit, R, Cg, Cg_out, dW);
   else if (units < 8192 && nsplit >= 16)
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, st, ws, nsplit, R, Cg,
                        Cg_out, dW);

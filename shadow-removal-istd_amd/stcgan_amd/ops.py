@@ -350,10 +350,10 @@ def _wgrad_kernel_name(plan, Hd, Wd):
     return f"wgrad_bf16_kernel<{bm}, {bn}, {wm}, {wn}, {sw}, {str(fast).lower()}>"
 
 
-# The narrow-R VALU weight gradient (stc_conv_wgrad_rows) for the PatchGAN logits layer (~25 us vs ~75 us
-# for the padded GEMM).  rows_kernel=False per call takes the GEMM path.  Its
-# accumulations are forced to non-packed v_fma_f32 (csrc/wgrad.hip): compiled to v_pk_fma_f32 with op_sel,
-# it returned sporadically different low-half sums with two processes on one GPU (tests/test_gpu_dist.py).
+# The narrow-R weight gradient (stc_conv_wgrad_rows) for the PatchGAN logits layer: bf16 on the MFMA rows kernel
+# (11 + 5 us with its ordered reduce, bs=32), fp32 on the VALU rows kernel (non-packed v_fma_f32: compiled to
+# v_pk_fma_f32 with op_sel it returned sporadically different low-half sums with two processes on one GPU,
+# tests/test_gpu_dist.py); ~75 us for the padded GEMM.  rows_kernel=False per call takes the GEMM path.
 _ROWS_DEFAULT = True
 
 
