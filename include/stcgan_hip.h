@@ -227,14 +227,6 @@ int stc_bn_finalize(const float* part, int nchunks, int C,
  * 1 identity).  One pass per BN'd tensor; the consuming GEMMs then stage plain operands. */
 int stc_bn_apply(int dtype, int B, stc_view x, int C, const float* scale, const float* shift,
                  stc_view y1, float slope1, stc_view y2, float slope2, void* stream);
-/* stc_bn_finalize followed by stc_bn_apply in one launch, for the small levels (C a multiple of 16,
- * B*H*W <= 2048): the same tables, running-stat update and outputs.  Returns 1 (nothing launched)
- * when the shape does not qualify -- the caller then makes the two calls.                        */
-int stc_bn_finalize_apply(int dtype, int B, stc_view x, int C, const float* part, int nchunks,
-                          const float* gamma, const float* beta, float* running_mean, float* running_var,
-                          int64_t* num_batches_tracked, float momentum, float eps, float* mean, float* rstd,
-                          float* scale, float* shift, stc_view y1, float slope1, stc_view y2, float slope2,
-                          void* stream);
 
 /* BN backward fused with the activation backward of its consumers:
  *   n  = x*scale + shift (the BN output; scale/shift from stc_bn_finalize)

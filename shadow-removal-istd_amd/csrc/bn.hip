@@ -694,164 +694,6 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(View x, PixDiv pd, long l
   }
 }
 
-// BatchNorm finalize + apply in one launch for the small layers (the generator's 8x8 .. 1x1 levels: <= 2048 pixels):
-// a block owns FA_CB channels -- each wave merges its channels' conv-epilogue partials exactly as
-// bn_finalize_wave_kernel (same order, same tables, same running-stat update) -- then applies them to every pixel of
-// those channels as bn_apply_kernel does (y1 = act(x*scale+shift, s1) [, y2 = act(.., s2)]).  Saves the separate
-// finalize launch (and its dependency gap) on the deep chain, where each costs about as much as the work.
-constexpr int FA_CB = 16;
-template <typename T>
-__global__ void __launch_bounds__(256) bn_finalize_apply_kernel(const float* part, int nchunks, int C, const float* gamma,
-                                                                const float* beta, float* rmean, float* rvar,
-                                                                long long* nbt, float momentum, float eps, float* mean_o,
-                                                                float* rstd_o, float* scale, float* shift, View x,
-                                                                PixDiv pd, long long P, View y1, float s1, View y2,
-                                                                float s2, int has2) {
-  constexpr int N = VW<T>::N;
-  __shared__ float tsc[FA_CB], tsh[FA_CB];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c0 = blockIdx.x * FA_CB;
-  for (int cl = wave; cl < FA_CB; cl += 4) {
-    const int c = c0 + cl;
-    auto load4 = [&](int k0, float4* pp) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + u * 64;
-        pp[u] = k < nchunks ? *reinterpret_cast<const float4*>(part + ((long long)k * C + c) * 4)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    };
-    double n = 0, sm = 0;
-    for (int k0 = lane; k0 < nchunks; k0 += 256) {
-      float4 pp[4];
-      load4(k0, pp);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (pp[u].x <= 0.f) continue;
-        n += pp[u].x;
-        sm += (double)pp[u].x * pp[u].w + (double)pp[u].y;
-      }
-    }
-    const double Nn = wave_sum(n), S = wave_sum(sm);
-    const double mu = Nn > 0 ? S / Nn : 0.0;
-    double m2 = 0;
-    for (int k0 = lane; k0 < nchunks; k0 += 256) {
-      float4 pp[4];
-      load4(k0, pp);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (pp[u].x <= 0.f) continue;
-        const double nb = pp[u].x, sv = pp[u].y, r = sv / nb;
-        double q = (double)pp[u].z - sv * r;
-        if (q < 0) q = 0;
-        const double d = (double)pp[u].w + r - mu;
-        m2 += q + nb * d * d;
-      }
-    }
-    const double M2 = wave_sum(m2);
-    if (lane == 0) {
-      bn_finalize_store(c, Nn, mu, M2, gamma, beta, rmean, rvar, nbt, momentum, eps, mean_o, rstd_o, scale, shift);
-      tsc[cl] = scale[c];  // (this thread's own stores)
-      tsh[cl] = shift[c];
-    }
-  }
-  __syncthreads();
-  constexpr int G = FA_CB / N;  // channel groups of the block
-  const int g = threadIdx.x % G, c = c0 + N * g;
-  float sc[N], sh[N];
-#pragma unroll
-  for (int e = 0; e < N; ++e) { sc[e] = tsc[N * g + e]; sh[e] = tsh[N * g + e]; }
-  for (long long pix = threadIdx.x / G; pix < P; pix += 256 / G) {
-    int b, yy, xx;
-    pix_bxy(pd, pix, b, yy, xx);
-    float v[N], o[N];
-    VW<T>::load(reinterpret_cast<const T*>(x.p) + vidx(x, b, yy, xx, c), v);
-#pragma unroll
-    for (int e = 0; e < N; ++e) v[e] = fmaf(v[e], sc[e], sh[e]);
-#pragma unroll
-    for (int e = 0; e < N; ++e) o[e] = act(v[e], s1);
-    VW<T>::store(reinterpret_cast<T*>(y1.p) + vidx(y1, b, yy, xx, c), o);
-    if (has2) {
-#pragma unroll
-      for (int e = 0; e < N; ++e) o[e] = act(v[e], s2);
-      VW<T>::store(reinterpret_cast<T*>(y2.p) + vidx(y2, b, yy, xx, c), o);
-    }
-  }
-}
-
-// The BatchNorm backward's finalize (dbeta, dgamma: bn_bwd_finalize_wave_kernel's merge) + apply (bn_bwd_apply_kernel's
-// arithmetic) in one launch for the small levels (<= 2048 pixels), a block per FA_CB channels.
-template <typename T>
-__global__ void __launch_bounds__(256) bn_bwd_finalize_apply_kernel(View x, PixDiv pd, long long P, int C,
-                                                                    const float* scale, const float* shift,
-                                                                    const float* mean, const float* rstd,
-                                                                    const float* gamma, GradIn gi, const float* part,
-                                                                    int nchunks, float* dgamma, float* dbeta, View dx) {
-  constexpr int N = VW<T>::N;
-  __shared__ float tdg[FA_CB], tdb[FA_CB];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c0 = blockIdx.x * FA_CB;
-  for (int cl = wave; cl < FA_CB; cl += 4) {
-    const int c = c0 + cl;
-    double a = 0, b = 0;
-    for (int k0 = lane; k0 < nchunks; k0 += 256) {
-      float2 pp[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + u * 64;
-        pp[u] = k < nchunks ? *reinterpret_cast<const float2*>(part + ((long long)k * C + c) * 2) : make_float2(0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a += pp[u].x;
-        b += pp[u].y;
-      }
-    }
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if (lane == 0) {
-      dbeta[c] = (float)a;
-      dgamma[c] = (float)b;
-      tdb[cl] = (float)a;
-      tdg[cl] = (float)b;
-    }
-  }
-  __syncthreads();
-  constexpr int G = FA_CB / N;
-  const int g = threadIdx.x % G, c = c0 + N * g;
-  const float invP = 1.f / (float)P;
-  float sc[N], sh[N], k0[N], k1[N], k2[N];
-  {
-    float mu[N], rs[N], gm[N];
-    ldc<N>(scale + c, sc); ldc<N>(shift + c, sh);
-    ldc<N>(mean + c, mu); ldc<N>(rstd + c, rs); ldc<N>(gamma + c, gm);
-#pragma unroll
-    for (int e = 0; e < N; ++e) {
-      const float dg = tdg[N * g + e], db = tdb[N * g + e];
-      k1[e] = gm[e] * rs[e];
-      k2[e] = k1[e] * rs[e] * dg * invP;
-      k0[e] = k1[e] * (db * invP - mu[e] * rs[e] * dg * invP);
-    }
-  }
-  for (long long pix = threadIdx.x / G; pix < P; pix += 256 / G) {
-    int b, yy, xx;
-    pix_bxy(pd, pix, b, yy, xx);
-    float v[N], g1[N], g2[N], d[N];
-    VW<T>::load(reinterpret_cast<const T*>(x.p) + vidx(x, b, yy, xx, c), v);
-    if (gi.has1) VW<T>::load(reinterpret_cast<const T*>(gi.g1.p) + vidx(gi.g1, b, yy, xx, c), g1);
-    if (gi.has2) VW<T>::load(reinterpret_cast<const T*>(gi.g2.p) + vidx(gi.g2, b, yy, xx, c), g2);
-#pragma unroll
-    for (int e = 0; e < N; ++e) {
-      const float n = fmaf(v[e], sc[e], sh[e]);
-      float dn = 0.f;
-      if (gi.has1) dn += g1[e] * dact(n, gi.s1);
-      if (gi.has2) dn += g2[e] * dact(n, gi.s2);
-      d[e] = fmaf(k1[e], dn, -fmaf(k2[e], v[e], k0[e]));
-    }
-    VW<T>::store(reinterpret_cast<T*>(dx.p) + vidx(dx, b, yy, xx, c), d);
-  }
-}
-
 // part[chunk][c] = sum over the chunk's pixels of x (conv bias gradients)
 template <typename T>
 __global__ void __launch_bounds__(256) chan_sum_kernel(View x, PixDiv pd, long long P, int C, float* part, int nchunks) {
@@ -1010,33 +852,6 @@ extern "C" int stc_bn_finalize(const float* part, int nchunks, int C, const floa
   return 0;
 }
 
-// finalize + apply in one launch (bn_finalize_apply_kernel): C a multiple of 16, <= 2048 pixels; returns 1 without
-// launching anything when the shape does not qualify (the caller then runs stc_bn_finalize + stc_bn_apply)
-extern "C" int stc_bn_finalize_apply(int dtype, int B, stc_view x, int C, const float* part, int nchunks,
-                                     const float* gamma, const float* beta, float* running_mean, float* running_var,
-                                     int64_t* num_batches_tracked, float momentum, float eps, float* mean, float* rstd,
-                                     float* scale, float* shift, stc_view y1, float slope1, stc_view y2, float slope2,
-                                     void* stream) {
-  const long long P = (long long)B * x.H * x.W;
-  if (part == nullptr || C % FA_CB != 0 || P > 2048 || !y1.p || !vec_ok(dtype, C, x) || !vec_ok(dtype, C, y1) ||
-      (y2.p && !vec_ok(dtype, C, y2)))
-    return 1;
-  STC_REQUIRE(scale && shift, "stc_bn_finalize_apply: table outputs required");
-  hipStream_t st = (hipStream_t)stream;
-  View v = mkview(x), o1 = mkview(y1), o2 = y2.p ? mkview(y2) : mkview(y1);
-  const PixDiv pd = mkpix(B, x.H, x.W);
-  const int h2 = y2.p != nullptr ? 1 : 0;
-#define STC_FA(T_)                                                                                                  \
-  hipLaunchKernelGGL((bn_finalize_apply_kernel<T_>), dim3(C / FA_CB), dim3(256), 0, st, part, nchunks, C, gamma, beta, \
-                     running_mean, running_var, (long long*)num_batches_tracked, momentum, eps, mean, rstd, scale,     \
-                     shift, v, pd, P, o1, slope1, o2, slope2, h2)
-  if (dtype == STC_F32) STC_FA(float);
-  else STC_FA(bf16);
-#undef STC_FA
-  STC_CHECK_LAUNCH();
-  return 0;
-}
-
 extern "C" int stc_bn_bwd_reduce(int dtype, int B, stc_view x, int C, const float* scale, const float* shift,
                                  const float* mean, const float* rstd, stc_view g1, float slope1, stc_view g2,
                                  float slope2, float* part2, int nchunks, void* stream) {
@@ -1067,19 +882,6 @@ extern "C" int stc_bn_bwd_apply(int dtype, int B, stc_view x, int C, const float
   GradIn gi = mkgrad(g1, slope1, g2, slope2);
   if (mean) {
     STC_REQUIRE(part2 && dgamma && dbeta && gamma && rstd && scale && shift, "stc_bn_bwd_apply: missing BN tensors");
-    const long long Ps = (long long)B * x.H * x.W;
-    if (Ps <= 2048 && C % FA_CB == 0) {  // the small levels: finalize + apply in one launch
-      View v = mkview(x), o = mkview(dx);
-      const PixDiv pd = mkpix(B, x.H, x.W);
-      if (dtype == STC_F32)
-        hipLaunchKernelGGL(bn_bwd_finalize_apply_kernel<float>, dim3(C / FA_CB), dim3(256), 0, st, v, pd, Ps, C, scale,
-                           shift, mean, rstd, gamma, gi, part2, nchunks, dgamma, dbeta, o);
-      else
-        hipLaunchKernelGGL(bn_bwd_finalize_apply_kernel<bf16>, dim3(C / FA_CB), dim3(256), 0, st, v, pd, Ps, C, scale,
-                           shift, mean, rstd, gamma, gi, part2, nchunks, dgamma, dbeta, o);
-      STC_CHECK_LAUNCH();
-      return 0;
-    }
     if (nchunks <= 256)
       hipLaunchKernelGGL(bn_bwd_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part2, nchunks, C, dgamma, dbeta);
     else

@@ -71,8 +71,6 @@ _SIGS = {
     "stc_chan_sum": (_i32, [_i32, _i32, View, _i32, _i32, _vp, _i32, _vp, _vp]),
     "stc_bn_apply": (_i32, [_i32, _i32, View, _i32, _vp, _vp, View, _f32, View, _f32, _vp]),
     "stc_bn_finalize": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp, _vp]),
-    "stc_bn_finalize_apply": (_i32, [_i32, _i32, View, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp,
-                                     _vp, _vp, View, _f32, View, _f32, _vp]),
     "stc_bn_bwd_reduce": (_i32, [_i32, _i32, View, _i32, _vp, _vp, _vp, _vp, View, _f32, View, _f32, _vp, _i32,
                                  _vp]),
     "stc_bn_bwd_apply": (_i32, [_i32, _i32, View, _i32, _vp, _vp, _vp, _vp, _vp, View, _f32, View, _f32, _vp, _i32,

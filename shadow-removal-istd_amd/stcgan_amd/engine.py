@@ -52,8 +52,6 @@ def _trace_new(kind):
 # gradient and saved input; nothing on the chain needs them), so they run on a side stream per calling
 # stream and overlap the rest of the chain -- most of the deep (1x1-8x8) layers' kernels are latency-bound
 # small grids.  Joined before the backward returns its gradients.
-# BatchNorm finalize + apply in one launch on the small generator levels (stc_bn_finalize_apply); False: the two calls
-FUSE_BN_APPLY = True
 WGRAD_OVERLAP = True
 # interleaved A/B (scripts/train_steps.py --ab): none 13.74, <= 32x32 13.45, <= 64x64 13.64, all 13.75 ms/step
 WGRAD_OVERLAP_MAX_PIX = 32 * 32
@@ -221,26 +219,17 @@ def _pad2(S, k):
     return (2 * S[k + 1][0], 2 * S[k + 1][1])
 
 
-def _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev, apply=None):
+def _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev):
     """Conv whose output feeds a BatchNorm2d: returns ((2, cout) scale/shift table, (mean, rstd) or None).
-    Train mode: the batch statistics come out of the conv itself (stc_conv_fwd_ex).  apply = (view of the BN
-    domain, y1, s1, y2, s2): also materialise the activations (stc_bn_apply) -- on the small levels fused with the
-    finalize into one launch (stc_bn_finalize_apply)."""
+    Train mode: the batch statistics come out of the conv itself (stc_conv_fwd_ex)."""
     t = torch.empty((2, cout), dtype=torch.float32, device=dev)
     if train:
         part, nch = ops.conv_stats(kind, B, xv, cin, w, cout, yv, dt)
-        st = None
-        if apply is not None and FUSE_BN_APPLY:
-            st = ops.bn_finalize_apply(B, apply[0], cout, dt, part, nch, bn, t[0], t[1], *apply[1:])
-            if st is not None:
-                return t, st
         st = ops.bn_finalize_part(part, nch, cout, bn, t[0], t[1])
     else:
         ops.conv(kind, B, xv, cin, w, cout, yv, dt)
         ops.bn_eval_table(cout, bn, t[0], t[1])
         st = None
-    if apply is not None:
-        ops.bn_apply(B, apply[0], cout, dt, (t[0], t[1]), *apply[1:])
     return t, st
 
 
@@ -268,9 +257,9 @@ def gen_forward(plan, sources, train, dt, cache, save):
     rq = [None] + [_nhwc(B, *_pad2(S, k), co[k - 1], dt, dev) for k in range(1, Lv)]
     tab_d, tab_u, st_d, st_u = {}, {}, {}, {}
 
-    def conv_bn(kind, xv, cin_, w, cout, yv, bn, apply=None):
-        """conv -> BatchNorm table (batch statistics fused into the conv in train mode) [-> activations]."""
-        return _conv_bn(kind, B, xv, cin_, w, cout, yv, dt, bn, train, dev, apply)
+    def conv_bn(kind, xv, cin_, w, cout, yv, bn):
+        """conv -> BatchNorm table (batch statistics fused into the conv in train mode)."""
+        return _conv_bn(kind, B, xv, cin_, w, cout, yv, dt, bn, train, dev)
 
     # ---- down path
     w0 = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_FWD, co[0], cin_pad, dt)
@@ -287,8 +276,9 @@ def gen_forward(plan, sources, train, dt, cache, save):
         wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
         if k <= Lv - 2:
             tab_d[k], st_d[k] = conv_bn(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k],
-                                        L.nhwc_view(rd[k]), plan.bnd[k],
-                                        (L.nhwc_view(rd[k]), L.nhwc_view(ad[k]), LRELU, L.nhwc_view(cr[k], 0), 0.0))
+                                        L.nhwc_view(rd[k]), plan.bnd[k])
+            ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]),
+                         LRELU, L.nhwc_view(cr[k], 0), 0.0)
         else:  # innermost: no down-norm (STCGAN/networks.py:118-124)
             ops.conv(L.CONV_S2, B, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]), dt)
             ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, None, L.nhwc_view(cr[k]), 0.0)
@@ -296,14 +286,10 @@ def gen_forward(plan, sources, train, dt, cache, save):
     for k in range(Lv - 1, 0, -1):
         wt = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_FWD, co[k - 1], cin_t(k), dt)
         # statistics over the full ConvT extent (before the crop of an odd level)
-        # (the apply covers the cropped extent S[k]; the statistics the full one -- no fused form then)
-        crop = tuple(S[k]) != tuple(_pad2(S, k))
         tab_u[k], st_u[k] = conv_bn(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
-                                    plan.bnu[k], None if crop else
-                                    (L.nhwc_view(rq[k]), L.nhwc_view(cr[k - 1], co[k - 1]), 0.0, None, 1.0))
-        if crop:
-            ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
-                         L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
+                                    plan.bnu[k])
+        ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
+                     L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
     # ---- outermost: tanh(convT_0(cr[0]) + bias) -> NCHW fp32
     Ho, Wo = 2 * S[1][0], 2 * S[1][1]
     y = torch.empty((B, plan.out_c, Ho, Wo), dtype=torch.float32, device=dev)

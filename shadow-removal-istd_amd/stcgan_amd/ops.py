@@ -311,23 +311,6 @@ def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True
     return mean, rstd
 
 
-def bn_finalize_apply(B, xv, C, dt, part, nch, bn, scale_out, shift_out, y1, s1, y2=None, s2=1.0):
-    """bn_finalize_part + bn_apply(table) in one launch for the small levels (stc_bn_finalize_apply): returns
-    (mean, rstd), or None when the shape does not qualify (nothing launched: make the two calls)."""
-    dev = scale_out.device
-    mean = torch.empty(C, dtype=torch.float32, device=dev)
-    rstd = torch.empty(C, dtype=torch.float32, device=dev)
-    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
-    rc = lib().stc_bn_finalize_apply(L.dtype_code(dt), B, xv, C, ptr(part), nch, ptr(bn.weight), ptr(bn.bias),
-                                     ptr(bn.running_mean), ptr(bn.running_var), ptr(bn.num_batches_tracked), float(mom),
-                                     float(bn.eps), ptr(mean), ptr(rstd), ptr(scale_out), ptr(shift_out), y1, float(s1),
-                                     y2 if y2 is not None else L.NULL_VIEW, float(s2), stream())
-    if rc == 1:
-        return None
-    check(rc, "stc_bn_finalize_apply")
-    return mean, rstd
-
-
 # bf16 weight-gradient tile configurations (csrc/wgrad_bf16.hip kWbCfg): cfg -> (BM, BN, WM, WN, swapped)
 _WB_TILES = [(128, 128, 2, 2, "false"), (64, 128, 1, 4, "false"), (128, 16, 4, 1, "true"), (256, 256, 2, 4, "false"),
              (256, 128, 4, 2, "false"), (128, 256, 2, 4, "false"), (128, 128, 2, 2, "false", 4, 4),

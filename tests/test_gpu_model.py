@@ -215,34 +215,3 @@ def test_bf16_train_step_runs_and_tracks_fp32():
     for k in ["G", "D", "data1", "data2"]:
         a, b = res["fp32"][k], res["bf16"][k]
         assert abs(a - b) <= 2e-2 * abs(a) + 1e-4, (k, a, b)
-
-
-@pytest.mark.parametrize("dtype,size", [("bf16", 256), ("fp32", 256), ("bf16", 96)])
-def test_fused_bn_finalize_apply_bit_identical(dtype, size):
-    """The small generator levels' BatchNorm finalize + apply in one launch (engine.FUSE_BN_APPLY,
-    stc_bn_finalize_apply) against the two calls: identical outputs, gradients and running statistics (the same
-    merge order and arithmetic; 96x96 also takes the odd-level crop path)."""
-    from stcgan_amd import engine
-    x = uniform((4, 3, size, size), 501).to(DEV)
-    res = []
-    for fuse in (True, False):
-        engine.FUSE_BN_APPLY = fuse
-        try:
-            net, _ = make_net("G1", 64, dtype=dtype)
-            net.train()
-            xi = x.clone().requires_grad_(True)
-            y = net(xi)
-            y.backward(torch.ones_like(y))
-            torch.cuda.synchronize()
-            res.append((y.detach().cpu(), xi.grad.cpu(),
-                        {k: v.detach().cpu().clone() for k, v in net.state_dict().items()},
-                        [p.grad.detach().cpu().clone() for p in net.parameters()]))
-        finally:
-            engine.FUSE_BN_APPLY = True
-    (y0, gx0, sd0, g0), (y1, gx1, sd1, g1) = res
-    assert torch.equal(y0, y1)
-    assert torch.equal(gx0, gx1)
-    for k in sd0:
-        assert torch.equal(sd0[k], sd1[k]), k
-    for a, b in zip(g0, g1):
-        assert torch.equal(a, b)
