@@ -84,6 +84,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   static_assert(GW % 16 == 0 && BM % GW == 0 && TM % GW == 0 && FN == 4 && FM % 2 == 0 && BG >= 1,
                 "whole output rows per tile and per wave, 16-row fragments inside an output row");
   static_assert(S1 ? AG % 2 == 0 : NP >= NG, "every MFMA group issues a piece (S1: whole halves of a stage)");
+  static_assert(BM * (BN * 2 + 16) + WM * BN * 16 <= G::LDS, "epilogue tile + statistics merge area");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -558,9 +558,9 @@ constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 static size_t bf16_lds_bytes(int cfg) {
   const TileCfg& t = kTiles[cfg];
   size_t stage = (size_t)t.NST * (t.BM + t.BN) * t.BK * 2;
-  size_t epi = (size_t)t.BM * (t.BN * 2 + 16);
-  size_t red = (size_t)t.WM * t.BN * 3 * 4;
-  return std::max(stage, std::max(epi, red));
+  // the epilogue's bf16 tile and, past it, the BatchNorm statistics' [WM][BN][4] merge area (igemm_epilogue)
+  size_t epi = (size_t)t.BM * (t.BN * 2 + 16) + (size_t)t.WM * t.BN * 16;
+  return std::max(stage, epi);
 }
 
 // Tile / split-K choice (fitted to the sweep of scripts/tune_bf16.py over one train step, see

@@ -198,12 +198,13 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
   }
 
   __syncthreads();  // every wave is done with the stage buffers
-  if (p.stats) {
-    // BatchNorm batch statistics of the tile, one shifted pass per wave over its accumulators
-    // (shift = the column's value in the wave's first row: S1 = sum(x - shift), S2 = sum((x - shift)^2)),
-    // then the WM row-waves merged through LDS into the tile's {count, 0, M2, mean} (Chan).
+  // BatchNorm batch statistics of the tile, one shifted pass per wave over its accumulators (shift = the column's
+  // value in the wave's first row: S1 = sum(x - shift), S2 = sum((x - shift)^2)), then the WM row-waves merged
+  // through LDS (at redp) into the tile's {count, 0, M2, mean} (Chan).  With 16-byte stores it runs after they are
+  // issued (its LDS area past the staged tile), so the arithmetic and its barriers overlap the stores' drain.
+  auto tile_stats = [&](char* redp) {
     int rows_w = min(TM, max(0, p.M - (m0 + wm * TM)));
-    float* red = reinterpret_cast<float*>(smem);  // [WM][BN][4] {S1, S2, shift, rows}
+    float* red = reinterpret_cast<float*>(redp);  // [WM][BN][4] {S1, S2, shift, rows}
     float sh[FN], s1[FN], s2[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -269,7 +270,8 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
         q[0] = s1[j]; q[1] = s2[j]; q[2] = sh[j]; q[3] = (float)rows_w;
       }
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (LDS only: the stores stay in flight)
+    __builtin_amdgcn_s_barrier();
     const long long tile = (long long)ph * p.mtiles + mt;
     for (int c = tid; c < BN; c += 64 * NW) {
       const int n = n0 + c;
@@ -288,9 +290,10 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
       }
       *reinterpret_cast<float4*>(p.stats + (tile * p.N + n) * 4) = make_float4(cnt, 0.f, m2, mean);
     }
-    __syncthreads();
-  }
-
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (LDS only: the stores stay in flight)
+    __builtin_amdgcn_s_barrier();
+  };
+  if (p.stats && !p.vec_out) tile_stats(smem);
   if (p.vec_out) {
     // bf16 tile through LDS: [BM][BN] with a 16-byte row pad, then 16-byte row stores
     constexpr int PITCH = BN * 2 + 16;
@@ -387,6 +390,7 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
           if (++y == p.GH) { y = 0; ++b; }
         }
       }
+      if (p.stats) tile_stats(smem + BM * PITCH);
       return;
     }
     // fused BatchNorm-backward reduction: {sum dn, sum dn*xhat} of this thread's 8-channel chunk
