@@ -3,6 +3,10 @@
 #pragma once
 #include "common.hpp"
 
+#ifndef STC_BNB_G  // rows per group of in-flight BN-input loads in the fused BN-backward epilogue (tuning builds)
+#define STC_BNB_G 4
+#endif
+
 namespace stc {
 
 struct GParams {
@@ -306,7 +310,7 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
     // fused BatchNorm backward: the BN-input / second-gradient rows of a group of G output rows (addresses
     // independent of the GEMM result); the first group is issued before the tile staging below, so its
     // memory latency overlaps the accumulator shuffle and the barrier
-    constexpr int G = ITER < 4 ? ITER : 4;
+    constexpr int G = ITER < STC_BNB_G ? ITER : STC_BNB_G;
     static_assert(ITER % G == 0, "whole groups");
     const int nch = n - p.bch_off;  // BN channel of this thread's chunk
     const bool bnb_on = nch >= 0 && nch < p.bC;
