@@ -644,6 +644,70 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) n
   }
 }
 
+// ---- the PatchGAN logits layer (Conv2d k4 s1 p1, CIN -> 1; STCGAN/networks.py:183-184) in two passes: the 16 tap
+// products of every input pixel, Y[q][tap] = sum_c x[q][c] w[tap][c] (an M = pixels, N = 16 taps, K = CIN GEMM on
+// v_mfma_f32_16x16x32_bf16 with the A fragments loaded straight from HBM -- each input byte read once, no halo), then
+// out[y][x] = bias + sum_taps Y[(y + ky - 1, x + kx - 1)][tap] (fixed tap order; out-of-image pixels contribute 0).
+// The tiled kernel re-read the 4x16 tiles' halo (1.7x) and split the 8192-deep reduction over blocks.
+template <int CIN>
+__global__ void __launch_bounds__(256) logits_taps_kernel(const HParams p, float* __restrict__ Y) {
+  constexpr int KS = CIN / 32;
+  const int lane = threadIdx.x & 63;
+  const long long Q = (long long)p.Mtot;                     // input pixels (B * IH * IW)
+  const long long q0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  if (q0 >= Q) return;
+  const int rl = lane & 15, kq = lane >> 4;
+  // B: tap rl, channels 32 k + 8 kq .. + 7
+  bf16x8_h bw[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) bw[k] = *reinterpret_cast<const bf16x8_h*>(p.w + rl * CIN + 32 * k + 8 * kq);
+  // A: pixel q0 + rl (clamped past the end), the same channels
+  const long long q = min(q0 + rl, Q - 1);
+  const int ihw = p.IH * p.IW;
+  const int b = (int)(q / ihw), rem = (int)(q - (long long)b * ihw), iy = rem / p.IW, ix = rem - iy * p.IW;
+  const bf16* xp = reinterpret_cast<const bf16*>(p.a) + (long long)b * p.a_bs + (long long)iy * p.a_rs +
+                   (long long)ix * p.a_ps + p.a_co + 8 * kq;
+  bf16x8_h av[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) av[k] = *reinterpret_cast<const bf16x8_h*>(xp + 32 * k);
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < KS; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[k], bw[k], acc, 0, 0, 0);
+  // acc[e] = Y[q0 + 4 kq + e][tap rl]
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long long qq = q0 + 4 * kq + e;
+    if (qq < Q) Y[qq * 16 + rl] = acc[e];
+  }
+}
+
+// 4 lanes per output pixel (one kernel row each: its 4 taps' loads in flight together), summed in a fixed order
+__global__ void __launch_bounds__(256) logits_gather_kernel(const HParams p, const float* __restrict__ Y) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long idx = t >> 2;
+  const int ky = (int)(t & 3);
+  const long long total = (long long)(p.Mtot / ((long long)p.IH * p.IW)) * p.GH * p.GW;
+  const long long ic = idx < total ? idx : total - 1;
+  const int ghw = p.GH * p.GW;
+  const int b = (int)(ic / ghw), rem = (int)(ic - (long long)b * ghw), gy = rem / p.GW, gx = rem - gy * p.GW;
+  const float* yb = Y + (long long)b * p.IH * p.IW * 16;
+  const int iy = gy + ky - 1;
+  float tv[4];
+#pragma unroll
+  for (int kx = 0; kx < 4; ++kx) {
+    const int ix = gx + kx - 1;
+    const bool ok = (unsigned)iy < (unsigned)p.IH && (unsigned)ix < (unsigned)p.IW;
+    tv[kx] = ok ? yb[((long long)iy * p.IW + ix) * 16 + ky * 4 + kx] : 0.f;
+  }
+  float v = (tv[0] + tv[1]) + (tv[2] + tv[3]);
+  v += __shfl_xor(v, 1, 64);  // (rows 0 + 1, 2 + 3), then the two pairs: the same order on every lane
+  v += __shfl_xor(v, 2, 64);
+  if (ky != 0 || idx >= total) return;
+  if (p.bias) v += p.bias[0];
+  if (p.tanh_) v = tanhf(v);
+  store_out(p, (long long)b * p.c_bs + (long long)gy * p.c_rs + (long long)gx * p.c_ps + (long long)p.c_co * p.c_cs, v);
+}
+
 // split-K combine: out = epi(sum_s ws[s][m][n'])
 template <int GEOM>
 __global__ void narrow_reduce_kernel(const HParams p, int B) {
@@ -699,6 +763,9 @@ static int stream_ns(int cin, const int32_t* force) {
   if (force && (force[1] & 32) && force[0] > 0) return force[0];
   return cin == 128 ? 3 : 4;
 }
+
+// the two-pass logits form: conv s1 with one output channel and 512 / 256 input channels
+static bool logits_ok(int geom, int cin, int cout) { return geom == 1 && cout == 1 && (cin == 512 || cin == 256); }
 
 static size_t stream_lds(int cin, int ns) {
   const int pieces = ((NS_TW + 2) * cin * 2 + 1023) / 1024;
@@ -771,7 +838,8 @@ int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout
   int ty, txb, ns, kern;
   const int np = geom == 0 ? 4 * Cout : Cout;
   narrow_plan(geom, B, GH, GW, Cin, np, nullptr, &ty, &txb, &ns, &kern, false);  // (a forced tiled plan's slab)
-  return (ns <= 1 ? 0 : (int64_t)ns * B * GH * GW * np * 4) + narrow_frag_bytes(geom, Cin, Cout);
+  const int64_t taps = logits_ok(geom, Cin, Cout) ? (int64_t)B * (GH + 1) * (GW + 1) * 16 * 4 : 0;  // (conv s1: IH = GH+1)
+  return std::max<int64_t>((ns <= 1 ? 0 : (int64_t)ns * B * GH * GW * np * 4) + narrow_frag_bytes(geom, Cin, Cout), taps);
 }
 
 int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
@@ -802,6 +870,23 @@ int bf16_narrow_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, 
   const int nchunks = Cin / 64;
   p.chunks_per_split = cdiv(nchunks, ns);
   p.nsplit = cdiv(nchunks, p.chunks_per_split);
+  if (logits_ok(geom, Cin, Cout) && !(force && (force[0] > 0 || force[1] != 0))) {
+    STC_REQUIRE(x.H == p.GH + 1 && x.W == p.GW + 1, "narrow bf16: logits geometry (%dx%d -> %dx%d)", x.H, x.W, p.GH, p.GW);
+    const int64_t need = (int64_t)B * x.H * x.W * 16 * 4;
+    STC_REQUIRE(ws && ws_bytes >= need, "narrow bf16: workspace %lld < %lld", (long long)ws_bytes, (long long)need);
+    p.Mtot = (long long)B * x.H * x.W;  // (here: input pixels)
+    if (p.Mtot == 0 || (long long)B * p.GH * p.GW == 0) return 0;
+    float* Y = (float*)ws;
+    const unsigned g1 = (unsigned)((p.Mtot + 63) / 64), g2 = (unsigned)((4LL * B * p.GH * p.GW + 255) / 256);
+    main_timer_begin(st);
+    if (Cin == 512) hipLaunchKernelGGL(logits_taps_kernel<512>, dim3(g1), dim3(256), 0, st, p, Y);
+    else hipLaunchKernelGGL(logits_taps_kernel<256>, dim3(g1), dim3(256), 0, st, p, Y);
+    main_timer_end(st);
+    STC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(logits_gather_kernel, dim3(g2), dim3(256), 0, st, p, (const float*)Y);
+    STC_CHECK_LAUNCH();
+    return 0;
+  }
   const int64_t slab_bytes = p.nsplit > 1 ? (int64_t)p.nsplit * B * p.GH * p.GW * p.NP * 4 : 0;
   const int64_t frag_bytes = narrow_frag_bytes(geom, Cin, Cout);
   STC_REQUIRE(ws && ws_bytes >= slab_bytes + frag_bytes, "narrow bf16: workspace %lld < %lld", (long long)ws_bytes,

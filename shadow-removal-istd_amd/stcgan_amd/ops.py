@@ -228,6 +228,8 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
             if geom == 0 and gh % 16 == 0 and gw % 64 == 0 and ((cin == 128 and npc <= 16) or
                                                                (cin == 64 and 16 < npc <= 32)):
                 return f"narrow_stream_kernel<{cin}, {nb}, {3 if cin == 128 else 4}>", True
+            if geom == 1 and cout == 1 and cin in (256, 512):  # the two-pass logits form (taps GEMM + gather)
+                return f"logits_taps_kernel<{cin}>", False
             return f"narrow_wk_kernel<{geom}, {nb}, 4, 1>", ws == 0
         return "narrow_tiled_kernel", True
     if cfg == HALO_CFG:  # the LDS-resident input halo kernels (csrc/halo_bf16.hip): template as rocprof names it

@@ -143,7 +143,9 @@ NARROW = [  # kind, B, Cin, N, grid H, grid W
     ("convT", 2, 128, 1, 16, 16),
     ("convT", 1, 64, 8, 9, 13),      # first-layer input gradient (N = 8 padded channels), ragged tiles
     ("convT", 3, 64, 4, 33, 17),
-    ("conv_s1", 2, 512, 1, 30, 30),  # PatchGAN logits 31x31 -> 30x30 (split over channel chunks)
+    ("conv_s1", 2, 512, 1, 30, 30),  # PatchGAN logits 31x31 -> 30x30 (the two-pass taps GEMM + gather)
+    ("conv_s1", 32, 512, 1, 30, 30),  # ... at the train step's batch
+    ("conv_s1", 3, 256, 1, 7, 9),    # ... with 256 channels, ragged
     ("conv_s1", 1, 128, 2, 11, 9),
 ]
 
