@@ -22,11 +22,17 @@
 
 namespace stc {
 
-constexpr int STEM_RB = 8;   // output rows per block
+// output rows per block: 8 for the activation modes, 16 for the BN-backward modes (scripts/ab_stem.py, bs = 32,
+// profiles/r04/stem/strip_*.log: activation 25.8 / 29.9 us at 8 against 26.2 / 30.9 at 4 and 31.9 / 33.7 at 16; the
+// output layer's input gradient + BN apply 113.1 us at 16 against 118.3 at 8, the logits layer's 45.8 against 51.7)
+constexpr int STEM_RB = 8;
+constexpr int STEM_RB_BNB = 16;
+constexpr int S1D_RB = 16;
 constexpr int STEM_NS = 8;   // input-row slots in the LDS ring
 
 template <int WIN, int N, int MODE>
 __global__ void __launch_bounds__(256) stem_conv_kernel(const GParams p) {
+  constexpr int RB = MODE == 3 ? STEM_RB_BNB : STEM_RB;
   constexpr int WOUT = WIN / 2;
   constexpr int ROWB = WIN * 16;              // bytes of one input row (8 bf16 channels per pixel)
   constexpr int PPW = WIN / 256;              // 1 KiB DMA pieces per wave per input row
@@ -44,8 +50,8 @@ __global__ void __launch_bounds__(256) stem_conv_kernel(const GParams p) {
   char* ring = smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* stg = smem + STEM_NS * ROWB + wave * 16 * PITCH;
-  const int strips = p.GH / STEM_RB;
-  const int img = blockIdx.x / strips, oy0 = (blockIdx.x - img * strips) * STEM_RB;
+  const int strips = p.GH / RB;
+  const int img = blockIdx.x / strips, oy0 = (blockIdx.x - img * strips) * RB;
   const int rl = lane & 15, kq = lane >> 4;
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, (short)0, (int)p.a_bytes, 0x00020000);
@@ -93,18 +99,18 @@ __global__ void __launch_bounds__(256) stem_conv_kernel(const GParams p) {
   // prologue: the 4 rows of output row 0 and the 2 new rows of output rows 1 and 2
 #pragma unroll
   for (int r = 0; r < 8; ++r) load_row(r);
-  for (int t = 0; t < STEM_RB; ++t) {
+  for (int t = 0; t < RB; ++t) {
     // rows 2t .. 2t+3 must have landed; younger: this wave's other VMEM ops (stores, BN loads) of output rows t-2 and
     // t-1 and the loads of rows 2t+4 .. 2t+7 issued between them (t = 0: the loads of rows 4..7; t = 1: rows 6, 7
     // before the ops of row 0)
     if (t == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PPW) : "memory");
     else if (t == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + OPW) : "memory");
-    else if (t + 1 < STEM_RB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + 2 * OPW) : "memory");
+    else if (t + 1 < RB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW + 2 * OPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPW) : "memory");
     __builtin_amdgcn_s_barrier();
     // refill rows 2t + 6, 2t + 7 into the slots of rows 2t - 2, 2t - 1, last read by output row t - 1, which every
     // wave finished before this barrier (the slots of rows 2t .. 2t + 3 are this row's)
-    if (t >= 1 && 2 * t + 7 < 2 * STEM_RB + 2) {
+    if (t >= 1 && 2 * t + 7 < 2 * RB + 2) {
       load_row(2 * t + 6);
       load_row(2 * t + 7);
     }
@@ -225,17 +231,17 @@ constexpr int S1D_W = 31, S1D_PAD = 32;
 __global__ void __launch_bounds__(256) stem_s1d_kernel(const GParams p) {
   constexpr int NF = 8, CPX = 16, PXS = 4, NPASS = 4;  // 128 channels: 16-byte chunks per pixel, store passes
   constexpr int PITCH = 128 * 2 + 16;
-  constexpr int NRW = STEM_RB + 3;                     // staged dy rows
+  constexpr int NRW = S1D_RB + 3;                     // staged dy rows
   __shared__ __attribute__((aligned(16))) char dys[NRW * S1D_PAD * 16];
   __shared__ __attribute__((aligned(16))) char stgs[4 * 16 * PITCH];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* stg = stgs + wave * 16 * PITCH;
-  const int nslices = p.N / 128, strips = (p.GH + STEM_RB - 1) / STEM_RB;
+  const int nslices = p.N / 128, strips = (p.GH + S1D_RB - 1) / S1D_RB;
   int bid = blockIdx.x;
   const int ns = bid % nslices;
   bid /= nslices;
   const int strip = bid % strips, img = bid / strips;
-  const int y0 = strip * STEM_RB, n0 = ns * 128;
+  const int y0 = strip * S1D_RB, n0 = ns * 128;
   const int rl = lane & 15, kq = lane >> 4;
   // dy rows y0 - 2 .. y0 + 8 (local r), columns 0 .. 31 (>= IW: zero)
   for (int i = tid; i < NRW * S1D_PAD; i += 256) {
@@ -266,7 +272,7 @@ __global__ void __launch_bounds__(256) stem_s1d_kernel(const GParams p) {
   const bf16x8_t zero8 = {};
   __syncthreads();
   // task k of this wave: output row y0 + (k >> 1) within the image, pixels 16 (k & 1) .. + 15
-  const int ntask = 2 * min(STEM_RB, p.GH - y0);
+  const int ntask = 2 * min(S1D_RB, p.GH - y0);
   auto bn_load = [&](int k, uint4 (&v)[NPASS]) {
     const int y = y0 + (k >> 1);
 #pragma unroll
@@ -358,7 +364,7 @@ __global__ void __launch_bounds__(256) stem_s1d_kernel(const GParams p) {
 // outputs with the fused BN-backward sums (input width 256).
 static bool stem_sizes(int kind, int Cin, int Cout, int Hg, int Wg, bool bnb) {
   return kind == STC_CONV_S2 && Cin == 8 && Cout == (bnb ? 128 : 64) && (Wg == 128 || (Wg == 256 && !bnb)) &&
-         Hg % STEM_RB == 0;
+         Hg % (bnb ? STEM_RB_BNB : STEM_RB) == 0;
 }
 
 bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y, bool bnb) {
@@ -374,8 +380,8 @@ static bool s1d_sizes(int kind, int Cin, int Cout, int Hg, int Wg) {
 
 // BN-backward partial count of the fused input gradient when it takes one of these kernels (0: it does not)
 int stem_bnb_chunks(int kind, int B, int Hg, int Wg, int Cin, int Cout) {
-  if (s1d_sizes(kind, Cin, Cout, Hg, Wg)) return B * ((Hg + STEM_RB - 1) / STEM_RB);
-  return stem_sizes(kind, Cin, Cout, Hg, Wg, true) ? B * (Hg / STEM_RB) : 0;
+  if (s1d_sizes(kind, Cin, Cout, Hg, Wg)) return B * ((Hg + S1D_RB - 1) / S1D_RB);
+  return stem_sizes(kind, Cin, Cout, Hg, Wg, true) ? B * (Hg / STEM_RB_BNB) : 0;
 }
 
 bool stem_s1d_eligible(int kind, int B, const stc_view& dy, int Cin, int Cout, const stc_view& y) {
@@ -385,7 +391,7 @@ bool stem_s1d_eligible(int kind, int B, const stc_view& dy, int Cin, int Cout, c
 
 int stem_s1d_launch(GParams& p, hipStream_t st) {
   const int B = p.M / (p.GH * p.GW);
-  const dim3 grid((unsigned)(B * ((p.GH + STEM_RB - 1) / STEM_RB) * (p.N / 128)));
+  const dim3 grid((unsigned)(B * ((p.GH + S1D_RB - 1) / S1D_RB) * (p.N / 128)));
   main_timer_begin(st);
   hipLaunchKernelGGL(stem_s1d_kernel, grid, dim3(256), 0, st, p);
   main_timer_end(st);
@@ -395,8 +401,8 @@ int stem_s1d_launch(GParams& p, hipStream_t st) {
 
 int stem_launch(GParams& p, hipStream_t st) {
   const int B = p.M / (p.GH * p.GW);
-  const dim3 grid((unsigned)(B * (p.GH / STEM_RB)));
   const bool bnb = p.part2 != nullptr;
+  const dim3 grid((unsigned)(B * (p.GH / (bnb ? STEM_RB_BNB : STEM_RB))));
   const int n = bnb ? 128 : 64;
   const size_t lds = std::max((size_t)STEM_NS * p.IW * 16 + 4 * 16 * (n * 2 + 16), (size_t)256 * 16 * 4);
   main_timer_begin(st);
