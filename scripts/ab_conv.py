@@ -1,5 +1,6 @@
 """A/B timer of the conv-s2 GEMMs of one train step (bs 32, 256x256, bf16): the automatic plan (the halo kernel,
-csrc/halo_bf16.hip, where it applies) against the automatic im2col plan (force {-2, 0}), interleaved rounds in
+csrc/halo_bf16.hip, where it applies) against the automatic im2col plan (force {-2, 0}) and the 8-wave 256 x 128
+halo block (force {HALO_CFG, 1}), interleaved rounds in
 one process, HIP events over 20 launches each; prints us / TFLOP/s per shape and the relative output difference."""
 import os
 import sys
@@ -16,6 +17,7 @@ BF = torch.bfloat16
 SHAPES = [  # (kind, GEMM grid, cin, cout, what)
     (L.CONV_S2, 64, 64, 128, "e2 / D c2 fwd"),
     (L.CONV_S2, 32, 128, 256, "e3 / D c3 fwd"),
+    (L.CONV_S2, 16, 256, 512, "e4 fwd (256 x 64 halo tile)"),
     (L.CONV_S2, 64, 64, 256, "d2 dgrad (ConvT 256->64)"),
     (L.CONV_S2, 32, 128, 512, "d3 dgrad (ConvT 512->128)"),
     (L.CONV_S2, 16, 256, 1024, "d4 dgrad (ConvT 1024->256)"),
@@ -49,10 +51,11 @@ def main():
             w = torch.randn((cout, cin, 4, 4), generator=g, device=dev) * 0.05
             wp = ops.pack(L.PACK_CONV_FWD, w, cout, cin, BF)
         ys = {}
-        times = {"halo": [], "im2col": []}
+        cands = (("halo", None), ("im2col", (-2, 0)), ("halo8w", (ops.HALO_CFG, 1)), ("n64w8", (ops.HALO_CFG, 4)))
+        times = {c[0]: [] for c in cands}
         plans = {}
         for rnd in range(5):
-            for name, force in (("halo", None), ("im2col", (-2, 0))):
+            for name, force in cands:
                 y = torch.empty((B, oh, oh, cout), device=dev, dtype=BF)
                 plans[name] = ops.conv_query(kind, B, gh, gh, cin, cout, BF, force=force)[2]
                 ops.conv_stats(kind, B, L.nhwc_view(x), cin, wp, cout, L.nhwc_view(y), BF, force=force)
@@ -68,7 +71,7 @@ def main():
         fl = 2.0 * B * gh * gh * cout * 16 * cin
         d = float((ys["halo"].float() - ys["im2col"].float()).abs().max() / ys["im2col"].float().abs().max())
         line = f"{what:28s} grid{gh} cin{cin} cout{cout}:"
-        for name in ("halo", "im2col"):
+        for name, _ in cands:
             t = sorted(times[name])
             line += f"  {name} plan{list(plans[name])} med {t[2]:.1f} us min {t[0]:.1f} ({fl / t[0] / 1e6:.0f} TF)"
         print(line + f"  rel diff {d:.2e}", flush=True)

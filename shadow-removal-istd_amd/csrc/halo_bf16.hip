@@ -362,9 +362,21 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
 // chunks, 16-byte NHWC bf16 views (no split K).  N tile: 128 output channels, 64 for a ConvT with N <= 64.
 // Conv2d k4 s1 p1 (kinds STC_CONV_S1 / STC_CONV_S1_DGRAD): a 32-wide GEMM grid only (the PatchGAN's 32 x 32 input
 // at 256 x 256); the forward's GEMM grid is its input grid (output + 1 row and column).
-static int halo_bn(int kind, int Cout) { return kind == STC_CONVT_S2 && Cout <= 64 ? 64 : HB_BN; }
+// N tile: 64 channels for a ConvT with N <= 64, and for a conv-s2 grid whose 128-channel tiles leave the chip
+// below 256 blocks while 64-channel ones fill it (the 16 x 16 level at bs 32: 128 -> 256 blocks of the 4-wave
+// 256 x 64 block); force shape 3 takes the 64-channel tile for any conv-s2 layer (tests / A/B).
+static int halo_bn(int kind, long long mtiles, int Cout, int shape) {
+  if (kind == STC_CONVT_S2) return Cout <= 64 ? 64 : HB_BN;
+  if (kind != STC_CONV_S2 || shape == 1 || shape == 2) return HB_BN;
+  if (shape == 3 || shape == 4) return 64;
+  return mtiles * ((Cout + HB_BN - 1) / HB_BN) < 256 && mtiles * ((Cout + 63) / 64) >= 256 ? 64 : HB_BN;
+}
 static void halo_grid(int kind, int& GH, int& GW) {
   if (kind == STC_CONV_S1) { ++GH; ++GW; }
+}
+int halo_plan_bn(int kind, int B, int GH, int GW, int Cout, int shape) {
+  halo_grid(kind, GH, GW);
+  return halo_bn(kind, (long long)B * GH * GW / HB_BM, Cout, shape);
 }
 
 bool halo_geometry_ok(int kind, int B, int GH, int GW, int Cin, int Cout) {
@@ -377,9 +389,10 @@ bool halo_geometry_ok(int kind, int B, int GH, int GW, int Cin, int Cout) {
 }
 
 static long long halo_blocks(int kind, int B, int GH, int GW, int Cout) {
-  const int bn = halo_bn(kind, Cout);
   halo_grid(kind, GH, GW);
-  return (long long)B * GH * GW / HB_BM * ((Cout + bn - 1) / bn) * (kind == STC_CONVT_S2 ? 4 : 1);
+  const long long mt = (long long)B * GH * GW / HB_BM;
+  const int bn = halo_bn(kind, mt, Cout, 0);
+  return mt * ((Cout + bn - 1) / bn) * (kind == STC_CONVT_S2 ? 4 : 1);
 }
 
 // The automatic plan takes the halo kernel when it fills the chip: >= 256 blocks (one 8-wave block per CU).
@@ -407,8 +420,8 @@ int halo_chunks(int kind, int B, int GH, int GW) {
 }
 
 // p: filled by bf16_conv_fwd (geometry, operands, output, epilogue options; vec_out set).  shape: 0 automatic,
-// 1 the 8-wave 160 KiB block, 2 the 4-wave 80 KiB block (force_plan {HALO_CFG, shape}: tests / A/B; N <= 64
-// ConvTs always take the 4-wave 256 x 64 block).
+// 1 the 8-wave 160 KiB block, 2 the 4-wave 80 KiB block, 3 (conv-s2) the 4-wave 256 x 64 block (force_plan
+// {HALO_CFG, shape}: tests / A/B; N <= 64 ConvTs always take the 256 x 64 block).
 int halo_launch(GParams& p, hipStream_t st, int shape) {
   const bool convt = p.nphase == 4;
   const int geom = convt ? 1 : (p.in_stride == 2 ? 0 : (p.stepy > 0 ? 2 : 3));
@@ -421,8 +434,8 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
     p.inv_gw = 1.0f / (float)p.GW;
   }
   STC_REQUIRE(p.vec_out && !p.ws && (p.nphase == 1 || convt) && p.M % HB_BM == 0, "halo conv: bad launch parameters");
-  const int bn = convt && p.N <= 64 ? 64 : HB_BN;
   p.mtiles = p.M / HB_BM;
+  const int bn = halo_bn(convt ? STC_CONVT_S2 : (geom == 0 ? STC_CONV_S2 : STC_CONV_S1), p.mtiles, p.N, shape);
   p.ntiles = (p.N + bn - 1) / bn;
   p.ksplit = 1;
   p.kchunk = p.K;
@@ -435,6 +448,10 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
 #define STC_EXP_TWO_MIN 512
 #endif
   const bool two = shape == 2 || (shape != 1 && blocks >= STC_EXP_TWO_MIN) || bn == 64;
+#ifndef STC_EXP_N64_8W
+#define STC_EXP_N64_8W 0
+#endif
+  const bool n64_8w = shape == 4 || (shape == 0 && STC_EXP_N64_8W);  // conv-s2 256 x 64: 8 waves of 32 x 64
 #define STC_HK(G_, GW_, BN_, B_, RB_, WM_, WN_)                                                               \
   hipLaunchKernelGGL((halo_conv_kernel<G_, GW_, BN_, B_, RB_, WM_, WN_>), grid, dim3(64 * WM_ * WN_),         \
                      (HaloGeom<RB_, BN_>::LDS), st, p)
@@ -443,7 +460,11 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
 #define STC_H(GW_)                                          \
   case GW_:                                                 \
     if (!convt) {                                           \
-      if (two) { STC_HB(0, GW_, 128, 64, 2, 2) }            \
+      if (bn == 64) {                                       \
+        if (n64_8w) { STC_HB(0, GW_, 64, (GW_ <= 32 ? 128 : 64), (GW_ <= 32 ? 8 : 4), 1) } \
+        else { STC_HB(0, GW_, 64, 64, 4, 1) }               \
+      }                                                     \
+      else if (two) { STC_HB(0, GW_, 128, 64, 2, 2) }       \
       else { STC_HB(0, GW_, 128, 128, 4, 2) }               \
     } else if (bn == 64) {                                  \
       STC_HB(1, GW_, 64, 64, 4, 1)                          \

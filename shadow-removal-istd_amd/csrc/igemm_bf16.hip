@@ -803,6 +803,7 @@ bool halo_auto(int kind, int B, int GH, int GW, int Cin, int Cout);
 bool halo_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y);
 int halo_chunks(int kind, int B, int GH, int GW);
 int halo_launch(GParams& p, hipStream_t st, int shape);
+int halo_plan_bn(int kind, int B, int GH, int GW, int Cout, int shape);
 // the Cin = 8 first layers with the activation epilogue (stem_bf16.hip)
 bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y, bool bnb);
 int stem_launch(GParams& p, hipStream_t st);
@@ -819,7 +820,7 @@ int bf16_conv_query(int kind, int B, int Hg, int Wg, int Cin, int Cout, int out_
     if (ws_bytes) *ws_bytes = 0;
     if (stats_chunks) *stats_chunks = halo_chunks(kind, B, Hg, Wg);
     if (plan_out) {
-      plan_out[0] = 256; plan_out[1] = kind == STC_CONVT_S2 && Cout <= 64 ? 64 : 128; plan_out[2] = 1; plan_out[3] = 0;
+      plan_out[0] = 256; plan_out[1] = halo_plan_bn(kind, B, Hg, Wg, Cout, force && force[0] == HALO_CFG ? force[1] : 0); plan_out[2] = 1; plan_out[3] = 0;
       plan_out[4] = HALO_CFG;
     }
     return 0;

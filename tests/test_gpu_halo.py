@@ -22,6 +22,8 @@ DEV = "cuda"
 BF = torch.bfloat16
 HALO = (ops.HALO_CFG, 1)   # the 8-wave block (one per CU)
 HALO2 = (ops.HALO_CFG, 2)  # the 4-wave block (two per CU)
+HALO64 = (ops.HALO_CFG, 3)  # the 4-wave 256 x 64 block (conv-s2)
+HALO64W8 = (ops.HALO_CFG, 4)  # the 8-wave 256 x 64 block (conv-s2, grids <= 32 wide; else the 4-wave one)
 
 
 def nhwc(t):
@@ -79,7 +81,7 @@ CASES = [  # B, Cin, Cout, GH, GW
 ]
 
 
-@pytest.mark.parametrize("shape", [HALO, HALO2], ids=["8wave", "4wave"])
+@pytest.mark.parametrize("shape", [HALO, HALO2, HALO64, HALO64W8], ids=["8wave", "4wave", "n64", "n64w8"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
 def test_halo_conv_s2(case, shape):
     B, Cin, Cout, GH, GW = case
@@ -87,7 +89,7 @@ def test_halo_conv_s2(case, shape):
     w = q(rnd(Cout, Cin, 4, 4, seed=2, scale=0.05, dev=DEV))
     ref = F.conv2d(x, w, None, 2, 1)
     y, mean, var, plan = run(B, x, w, Cin, Cout, GH, GW, shape)
-    assert plan[4] == ops.HALO_CFG and plan[0] == 256
+    assert plan[4] == ops.HALO_CFG and plan[0] == 256 and plan[1] == (64 if shape in (HALO64, HALO64W8) else 128)
     check(y, ref, mean, var, f"halo {case}")
     # the im2col tile on the same operands: equal up to the summation order
     y2, _, _, plan2 = run(B, x, w, Cin, Cout, GH, GW, (0, 1))
@@ -96,7 +98,7 @@ def test_halo_conv_s2(case, shape):
     assert float((y - y2).abs().max()) <= 1e-2 * scale
 
 
-@pytest.mark.parametrize("shape", [HALO, HALO2], ids=["8wave", "4wave"])
+@pytest.mark.parametrize("shape", [HALO, HALO2, HALO64, HALO64W8], ids=["8wave", "4wave", "n64", "n64w8"])
 def test_halo_views_and_bias(shape):
     """Input from a channel slice of a wider buffer (the concat buffers), output into the second half of one,
     with a bias epilogue."""
@@ -113,9 +115,30 @@ def test_halo_plan_automatic_at_train_sizes():
     """The train step's conv-s2 layers with 64-channel chunks and enough blocks take the halo kernel; the
     others keep their im2col plans."""
     for (gh, cin, cout) in ((64, 64, 128), (32, 128, 256), (64, 64, 256), (32, 128, 512), (16, 256, 1024)):
-        assert ops.conv_query(L.CONV_S2, 32, gh, gh, cin, cout, BF)[2][4] == ops.HALO_CFG, (gh, cin, cout)
-    for (gh, cin, cout) in ((128, 8, 64), (16, 256, 512), (8, 512, 512)):
+        plan = ops.conv_query(L.CONV_S2, 32, gh, gh, cin, cout, BF)[2]
+        assert plan[4] == ops.HALO_CFG and plan[1] == 128, (gh, cin, cout)
+    # e4 (16 x 16, N = 512): 128 blocks of 128 channels, 256 of 64 -> the 256 x 64 halo block
+    plan = ops.conv_query(L.CONV_S2, 32, 16, 16, 256, 512, BF)[2]
+    assert plan[4] == ops.HALO_CFG and plan[1] == 64
+    for (gh, cin, cout) in ((128, 8, 64), (8, 512, 512)):
         assert ops.conv_query(L.CONV_S2, 32, gh, gh, cin, cout, BF)[2][4] != ops.HALO_CFG, (gh, cin, cout)
+
+
+def test_halo_full_size_e4_n64():
+    """G's fourth down conv at the bench size (bs 32, 32x32x256 -> 16x16x512, the 256 x 64 halo block) with
+    statistics, vs the fp32 convolution of the same bf16 operands and the 4-wave 256 x 128 block (the same
+    32-channel stages, so the same K order per output)."""
+    B, Cin, Cout, GH = 32, 256, 512, 16
+    x = q(rnd(B, Cin, 2 * GH, 2 * GH, seed=8, dev=DEV))
+    w = q(rnd(Cout, Cin, 4, 4, seed=9, scale=0.05, dev=DEV))
+    ref = F.conv2d(x, w, None, 2, 1)
+    y, mean, var, plan = run(B, x, w, Cin, Cout, GH, GH, None)
+    assert plan[4] == ops.HALO_CFG and plan[1] == 64
+    check(y, ref, mean, var, "halo e4 full size")
+    y2, mean2, _, plan2 = run(B, x, w, Cin, Cout, GH, GH, HALO2)
+    assert plan2[1] == 128
+    assert torch.equal(y, y2)  # same K order per output: the N tile does not change the sums
+    assert float((mean - mean2).abs().max()) <= 1e-6 * (float(mean2.abs().max()) + 1e-6)
 
 
 def test_halo_full_size_e2():
