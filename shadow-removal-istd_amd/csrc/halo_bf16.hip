@@ -364,7 +364,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
 // at 256 x 256); the forward's GEMM grid is its input grid (output + 1 row and column).
 // N tile: 64 channels for a ConvT with N <= 64, and for a conv-s2 grid whose 128-channel tiles leave the chip
 // below 256 blocks while 64-channel ones fill it (the 16 x 16 level at bs 32: 128 -> 256 blocks of the 4-wave
-// 256 x 64 block); force shape 3 takes the 64-channel tile for any conv-s2 layer (tests / A/B).
+// 256 x 64 block, 8 waves of 32 x 64); force shapes 3 / 4 take the 64-channel tile (4 / 8 waves) for any conv-s2
+// layer (tests / A/B).
 static int halo_bn(int kind, long long mtiles, int Cout, int shape) {
   if (kind == STC_CONVT_S2) return Cout <= 64 ? 64 : HB_BN;
   if (kind != STC_CONV_S2 || shape == 1 || shape == 2) return HB_BN;
@@ -421,7 +422,8 @@ int halo_chunks(int kind, int B, int GH, int GW) {
 
 // p: filled by bf16_conv_fwd (geometry, operands, output, epilogue options; vec_out set).  shape: 0 automatic,
 // 1 the 8-wave 160 KiB block, 2 the 4-wave 80 KiB block, 3 (conv-s2) the 4-wave 256 x 64 block (force_plan
-// {HALO_CFG, shape}: tests / A/B; N <= 64 ConvTs always take the 256 x 64 block).
+// {HALO_CFG, shape}: tests / A/B; N <= 64 ConvTs always take the 4-wave 256 x 64 block), 4 the 8-wave 256 x 64
+// block (the automatic conv-s2 N-64 block; grids 64 wide keep 4 waves).
 int halo_launch(GParams& p, hipStream_t st, int shape) {
   const bool convt = p.nphase == 4;
   const int geom = convt ? 1 : (p.in_stride == 2 ? 0 : (p.stepy > 0 ? 2 : 3));
@@ -448,10 +450,9 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
 #define STC_EXP_TWO_MIN 512
 #endif
   const bool two = shape == 2 || (shape != 1 && blocks >= STC_EXP_TWO_MIN) || bn == 64;
-#ifndef STC_EXP_N64_8W
-#define STC_EXP_N64_8W 0
-#endif
-  const bool n64_8w = shape == 4 || (shape == 0 && STC_EXP_N64_8W);  // conv-s2 256 x 64: 8 waves of 32 x 64
+  // conv-s2 256 x 64: 8 waves of 32 x 64 in 128 KiB (automatic; e4 in the step 45 us against 59 for the 4-wave
+  // 256 x 64 block (force shape 3) and 65 for the im2col tile, profiles/r04/halo/e4_in_step.txt)
+  const bool n64_8w = shape != 3;
 #define STC_HK(G_, GW_, BN_, B_, RB_, WM_, WN_)                                                               \
   hipLaunchKernelGGL((halo_conv_kernel<G_, GW_, BN_, B_, RB_, WM_, WN_>), grid, dim3(64 * WM_ * WN_),         \
                      (HaloGeom<RB_, BN_>::LDS), st, p)

@@ -125,9 +125,10 @@ def test_halo_plan_automatic_at_train_sizes():
 
 
 def test_halo_full_size_e4_n64():
-    """G's fourth down conv at the bench size (bs 32, 32x32x256 -> 16x16x512, the 256 x 64 halo block) with
-    statistics, vs the fp32 convolution of the same bf16 operands and the 4-wave 256 x 128 block (the same
-    32-channel stages, so the same K order per output)."""
+    """G's fourth down conv at the bench size (bs 32, 32x32x256 -> 16x16x512, the 8-wave 256 x 64 halo block) with
+    statistics, vs the fp32 convolution of the same bf16 operands and the 8-wave 256 x 128 block (the same
+    64-channel stages, so the same K order per output); the 4-wave 256 x 64 block against the 4-wave 256 x 128
+    one likewise (32-channel stages)."""
     B, Cin, Cout, GH = 32, 256, 512, 16
     x = q(rnd(B, Cin, 2 * GH, 2 * GH, seed=8, dev=DEV))
     w = q(rnd(Cout, Cin, 4, 4, seed=9, scale=0.05, dev=DEV))
@@ -135,10 +136,12 @@ def test_halo_full_size_e4_n64():
     y, mean, var, plan = run(B, x, w, Cin, Cout, GH, GH, None)
     assert plan[4] == ops.HALO_CFG and plan[1] == 64
     check(y, ref, mean, var, "halo e4 full size")
-    y2, mean2, _, plan2 = run(B, x, w, Cin, Cout, GH, GH, HALO2)
-    assert plan2[1] == 128
-    assert torch.equal(y, y2)  # same K order per output: the N tile does not change the sums
-    assert float((mean - mean2).abs().max()) <= 1e-6 * (float(mean2.abs().max()) + 1e-6)
+    for shape_a, shape_b in ((None, HALO), (HALO64, HALO2)):
+        ya, ma, _, pa = run(B, x, w, Cin, Cout, GH, GH, shape_a)
+        yb, mb, _, pb = run(B, x, w, Cin, Cout, GH, GH, shape_b)
+        assert pa[1] == 64 and pb[1] == 128
+        assert torch.equal(ya, yb)  # same K order per output: the N tile does not change the sums
+        assert float((ma - mb).abs().max()) <= 1e-6 * (float(mb.abs().max()) + 1e-6)
 
 
 def test_halo_full_size_e2():
