@@ -116,7 +116,9 @@ int stc_conv_fwd_ex(int dtype, int kind, int B, stc_view x, int Cin, const void*
  * over the pixels inside x's extent; stc_bn_bwd_apply then finishes the BN backward
  * (STCGAN/networks.py:107-109,170-171,179-180 backward).  bf16 NHWC outputs compute the sums in
  * the GEMM epilogue / split-K reduction; other cases run the conv and stc_bn_bwd_reduce.
- * stc_conv_bwd_bn_chunks: the part2 chunk count for the same arguments.                    */
+ * stc_conv_bwd_bn_chunks_ex: the part2 chunk count for the same arguments (the kernel that runs, and so
+ * the count, depends on the views' layout); stc_conv_bwd_bn_chunks: the same from the shape alone, for dense
+ * 16-byte NHWC views at channel offset 0 (and no second gradient on the 31 x 31 logits-layer gradient).   */
 typedef struct {
   stc_view x;        /* BN input (raw pre-BN values), C channels, extent = the BN domain  */
   stc_view g_other;  /* optional second gradient into the BN output (p == NULL: none)     */
@@ -128,6 +130,8 @@ typedef struct {
   int32_t C, ch_off;
 } stc_bnb_fuse;
 int stc_conv_bwd_bn_chunks(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int xH, int xW);
+int stc_conv_bwd_bn_chunks_ex(int dtype, int kind, int B, stc_view dy, int Cin, int Cout, stc_view out,
+                              const stc_bnb_fuse* bnb);
 int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout, stc_view out,
                     const stc_bnb_fuse* bnb, float* part2, int nchunks,
                     void* workspace, int64_t workspace_bytes, void* stream);

@@ -853,8 +853,25 @@ static bool bnb_fused_path(int dtype, int kind, int B, const stc_view& dy, int C
 
 namespace stc {
 int stem_bnb_chunks(int kind, int B, int Hg, int Wg, int Cin, int Cout);
+int bf16_bnb_chunks(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y, bool g_other);
 }
 
+// the part2 chunk count of stc_conv_bwd_bn for these exact views (the kernel route depends on the layout)
+static int bwd_bn_chunks_of(int dtype, int kind, int B, const stc_view& dy, int Cin, int Cout, const stc_view& out,
+                            const stc_bnb_fuse& bnb) {
+  if (bnb_fused_path(dtype, kind, B, dy, Cin, Cout, out))
+    return bf16_bnb_chunks(kind, B, dy, Cin, Cout, out, bnb.g_other.p != nullptr);
+  return stc_chan_stats_chunks(B, bnb.x.H, bnb.x.W);
+}
+
+extern "C" int stc_conv_bwd_bn_chunks_ex(int dtype, int kind, int B, stc_view dy, int Cin, int Cout, stc_view out,
+                                         const stc_bnb_fuse* bnb) {
+  if (!bnb || kind < 0 || kind > 3) return fail(-1, "stc_conv_bwd_bn_chunks_ex: bad arguments"), 0;
+  return bwd_bn_chunks_of(dtype, kind, B, dy, Cin, Cout, out, *bnb);
+}
+
+// (shape-only form: assumes dense 16-byte NHWC views at channel offset 0 and no second gradient for the 31 x 31
+// logits-layer input gradient -- stc_conv_bwd_bn_chunks_ex answers for the actual views)
 extern "C" int stc_conv_bwd_bn_chunks(int dtype, int kind, int B, int Hg, int Wg, int Cin, int Cout, int xH, int xW) {
   if (bf16_path(dtype, kind, Cin, Cout)) {
     if (const int sn = stem_bnb_chunks(kind, B, Hg, Wg, Cin, Cout)) return sn;  // (the streaming Cin = 8 kernel)
@@ -871,20 +888,8 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
   STC_REQUIRE(bnb && part2, "stc_conv_bwd_bn: bnb and part2 required");
   hipStream_t st = (hipStream_t)stream;
   if (bnb_fused_path(dtype, kind, B, dy, Cin, Cout, out)) {
-    const Geometry g = geometry(kind);
-    const int Hg = kind == STC_CONVT_S2 ? dy.H : out.H, Wg = kind == STC_CONVT_S2 ? dy.W : out.W;
-    int32_t need = stem_bnb_chunks(kind, B, Hg, Wg, Cin, Cout);
-    if (need && kind == STC_CONV_S2) {  // the streaming Cin = 8 kernel: a dense 8-channel input view
-      STC_REQUIRE(dy.cs == 1 && dy.ps == 8 && dy.co == 0 && out.H * 2 == dy.H && out.W * 2 == dy.W,
-                  "stc_conv_bwd_bn: the 8-channel input of this shape must be a dense NHWC tensor");
-    } else if (need) {  // the logits layer's input gradient: no second gradient
-      STC_REQUIRE(!bnb->g_other.p && dy.cs == 1 && dy.ps % 8 == 0 && dy.co % 8 == 0,
-                  "stc_conv_bwd_bn: the 31x31 logits-layer input gradient takes no second gradient");
-    } else {
-      bf16_conv_query(kind, B, Hg, Wg, Cin, Cout, 0, nullptr, nullptr, &need, nullptr);
-    }
-    (void)g;
-    STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks)", nchunks, need);
+    const int need = bwd_bn_chunks_of(dtype, kind, B, dy, Cin, Cout, out, *bnb);
+    STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks_ex)", nchunks, need);
     return bf16_conv_fwd(kind, B, dy, Cin, w_packed, Cout, out, nullptr, 0, 0, nullptr, need, nullptr, workspace,
                          workspace_bytes, st, bnb, part2);
   }
@@ -896,7 +901,7 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
   g1.H = bnb->x.H;
   g1.W = bnb->x.W;
   const int need = stc_chan_stats_chunks(B, bnb->x.H, bnb->x.W);
-  STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks)", nchunks, need);
+  STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks_ex)", nchunks, need);
   return stc_bn_bwd_reduce(dtype, B, bnb->x, bnb->C, bnb->scale, bnb->shift, bnb->mean, bnb->rstd, g1, bnb->slope_self,
                            bnb->g_other, bnb->slope_other, part2, need, stream);
 }

@@ -809,6 +809,7 @@ bool stem_eligible(int kind, int B, const stc_view& x, int Cin, int Cout, const 
 int stem_launch(GParams& p, hipStream_t st);
 bool stem_s1d_eligible(int kind, int B, const stc_view& dy, int Cin, int Cout, const stc_view& y);
 int stem_s1d_launch(GParams& p, hipStream_t st);
+int stem_bnb_chunks(int kind, int B, int Hg, int Wg, int Cin, int Cout);
 static bool halo_plan(const int32_t* force, int kind, int B, int GH, int GW, int Cin, int Cout) {
   if (force && force[0] == HALO_CFG) return halo_geometry_ok(kind, B, GH, GW, Cin, Cout);
   return (!force || force[0] == -1) && halo_auto(kind, B, GH, GW, Cin, Cout);
@@ -911,6 +912,22 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
   }
   STC_REQUIRE(!(force && force[0] == HALO_CFG), "bf16 conv: the halo kernel does not take this shape / view");
   return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st);
+}
+
+// Partial count of the fused BN-backward sums for these views: the route bf16_conv_fwd takes for a BN-backward
+// call (no statistics, no forced plan) -- the streaming logits-gradient kernel, the streaming Cin = 8 kernel, the
+// halo kernel or the im2col tile -- decides it, so views that one of the streaming / halo kernels does not take
+// (not dense at channel offset 0, a second gradient for the 31 x 31 layer) get the chunk count of the kernel that
+// then runs, not the shape's default.
+int bf16_bnb_chunks(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y, bool g_other) {
+  const int Hg = kind == STC_CONVT_S2 ? x.H : y.H, Wg = kind == STC_CONVT_S2 ? x.W : y.W;
+  if (!g_other && stem_s1d_eligible(kind, B, x, Cin, Cout, y)) return stem_bnb_chunks(kind, B, Hg, Wg, Cin, Cout);
+  if (stem_eligible(kind, B, x, Cin, Cout, y, true)) return stem_bnb_chunks(kind, B, Hg, Wg, Cin, Cout);
+  if (halo_plan(nullptr, kind, B, Hg, Wg, Cin, Cout) && halo_eligible(kind, B, x, Cin, Cout, y))
+    return halo_chunks(kind, B, Hg, Wg);
+  const Geometry g = geometry(kind);
+  const int taps = g.taps_lg_tw == 2 ? 16 : 4;
+  return bf16_problem(B * Hg * Wg, Cout, taps * Cin, g.nphase, nullptr, true).stats_chunks;
 }
 
 // The activation epilogue applies when the layer runs as one LDS-DMA GEMM launch (no split-K) with 16-byte

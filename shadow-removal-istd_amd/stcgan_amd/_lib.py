@@ -53,6 +53,7 @@ _SIGS = {
     "stc_conv_fwd_plan": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "stc_conv_fwd_query": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "stc_conv_bwd_bn_chunks": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32]),
+    "stc_conv_bwd_bn_chunks_ex": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, _vp]),
     "stc_conv_bwd_bn": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _i32, _vp, _i64, _vp]),
     "stc_conv_fwd_ex": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _i32, _i32, _vp, _i32, _vp, _vp,
                                _i64, _vp]),
@@ -171,6 +172,11 @@ def nhwc_view(t, c0=0, H=None, W=None):
     v = View(t.data_ptr(), H, W, Ha * Wa * C, Wa * C, C, c0, 1, 0)
     v._keep = t
     return v
+
+
+def layout_key(v):
+    """The layout of a view as the kernels' routing sees it (extent, strides, channel offset, 16-byte alignment)."""
+    return (v.H, v.W, v.bs, v.rs, v.ps, v.co, v.cs, (v.p or 0) % 16)
 
 
 def nchw_view(t):

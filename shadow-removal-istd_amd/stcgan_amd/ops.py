@@ -237,7 +237,10 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
         geom = {L.CONV_S2: 0, L.CONVT_S2: 1, L.CONV_S1: 2, L.CONV_S1_DGRAD: 3}[kind]
         vh, vw = (gh + 1, gw + 1) if kind == L.CONV_S1 else (gh, gw)  # (the s1 forward: its input grid)
         blocks = B * vh * vw // 256 * ((cout + bn - 1) // bn) * (4 if convt else 1)
-        rb, wm, wn = (64, 4, 1) if bn == 64 else ((64, 2, 2) if blocks >= 512 else (128, 4, 2))
+        if bn == 64:  # (csrc/halo_bf16.hip halo_launch: conv-s2 grids <= 32 wide take the 8-wave 256 x 64 block)
+            rb, wm, wn = (128, 8, 1) if (kind == L.CONV_S2 and vw <= 32) else (64, 4, 1)
+        else:
+            rb, wm, wn = (64, 2, 2) if blocks >= 512 else (128, 4, 2)
         return (f"halo_conv_kernel<{geom}, {vw}, {bn}, {str(bnb).lower()}, {rb}, {wm}, {wn}>", True)
     if cfg >= 0:
         t = _BF16_TILES[cfg]
@@ -268,14 +271,17 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
     gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
     nbytes = _conv_ws_bytes(kind, B, gh, gw, cin, cout, dt)
     ws, nb = _ws(nbytes, dev)
-    key = ("bnbch", kind, B, gh, gw, cin, cout, dt, bn_x.H, bn_x.W)
-    nch = _MEMO.get(key)
-    if nch is None:
-        nch = _MEMO[key] = l.stc_conv_bwd_bn_chunks(L.dtype_code(dt), kind, B, gh, gw, cin, cout, bn_x.H, bn_x.W)
-    part = torch.empty((nch, C, 2), dtype=torch.float32, device=dev)
     scale, shift, mean, rstd = bn_state
     fuse = L.BnbFuse(bn_x, g_other if g_other is not None else L.NULL_VIEW, scale.data_ptr(), shift.data_ptr(),
                      mean.data_ptr(), rstd.data_ptr(), float(s_self), float(s_other), C, ch_off)
+    # the chunk count depends on which kernel takes the call, which depends on the views' layout (not only shapes)
+    key = ("bnbch", kind, B, cin, cout, dt, L.layout_key(xv), L.layout_key(yv), bn_x.H, bn_x.W, g_other is None)
+    nch = _MEMO.get(key)
+    if nch is None:
+        nch = _MEMO[key] = l.stc_conv_bwd_bn_chunks_ex(L.dtype_code(dt), kind, B, xv, cin, cout, yv,
+                                                       ctypes.byref(fuse))
+        check(0 if nch > 0 else -1, "stc_conv_bwd_bn_chunks_ex")
+    part = torch.empty((nch, C, 2), dtype=torch.float32, device=dev)
     timer = _timer
     if timer is not None:
         e0, e1 = _main_events()

@@ -416,7 +416,20 @@ class Adam(torch.optim.Optimizer):
         self._fast = {}
         self._steps = {}
         self._ov_done = {}
+        # the moment buffers keep their storage: a captured graph (STCGAN.capture) and its pointer tables hold
+        # their addresses, so the loaded values are copied into them rather than swapped in as new tensors
+        held = {id(p): (p, {k: v for k, v in self.state[p].items() if k in ("exp_avg", "exp_avg_sq")})
+                for g in self.param_groups for p in g["params"] if p in self.state}
         out = super().load_state_dict(state_dict)
+        for p, old in held.values():
+            st = self.state.get(p)
+            if st is None:
+                continue
+            for k, t in old.items():
+                new = st.get(k)
+                if new is not None and new is not t and new.shape == t.shape:
+                    t.copy_(new)
+                    st[k] = t
         # device-resident counts (device_step): the loaded state's; the counter tensors are kept (a captured
         # graph holds them), the next step takes the general path and writes them
         if self._dev:

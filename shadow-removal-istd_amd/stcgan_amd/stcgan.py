@@ -63,6 +63,14 @@ def batch_weight(local_n, global_n, world):
     return local_n * world / global_n
 
 
+def weighted_loss(loss, weight):
+    """The loss a rank back-propagates: its shard mean scaled by ``weight`` (batch_weight).  The gradient
+    exchange averages the ranks' gradients with equal weight, so sum_r w_r * grad(mean over shard r) / world =
+    grad(mean over the global batch) -- DataParallel's gradient, whose loss is computed on the gathered outputs
+    (STCGAN/stcgan.py:53-59) -- also when a ragged final batch gives the ranks shards of different sizes."""
+    return loss if weight == 1.0 else loss * weight
+
+
 def accumulate(acc, vals, d_out, weight=1.0):
     """Add one step's losses (``vals``: device fp32 scalars) and mean discriminator outputs (``d_out``: C1_real,
     C1_fake, C2_real, C2_fake) into the float64 device sums ``acc``, each value widened to float64 first (the
@@ -352,7 +360,7 @@ class STCGAN(object):
                 D_loss = self.lambda2 * D1_loss + self.lambda3 * D2_loss
             if training:
                 self._exchange(("D1", "D2"), 2)  # real + fake calls
-                D_loss.backward()
+                weighted_loss(D_loss, weight).backward()
                 self._finish_exchange(("D2", "D1"))
                 self.optim_D.step()
             d_out = (C1_real.detach(), C1_fake.detach(), C2_real.detach(), C2_fake.detach())
@@ -389,7 +397,7 @@ class STCGAN(object):
                 G_loss = data1_loss + self.lambda1 * data2_loss + self.lambda2 * G1_loss + self.lambda3 * G2_loss
             if training:
                 self._exchange(("G1", "G2"), 1)
-                G_loss.backward()
+                weighted_loss(G_loss, weight).backward()
                 self._finish_exchange(("G2", "G1"))
                 self.optim_G.step()
         if l1 is not None:  # nothing on the side lanes outlives the step

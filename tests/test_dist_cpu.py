@@ -209,6 +209,14 @@ def _worker_semantics(rank, world, port, out):
     w = stcgan.batch_weight(hi - lo, 5, world)
     stcgan.accumulate(acc, {"D": per_sample[lo:hi].mean()}, [c_out[lo:hi]] * 4, w)
     res["ragged"] = ((lo, hi), {k: float(v) for k, v in parallel.average_scalars(acc).items()})
+    # (5b) ... and its gradients: each rank back-propagates its shard mean scaled by the same weight
+    # (stcgan.weighted_loss), so the equal-weight rank average is the global-batch mean's gradient
+    wv = torch.zeros(3, requires_grad=True)
+    feats = torch.arange(15, dtype=torch.float32).reshape(5, 3) / 4.0 - 1.0
+    shard_mean = ((feats[lo:hi] * (wv + 0.5)).sum(1) ** 2).mean()
+    stcgan.weighted_loss(shard_mean, w).backward()
+    parallel.GradAllReduce([[wv]])()
+    res["ragged_grad"] = wv.grad.clone()
     # (6) GradAllReduce across a set_to_none zero_grad: autograd's fresh gradients are moved into the views
     q = torch.zeros(4, requires_grad=True)
     sync2 = parallel.GradAllReduce([[q]])
@@ -263,6 +271,11 @@ def test_dataparallel_semantics_world2():
         bounds, vals = r["ragged"]
         assert abs(vals["D"] - float(per_sample.mean())) < 1e-6  # (fp32 per-rank means)
         assert abs(vals["D1_fake"] - float(c_out.double().mean())) < 1e-6
+        # ... and the gradient is the global-batch mean's (DataParallel), not the mean of the shard means
+        wv = torch.zeros(3, requires_grad=True)
+        feats = torch.arange(15, dtype=torch.float32).reshape(5, 3) / 4.0 - 1.0
+        ((feats * (wv + 0.5)).sum(1) ** 2).mean().backward()
+        assert torch.allclose(r["ragged_grad"], wv.grad, atol=1e-6, rtol=1e-5), (r["ragged_grad"], wv.grad)
         # second backward after zero_grad(set_to_none): still averaged over ranks ((1+2)/2 + 1)
         g, owned = r["zero_grad"]
         assert owned and torch.equal(g, torch.full((4,), 2.5))

@@ -103,3 +103,34 @@ def test_general_path_step_after_replays():
     bad = _same(_state(eager), _state(graphed))
     assert not bad, bad[:8]
     assert float(graphed.optim_D.state[next(graphed.D1.parameters())]["step"]) == 7.0
+
+
+def test_replay_after_optimizer_state_load():
+    """An optimiser state loaded into a captured trainer (a checkpoint resume) must reach the replay: the loaded
+    moments are copied into the moment buffers the graph's pointer tables hold (torch's
+    load_state_dict swapped in new tensors, and the replay kept updating the old ones)."""
+    import copy
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    B = 2
+    x = torch.rand((B, 3, 256, 256), generator=g, device="cuda") * 2 - 1
+    m = (torch.rand((B, 1, 256, 256), generator=g, device="cuda") < 0.5).float() * 2 - 1
+    y = torch.rand((B, 3, 256, 256), generator=g, device="cuda") * 2 - 1
+    eager = _trainer("bf16", 16, "normal")
+    graphed = _trainer("bf16", 16, "normal")
+    replay = graphed.capture(x, m, y, warmup=1)  # 3 eager steps inside
+    for _ in range(3):
+        eager.train_step(x, m, y)
+    assert not _same(_state(eager), _state(graphed))
+    for oname in ("optim_G", "optim_D"):  # a different (synthetic) saved state, loaded into both trainers
+        sd = copy.deepcopy(getattr(eager, oname).state_dict())
+        for st in sd["state"].values():
+            st["exp_avg"].mul_(0.5)
+            st["exp_avg_sq"].mul_(2.0)
+        getattr(eager, oname).load_state_dict(copy.deepcopy(sd))
+        getattr(graphed, oname).load_state_dict(copy.deepcopy(sd))
+    assert not _same(_state(eager), _state(graphed))
+    eager.train_step(x, m, y)
+    replay()
+    bad = _same(_state(eager), _state(graphed))
+    assert not bad, bad[:8]
