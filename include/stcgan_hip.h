@@ -149,6 +149,48 @@ int stc_conv_fwd_act(int dtype, int kind, int B, stc_view x, int Cin, const void
                      stc_view y1, float slope1, stc_view y2, float slope2, const float* bias,
                      void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ---- the U-Net's innermost levels, one launch per layer (bf16) --------------------------------------
+ * Replaces, for the three innermost generator levels (STCGAN/networks.py:104-105 down convs, :119-121 /
+ * :126-128 up ConvTs: grids of 1x1 - 8x8 at 256x256), the four launches per layer of the im2col path --
+ * stc_conv_fwd_ex (split K), its split-K reduction, stc_bn_finalize, stc_bn_apply -- by one: the A operand
+ * is read RAW and each source's BatchNorm affine + activation is applied as it is staged, the table merged
+ * in the prologue from the producer's statistics partials (or given: eval mode); split-K slices are summed
+ * in-launch in split order by the last-arriving block of each tile (a ticket per tile, agent-scope
+ * release / acquire; tickets must be zero before the first launch and are left zero); the output's
+ * BatchNorm statistics partials come out in the stc_conv_fwd_ex format.  kind: STC_CONV_S2 (GEMM grid =
+ * output grid) or STC_CONVT_S2 (GEMM grid = input grid, 4 phases); the sources' channels are concatenated
+ * in order (the U-Net concat [skip | up] of a ConvT input); each a multiple of 64.
+ * A source's designated outputs (mean / rstd / scale / shift tables, running statistics, the batch count):
+ * written by this launch when non-NULL -- set them on exactly one launch that reads the source.
+ * stc_deep_conv_query: workspace (split-K slabs), tickets and statistics chunks of the plan;
+ * plan_out[5] = {BM, BN, ksplit, taps kept, blocks}.                                                     */
+typedef struct {
+  stc_view x;             /* NHWC bf16 source (raw conv output, or an activation: no table, slope 1)   */
+  int32_t C;              /* its channels (a multiple of 64)                                           */
+  int32_t nchunks;        /* statistics partial chunks (part != NULL)                                  */
+  const float* part;      /* [nchunks][C][4] statistics partials of x, or NULL                         */
+  const float* scale;     /* a ready table when part == NULL (NULL: identity)                          */
+  const float* shift;
+  const float* gamma;     /* BatchNorm affine (part != NULL)                                           */
+  const float* beta;
+  float eps, momentum;
+  float slope;            /* activation after the affine: 0 ReLU, 0.2 LeakyReLU, 1 none                */
+  int32_t pad_;
+  float* mean_out;        /* designated outputs (NULL: not this launch)                                */
+  float* rstd_out;
+  float* scale_out;
+  float* shift_out;
+  float* running_mean;
+  float* running_var;
+  int64_t* num_batches_tracked;
+} stc_deep_src;
+int stc_deep_conv_query(int kind, int B, int Hg, int Wg, int IH, int IW, int Cin, int Cout,
+                        const int32_t* force_plan, int64_t* workspace_bytes, int32_t* ntickets,
+                        int32_t* stats_chunks, int32_t* plan_out);
+int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src, const void* w_packed, int Cout, stc_view y,
+                  float* stats_part, int stats_chunks, const int32_t* force_plan, uint32_t* tickets, int ntickets,
+                  void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---- weight gradient ---------------------------------------------------------
  * dW[r][ci][kh][kw] = sum_{b,oy,ox} D[b,oy,ox,r] * G[b, oy*s+kh-1, ox*s+kw-1, ci]
  *   Conv2d s2/s1 : D = dy (grid = output), G = x (input), s = stride

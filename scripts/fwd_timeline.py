@@ -23,7 +23,11 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--deep", type=int, default=None, help="engine.DEEP (the innermost levels on stc_deep_conv)")
     a = ap.parse_args()
+    if a.deep is not None:
+        from stcgan_amd import engine
+        engine.DEEP = bool(a.deep)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     g1 = networks.get_generator(3, 1).apply(networks.weights_init).to(dev).set_compute_dtype(a.dtype).train()

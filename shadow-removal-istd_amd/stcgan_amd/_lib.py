@@ -38,6 +38,17 @@ class BnbFuse(ctypes.Structure):
                 ("slope_other", ctypes.c_float), ("C", ctypes.c_int32), ("ch_off", ctypes.c_int32)]
 
 
+class DeepSrc(ctypes.Structure):
+    """stc_deep_src: one source of a stc_deep_conv launch (a raw tensor + its BatchNorm statistics or table)."""
+    _fields_ = [("x", View), ("C", ctypes.c_int32), ("nchunks", ctypes.c_int32), ("part", ctypes.c_void_p),
+                ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p), ("gamma", ctypes.c_void_p),
+                ("beta", ctypes.c_void_p), ("eps", ctypes.c_float), ("momentum", ctypes.c_float),
+                ("slope", ctypes.c_float), ("pad_", ctypes.c_int32), ("mean_out", ctypes.c_void_p),
+                ("rstd_out", ctypes.c_void_p), ("scale_out", ctypes.c_void_p), ("shift_out", ctypes.c_void_p),
+                ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
+                ("num_batches_tracked", ctypes.c_void_p)]
+
+
 class PackDesc(ctypes.Structure):
     """stc_pack_desc: one stc_pack_weight job of a multi-tensor stc_pack_weights launch."""
     _fields_ = [("mode", ctypes.c_int32), ("P", ctypes.c_int32), ("Q", ctypes.c_int32), ("N_pad", ctypes.c_int32),
@@ -59,6 +70,8 @@ _SIGS = {
                                _i64, _vp]),
     "stc_conv_fwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View]),
     "stc_conv_fwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _f32, View, _f32, _vp, _vp, _i64, _vp]),
+    "stc_deep_conv_query": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "stc_deep_conv": (_i32, [_i32, _i32, _i32, _vp, _vp, _i32, View, _vp, _i32, _vp, _vp, _i32, _vp, _i64, _vp]),
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
                               _f32, _vp, _vp, _i64, _vp]),
     "stc_conv_wgrad_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32]),

@@ -193,6 +193,9 @@ class BucketExchange:
         self.member_params = [[by_id[i] for i in m] for m in self.members]
         self.expected = 1
         self.launch_order = []  # bucket indices in launch order (diagnostics / tests)
+        # diagnostics (scripts/exchange_timeline.py): when a list, every ready() call appends (parameter ids, event
+        # recorded on the stream that wrote them) and finish() appends ("finish", event) -- also at world 1
+        self.trace = None
         self.reset()
 
     def _cut(self, ids, a, e):
@@ -223,6 +226,10 @@ class BucketExchange:
         self.launch_order.append(b)
 
     def ready(self, params, stream=None):
+        if self.trace is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream if stream is not None else torch.cuda.current_stream())
+            self.trace.append(([id(p) for p in params], ev))
         if not self.active and self.on_complete is None:
             return
         for p in params:
@@ -252,6 +259,10 @@ class BucketExchange:
 
     def finish(self):
         w = world()
+        if self.trace is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.trace.append(("finish", ev))
         if not self.active:
             self.reset()
             return

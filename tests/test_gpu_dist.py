@@ -84,11 +84,21 @@ def _worker(rank, world, port, cfg, out):
     try:
         loss_type, ngf, dtype, family, same = cfg
         tr = _trainer(loss_type, ngf, dtype, family)
+        from stcgan_amd import engine
+        assert tr.streams and engine.WGRAD_OVERLAP  # (the side lanes and weight-gradient streams are on)
+        launched = {}
         for x, m, y in _global_batches():
             if not same:  # this rank's shard of the global batch
                 b = x.shape[0] // world
                 x, m, y = (t[rank * b:(rank + 1) * b] for t in (x, m, y))
             tr.train_step(x.cuda(), m.cuda(), y.cuda())
+            # every rank launched each network's bucket collectives in the same order (raises otherwise): the
+            # engine reports buckets in autograd order, whatever the lanes' enqueue timing
+            for n in NETS:
+                ex = getattr(tr, n).grad_exchange
+                ex.check_order()
+                launched[n] = len(ex.launch_order)
+        assert all(v > 0 for v in launched.values()), launched
         buf = io.BytesIO()
         torch.save(_state(tr), buf)  # bytes, not shared-memory tensors: the worker may exit first
         out.put((rank, buf.getvalue()))
