@@ -1,0 +1,14 @@
+#!/bin/bash
+# stc_deep_conv: GPU tests, then the plan sweep (scripts/deep_tune.py) and the forward with the deep path on / off.
+set -o pipefail
+O=gpurun_out/${1:-deep_tune}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_gpu_deep.py -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+timeout -k 10 500 python -u scripts/deep_tune.py ${TUNE_ARGS} > $O/tune.log 2>&1 || { tail -5 $O/tune.log; exit 1; }
+grep "==" $O/tune.log
+for d in 0 1; do
+  timeout -k 10 240 python scripts/fwd_timeline.py --reps 5 --deep $d > $O/fwd_deep$d.json 2> $O/fwd_deep$d.err || exit 1
+  echo "deep=$d $(cat $O/fwd_deep$d.json)"
+done

@@ -23,6 +23,8 @@
 //
 // v_mfma_f32_16x16x32_bf16, 4 waves (2 x 2), K-steps of 64 (one tap, 64 channels of one source), LDS double
 // buffer, A and B both register-staged (one uniform vmcnt discipline; the weights are read once per block).
+#include <type_traits>
+
 #include "igemm_bf16.hpp"
 
 namespace stc {
@@ -50,7 +52,7 @@ struct DeepParams {
   int IH, IW;               // A extent (both sources)
   int GH, GW, M;            // GEMM grid (conv: output, ConvT: input), rows per phase
   int N, Cin, ntaps;        // K = ntaps * Cin
-  unsigned char taps[4][16];  // per phase: packed tap index of K-tap t
+  unsigned long long tapl[4];  // per phase: packed tap index of K-tap t in bits [4t, 4t + 4)
   const bf16* w;
   int w_taps;               // taps per phase in the packed layout (16 / 4)
   long long w_phase_stride; // elements
@@ -199,10 +201,17 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
   }
   const bf16* wph = p.w + (long long)ph * p.w_phase_stride;
 
-  uint4 ra[AC], rb[BC];
+  // register ring: NS K-steps of A / B chunks in flight (one Regs per step, held by value: compile-time slots)
+  constexpr int NS = (AC + BC) <= 4 ? 3 : 2;
+  struct Regs {
+    uint4 a[AC], b[BC];
+    bool pad[AC];
+  };
+  const unsigned long long tapl = ph == 0 ? p.tapl[0] : (ph == 1 ? p.tapl[1] : (ph == 2 ? p.tapl[2] : p.tapl[3]));
   auto load = [&](int ks) {
+    Regs r;
     const int ti = ks / cpt, cb = (ks - ti * cpt) * 64;
-    const int tap = p.taps[ph][ti];
+    const int tap = (int)((tapl >> (4 * ti)) & 15u);
     int dy, dx;
     if (p.convt) { dy = py - (tap >> 1); dx = px - (tap & 1); }
     else { dy = (tap >> 2) - 1; dx = (tap & 3) - 1; }
@@ -217,27 +226,28 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
       const int iy = p.convt ? a_gy[u] + dy : 2 * a_gy[u] + dy, ix = p.convt ? a_gx[u] + dx : 2 * a_gx[u] + dx;
       const bool ok = a_in[u] && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
       const int iyc = ok ? iy : 0, ixc = ok ? ix : 0;
-      const uint4 v = *reinterpret_cast<const uint4*>(sp + (long long)a_b[u] * sbs + (long long)iyc * srs +
-                                                      (long long)ixc * sps + c + 8 * a_cj[u]);
-      ra[u] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
-      a_pad[u] = !ok;  // (padding: zero after the activation, not act(affine(0)))
+      // (clamped in-bounds address; the padding is zeroed when the chunk is staged -- a select on the loaded value
+      // here would wait for the load)
+      r.a[u] = *reinterpret_cast<const uint4*>(sp + (long long)a_b[u] * sbs + (long long)iyc * srs +
+                                               (long long)ixc * sps + c + 8 * a_cj[u]);
+      r.pad[u] = !ok;  // (padding: zero after the activation, not act(affine(0)))
     }
 #pragma unroll
     for (int u = 0; u < BC; ++u) {
-      const int n = n0 + b_row[u];
-      rb[u] = n < p.N ? *reinterpret_cast<const uint4*>(wph + ((long long)n * p.w_taps + tap) * p.Cin + cb + 8 * b_cj[u])
-                      : make_uint4(0u, 0u, 0u, 0u);
+      const int n = min(n0 + b_row[u], p.N - 1);  // (rows past N: any row; their columns are not stored)
+      r.b[u] = *reinterpret_cast<const uint4*>(wph + ((long long)n * p.w_taps + tap) * p.Cin + cb + 8 * b_cj[u]);
     }
+    return r;
   };
-  auto stage_store = [&](int ks, char* st) {
+  auto stage_store = [&](int ks, const Regs r, char* st) {
     const int cb = (ks % cpt) * 64;
     const bool s1 = p.nsrc == 2 && cb >= p.src[0].nc;
     const int mode = s1 ? p.src[1].mode : p.src[0].mode;
     const float slope = s1 ? p.src[1].slope : p.src[0].slope;
 #pragma unroll
     for (int u = 0; u < AC; ++u) {
-      uint4 v = ra[u];
-      if (mode && !a_pad[u]) {
+      uint4 v = r.pad[u] ? make_uint4(0u, 0u, 0u, 0u) : r.a[u];
+      if (mode && !r.pad[u]) {
         const int kc = cb + 8 * a_cj[u];
         const unsigned w[4] = {v.x, v.y, v.z, v.w};
         unsigned o[4];
@@ -255,7 +265,7 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
 #pragma unroll
     for (int u = 0; u < BC; ++u) {
       const int row = b_row[u];
-      *reinterpret_cast<uint4*>(st + BM * 128 + row * 128 + ((b_cj[u] ^ (row & 7)) * 16)) = rb[u];
+      *reinterpret_cast<uint4*>(st + BM * 128 + row * 128 + ((b_cj[u] ^ (row & 7)) * 16)) = r.b[u];
     }
   };
 
@@ -265,37 +275,54 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int rl = lane & 15, kq = lane >> 4;
+  auto compute = [&](const char* st) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * TM + 16 * i + rl;
+        fa[i] = *reinterpret_cast<const bf16x8_t*>(st + row * 128 + (((4 * kk + kq) ^ (row & 7)) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * TN + 16 * j + rl;
+        fb[j] = *reinterpret_cast<const bf16x8_t*>(st + BM * 128 + row * 128 + (((4 * kk + kq) ^ (row & 7)) * 16));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
 
   __syncthreads();  // (the prologue table)
   if (ks0 < ks1) {
-    load(ks0);
-    stage_store(ks0, smem);
+    // (loads of steps past ks1 are clamped to the last step: harmless re-reads, no branch around a load)
+    Regs R0 = load(ks0), R1 = load(min(ks0 + 1, ks1 - 1)), R2;
+    if constexpr (NS == 3) R2 = load(min(ks0 + 2, ks1 - 1));
+    stage_store(ks0, R0, smem);
     __syncthreads();
-    for (int ks = ks0; ks < ks1; ++ks) {
-      const int cur = (ks - ks0) & 1;
-      const char* st = smem + cur * STAGE;
-      const bool more = ks + 1 < ks1;
-      if (more) load(ks + 1);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8_t fa[FM], fb[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int row = wm * TM + 16 * i + rl;
-          fa[i] = *reinterpret_cast<const bf16x8_t*>(st + row * 128 + (((4 * kk + kq) ^ (row & 7)) * 16));
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int row = wn * TN + 16 * j + rl;
-          fb[j] = *reinterpret_cast<const bf16x8_t*>(st + BM * 128 + row * 128 + (((4 * kk + kq) ^ (row & 7)) * 16));
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      }
-      if (more) stage_store(ks + 1, smem + (cur ^ 1) * STAGE);
+    // step ks: its registers (slot (ks - ks0) % NS) were staged into LDS buffer (ks - ks0) & 1 by the previous step;
+    // refill the slot with step ks + NS, compute step ks, stage step ks + 1 into the other buffer, one barrier
+    auto step = [&](int base, auto dc, Regs& mine, const Regs& next) {
+      constexpr int d = decltype(dc)::value;
+      const int ks = base + d;
+      if (ks >= ks1) return;
+      mine = load(min(ks + NS, ks1 - 1));
+      compute(smem + ((ks - ks0) & 1) * STAGE);
+      if (ks + 1 < ks1) stage_store(ks + 1, next, smem + (((ks - ks0) & 1) ^ 1) * STAGE);
       __syncthreads();
+    };
+    for (int base = ks0; base < ks1; base += NS) {
+      if constexpr (NS == 3) {
+        step(base, std::integral_constant<int, 0>{}, R0, R1);
+        step(base, std::integral_constant<int, 1>{}, R1, R2);
+        step(base, std::integral_constant<int, 2>{}, R2, R0);
+      } else {
+        step(base, std::integral_constant<int, 0>{}, R0, R1);
+        step(base, std::integral_constant<int, 1>{}, R1, R0);
+      }
     }
   }
 
@@ -591,8 +618,10 @@ extern "C" int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src,
   p.inv_ghw = 1.0f / (float)(GH * GW);
   p.inv_gw = 1.0f / (float)GW;
   p.N = Cout; p.Cin = Cin; p.ntaps = pl.ntaps;
-  for (int a = 0; a < 4; ++a)
-    for (int b = 0; b < 16; ++b) p.taps[a][b] = pl.taps[a][b];
+  for (int a = 0; a < 4; ++a) {
+    p.tapl[a] = 0;
+    for (int b = 0; b < pl.ntaps; ++b) p.tapl[a] |= (unsigned long long)(pl.taps[a][b] & 15) << (4 * b);
+  }
   p.w = (const bf16*)w_packed;
   p.w_taps = convt ? 4 : 16;
   p.w_phase_stride = (long long)Cout * p.w_taps * Cin;

@@ -121,7 +121,7 @@ class STCGAN(object):
         # and the updates' HBM traffic only moved time into the backward's kernels (round-3 A/B, scripts/
         # ab_overlap.py: 13.22 vs 13.05 ms/step)
         world = parallel.world()
-        self.bucket_mb = float(getattr(args, "bucket_mb", 32 if world > 1 else 8))
+        self.bucket_mb = float(getattr(args, "bucket_mb", 16 if world > 1 else 8))
         for net in (self.G1, self.G2, self.D1, self.D2):
             net.grad_exchange = parallel.BucketExchange(parallel.flat_grads(net), self.bucket_mb)
         self.set_overlap_optim(bool(getattr(args, "overlap_optim", False)))
