@@ -5,19 +5,18 @@
 // latency and weight streaming, not MFMA work.  The im2col path ran each as four launches (the GEMM, a split-K
 // reduction, the BatchNorm finalize, the BatchNorm + activation pass); here one launch does all of it:
 //
-//   * A operand: register-staged from the RAW (pre-BatchNorm) output of the previous layer, BatchNorm affine +
+//   * A operand: register-staged from the RAW (pre-BatchNorm) output of the previous layer, its BatchNorm affine +
 //     activation applied in registers as the tile is staged (these activations are <= 1 M elements, so the
-//     transform costs nothing), up to two sources (the U-Net concat [skip | up] of a ConvT's input);
-//   * the BatchNorm table of each source is merged in the prologue from the producer's per-tile statistics
-//     partials ({n, S1, S2, shift} chunks, the stc_bn_finalize format), in fp64 and in a fixed order, for the
-//     channels the block's K range reads -- every block that reads a channel derives bit-identical values, and
-//     a designated block per channel writes the mean / rstd / scale / shift tables (for the backward) and the
-//     running statistics (no grid-wide hand-off: the table is a pure function of the partials);
+//     transform costs nothing), up to two sources (the U-Net concat [skip | up] of a ConvT's input), each with the
+//     (scale, shift) table its producer wrote;
 //   * split-K without a second launch: every K-slice block stores its fp32 tile (accumulator order), takes a
 //     ticket on its tile (agent-scope release / acquire, cdna_hip_programming.md Guideline 16 counter form);
-//     the block drawing the last ticket sums the slices in split order (deterministic for any arrival order),
-//     writes the bf16 output through LDS as 16-byte NHWC rows and the tile's BatchNorm statistics partial
-//     (count, mean, M2 from the fp32 sums), and resets the ticket for the next launch;
+//     the block drawing the last ticket sums the slices in split order (deterministic for any arrival order) and
+//     writes the bf16 output through LDS as 16-byte NHWC rows;
+//   * the output's BatchNorm without a finalize launch: each tile's reducer stores its (count, mean, M2) per
+//     channel and takes a ticket on its column of tiles; the last of a column merges that column's partials in
+//     a fixed order (fp64, stc_bn_finalize's arithmetic) into the mean / rstd / scale / shift tables and the
+//     running statistics of those channels -- the next layer reads the table as its source's affine;
 //   * taps that read only padding for every row of the launch (1x1 grids: 4 of 16 conv taps, 1 of 4 ConvT taps
 //     per phase) are dropped from K on the host (their weights are never read).
 //
@@ -29,20 +28,30 @@
 
 namespace stc {
 
+#ifndef DEEP_REG  // 1: register-staged K loop (buffer loads -> VGPRs -> BatchNorm + activation -> ds_write); 0: LDS-DMA ring
+#define DEEP_REG 1
+#endif
+#ifndef DEEP_NSTG
+#define DEEP_NSTG (DEEP_REG ? 2 : 4)
+#endif
+
 struct DeepSrc {
   const bf16* p;
+  unsigned bytes;       // extent of the source buffer (LDS-DMA range check)
   long long bs;
   int rs, ps, co;
   int nc;               // K channels taken from this source
-  const float* part;    // statistics partials [nch][nc][4] (null: table / identity)
-  int nch;
-  const float* scale;   // ready table (part == null); null with part == null: identity
+  const float* scale;   // (scale, shift) table of its BatchNorm (null: identity)
   const float* shift;
+  float slope;          // activation after the affine
+  int mode;             // 0 pass-through, 1 affine + activation
+};
+
+struct DeepBN {  // the output's BatchNorm (train mode): tables + running statistics written by the column finishers
   const float* gamma;
   const float* beta;
-  float eps, momentum, slope;
-  int mode;             // 0 pass-through, 1 affine + activation
-  float* mean_o; float* rstd_o; float* scale_o; float* shift_o;  // designated outputs (null: none)
+  float eps, momentum;
+  float* mean_o; float* rstd_o; float* scale_o; float* shift_o;
   float* rmean; float* rvar; long long* nbt;
 };
 
@@ -60,52 +69,101 @@ struct DeepParams {
   long long o_bs;
   int o_rs, o_ps, o_co;
   float* slab;              // [tiles][ksplit][BM * BN]
-  unsigned* tickets;        // [tiles]
-  float* stats;             // [nphase * mtiles][N][4] or null
+  unsigned* tickets;        // [tiles] tile tickets, then [ntiles] column tickets
+  float* stats;             // [nphase * mtiles][N][4] tile statistics partials, or null (no BatchNorm)
+  DeepBN bn;
   int nphase, mtiles, ntiles, ksplit, kps;  // kps: K-steps (64) per split
   float inv_ghw, inv_gw;
+  unsigned long long* dbg;  // diagnostics (stc_deep_debug_next): per block 8 wall-clock stamps, or null
 };
 
-// BatchNorm merge of one channel from {n, S1, S2, shift} partials (stc_bn_finalize's two fp64 passes, serial order)
-__device__ __forceinline__ void deep_merge(const DeepSrc& s, int c, double& N, double& mu, double& M2) {
-  double n = 0, sm = 0;
-  for (int k = 0; k < s.nch; ++k) {
-    const float4 pp = *reinterpret_cast<const float4*>(s.part + ((long long)k * s.nc + c) * 4);
-    if (pp.x <= 0.f) continue;
-    n += pp.x;
-    sm += (double)pp.x * pp.w + (double)pp.y;
+// phase stamps of the diagnostic build-free timeline (scripts/deep_tune.py --phases): 0 start, 1 tables staged, 2 K
+// loop done, 3 split-K hand-off passed (reducers), 4 tile output stored, 5 column hand-off passed (finishers), 6 end
+#define DEEP_STAMP(i) \
+  do { if (p.dbg && threadIdx.x == 0) p.dbg[(long long)blockIdx.x * 8 + (i)] = wall_clock64(); } while (0)
+
+// one agent-scope hand-off to the last arriver of a counter (Guideline 16 counter form): every wave's stores
+// drained, lane 0 releases and adds; returns (to every thread) whether this block drew the last ticket, after
+// which its loads of the other blocks' data are behind an acquire
+__device__ __forceinline__ bool deep_last_arriver(unsigned* counter, unsigned total, unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = old == total - 1 ? 1u : 0u;
   }
-  mu = n > 0 ? sm / n : 0.0;
-  double m2 = 0;
-  for (int k = 0; k < s.nch; ++k) {
-    const float4 pp = *reinterpret_cast<const float4*>(s.part + ((long long)k * s.nc + c) * 4);
-    if (pp.x <= 0.f) continue;
-    const double nb = pp.x, s1 = pp.y, r = s1 / nb;
-    double q = (double)pp.z - s1 * r;
-    if (q < 0) q = 0;
-    const double d = (double)pp.w + r - mu;
-    m2 += q + nb * d * d;
+  __syncthreads();
+  const bool last = *flag != 0u;
+  if (last) {
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (left zero: the next launch)
+    }
+    __syncthreads();
   }
-  N = n;
-  M2 = m2;
+  return last;
 }
 
-// (scale, shift) of channel c of source s: the same arithmetic as bn_finalize_store
-__device__ __forceinline__ void deep_table(const DeepSrc& s, int c, float& sc, float& sh) {
-  if (s.part) {
-    double N, mu, M2;
-    deep_merge(s, c, N, mu, M2);
-    const double var = N > 0 ? M2 / N : 0.0;
-    const float rs = (float)(1.0 / sqrt(var + (double)s.eps));
-    const float g = s.gamma ? s.gamma[c] : 1.f, bt = s.beta ? s.beta[c] : 0.f;
-    sc = g * rs;
-    sh = bt - (float)mu * sc;
-  } else if (s.scale) {
-    sc = s.scale[c];
-    sh = s.shift[c];
+// The column finisher: channel n's batch statistics from the column's tile partials {count, 0, M2, mean} (one per
+// (phase, m tile), merged in chunk order, fp64, the two passes of stc_bn_finalize), then table + running statistics.
+__device__ __forceinline__ void deep_finalize(const DeepParams& p, int n, bool count_batch) {
+  const int nch = p.nphase * p.mtiles;
+  constexpr int G = 16;  // chunk loads in flight per group
+  double nt = 0, sm = 0;
+  for (int k0 = 0; k0 < nch; k0 += G) {
+    float4 v[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      v[u] = *reinterpret_cast<const float4*>(p.stats + ((long long)min(k0 + u, nch - 1) * p.N + n) * 4);
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      if (k0 + u >= nch || v[u].x <= 0.f) continue;
+      nt += v[u].x;
+      sm += (double)v[u].x * v[u].w + (double)v[u].y;
+    }
+  }
+  const double mu = nt > 0 ? sm / nt : 0.0;
+  double m2 = 0;
+  for (int k0 = 0; k0 < nch; k0 += G) {
+    float4 v[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      v[u] = *reinterpret_cast<const float4*>(p.stats + ((long long)min(k0 + u, nch - 1) * p.N + n) * 4);
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      if (k0 + u >= nch || v[u].x <= 0.f) continue;
+      const double nb = v[u].x, s1 = v[u].y, r = s1 / nb;
+      double q = (double)v[u].z - s1 * r;
+      if (q < 0) q = 0;
+      const double d = (double)v[u].w + r - mu;
+      m2 += q + nb * d * d;
+    }
+  }
+  bn_finalize_store(n, nt, mu, m2, p.bn.gamma, p.bn.beta, p.bn.rmean, p.bn.rvar, count_batch ? p.bn.nbt : nullptr,
+                    p.bn.momentum, p.bn.eps, p.bn.mean_o, p.bn.rstd_o, p.bn.scale_o, p.bn.shift_o);
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+// N 16-byte LDS reads, all in flight, then one wait (the results are complete when the statement ends)
+template <int N>
+__device__ __forceinline__ void lds_read_wait(u32x4 (&v)[N], const unsigned (&a)[N]) {
+  if constexpr (N == 1) {
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v[0]) : "v"(a[0]) : "memory");
+  } else if constexpr (N == 2) {
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0]), "=&v"(v[1]) : "v"(a[0]), "v"(a[1]) : "memory");
   } else {
-    sc = 1.f;
-    sh = 0.f;
+    static_assert(N == 4, "1, 2 or 4 chunks per thread");
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]) : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]) : "memory");
   }
 }
 
@@ -115,157 +173,201 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int AC = BM * 8 / 256, BC = BN * 8 / 256;  // 16-byte chunks per thread per K-step (A / B)
   constexpr int STAGE = (BM + BN) * 128;
+  constexpr int NSTG = DEEP_NSTG;                      // LDS-DMA ring: NSTG - 1 K-steps in flight
+  constexpr int AG = BM / 32, BG = BN / 32, P = AG + BG;  // 1 KiB DMA pieces per wave per K-step
   static_assert(FM >= 1 && FN >= 1 && AC >= 1 && BC >= 1, "tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // LDS: [stage 0][stage 1][table: scale[1024] shift[1024]] ; the epilogue reuses the stages
-  float* tsc = reinterpret_cast<float*>(smem + 2 * STAGE);
+  // LDS: [NSTG stages][table: scale[1024] shift[1024]][flag]; the epilogue reuses the stages
+  float* tsc = reinterpret_cast<float*>(smem + NSTG * STAGE);
   float* tsh = tsc + 1024;
 
+  DEEP_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  // XCD-aware: a tile's K slices on one XCD (its reducer then reads same-XCD slabs), consecutive tiles together
+  // XCD-aware: consecutive ids share an XCD (blocks b, b + 8, ... are dealt to one); the order is (phase, column of
+  // output channels, row tile, K slice) -- a tile's K slices on one XCD (its reducer reads same-XCD slabs) and the
+  // row tiles of one column of channels together, so each XCD streams its own slice of the weights (with the
+  // columns spread over the XCDs, every XCD's L2 fetched every weight: 8x the HBM traffic of the layer's weights)
   const int nwg = p.nphase * p.mtiles * p.ntiles * p.ksplit;
   int bid = blockIdx.x;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
+#ifndef DEEP_ORDER
+#define DEEP_ORDER 0
+#endif
   const int split = bid % p.ksplit;
-  const int tile = bid / p.ksplit;
-  const int nt = tile % p.ntiles;
-  const int mt = (tile / p.ntiles) % p.mtiles;
-  const int ph = tile / (p.ntiles * p.mtiles);
+  const int tq = bid / p.ksplit;  // (phase, column, row tile)
+#if DEEP_ORDER == 0
+  const int mt = tq % p.mtiles;
+  const int nt = (tq / p.mtiles) % p.ntiles;
+#else  // (experiment: row-major tiles, the column fastest)
+  const int nt = tq % p.ntiles;
+  const int mt = (tq / p.ntiles) % p.mtiles;
+#endif
+  const int ph = tq / (p.mtiles * p.ntiles);
+  const int tile = (ph * p.mtiles + mt) * p.ntiles + nt;  // (slab / ticket index)
   const int py = ph >> 1, px = ph & 1;
   const int m0 = mt * BM, n0 = nt * BN;
   const int cpt = p.Cin / 64;  // K-steps per tap
   const int nks = p.ntaps * cpt;
   const int ks0 = split * p.kps, ks1 = min(nks, ks0 + p.kps);
 
-  // ---- designated finalize outputs: block b owns channels [b * nc / nwg, (b + 1) * nc / nwg) of each source
-  auto designated = [&](const DeepSrc& s) {
-    if (!s.mean_o) return;
-    const int c0 = (int)((long long)blockIdx.x * s.nc / nwg), c1 = (int)((long long)(blockIdx.x + 1) * s.nc / nwg);
-    for (int c = c0 + tid; c < c1; c += 256) {
-      double N, mu, M2;
-      deep_merge(s, c, N, mu, M2);
-      bn_finalize_store(c, N, mu, M2, s.gamma, s.beta, s.rmean, s.rvar, nullptr, s.momentum, s.eps, s.mean_o, s.rstd_o,
-                        s.scale_o, s.shift_o);
-    }
-    if (blockIdx.x == 0 && tid == 0 && s.nbt) s.nbt[0] += 1;
-  };
-  designated(p.src[0]);
-  if (p.nsrc == 2) designated(p.src[1]);
-
-  // ---- prologue tables of the channels this block's K range reads (LDS, indexed by the K channel)
-  {
+  // ---- the sources' (scale, shift) tables of the channels this block's K range reads (LDS, indexed by K channel)
+  auto fill_tables = [&]() {
     const int a0 = ks0 % cpt, len = ks1 - ks0;
-    for (int kc = tid; kc < p.Cin; kc += 256) {
-      // K channel kc is read when some K-step in [ks0, ks1) has channel block kc / 64
-      if (((kc >> 6) - a0 + cpt) % cpt >= len) continue;
-      float sc, sh;
-      if (p.nsrc == 2 && kc >= p.src[0].nc) {
-        if (p.src[1].mode == 0) continue;
-        deep_table(p.src[1], kc - p.src[0].nc, sc, sh);
-      } else {
-        if (p.src[0].mode == 0) continue;
-        deep_table(p.src[0], kc, sc, sh);
+    float vs[4], vh[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // (all loads in flight, then the LDS writes: Cin <= 1024)
+      const int kc = tid + 256 * u;
+      vs[u] = 1.f;
+      vh[u] = 0.f;
+      if (kc >= p.Cin || ((kc >> 6) - a0 + cpt) % cpt >= len) continue;
+      const bool s1 = p.nsrc == 2 && kc >= p.src[0].nc;
+      const float* sc = s1 ? p.src[1].scale : p.src[0].scale;
+      const float* sh = s1 ? p.src[1].shift : p.src[0].shift;
+      const int c = kc - (s1 ? p.src[0].nc : 0);
+      if (sc) {
+        vs[u] = sc[c];
+        vh[u] = sh[c];
       }
-      tsc[kc] = sc;
-      tsh[kc] = sh;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int kc = tid + 256 * u;
+      if (kc < p.Cin) {
+        tsc[kc] = vs[u];
+        tsh[kc] = vh[u];
+      }
+    }
+  };
+
+  // ---- LDS-DMA lane roles: piece = 8 rows x 128 B; lane -> row (lane >> 3) of the piece, LDS slot lane & 7, which
+  // holds source chunk slot ^ (row & 7) (the swizzle every 16-row fragment read is conflict-free with).  Per DMA row,
+  // computed once: the element offset of its tap-0 source pixel in each source and the set of taps that read
+  // padding (bit t: K-tap index t, all bits for rows past M) -- a K-step then costs one add and a bit test per row.
+  const int prow = lane >> 3, pslot = lane & 7;
+  const int schunk = pslot ^ (prow & 7);  // (piece rows start at multiples of 8: row & 7 == prow)
+  const int GHW = p.GH * p.GW;
+  const unsigned long long tapl = ph == 0 ? p.tapl[0] : (ph == 1 ? p.tapl[1] : (ph == 2 ? p.tapl[2] : p.tapl[3]));
+  // tap t of the K order -> (row, column) offset of its source pixel from the tap-0 pixel's (conv: (+ky, +kx) from
+  // (2gy - 1, 2gx - 1); ConvT phase (py, px): (-ty, -tx) from (gy + py, gx + px))
+  auto tap_rc = [&](int tap, int& dy, int& dx) {
+    if (p.convt) { dy = -(tap >> 1); dx = -(tap & 1); }
+    else { dy = tap >> 2; dx = tap & 3; }
+  };
+  // the in-range K taps of a grid point (bit t set: tap t reads padding)
+  auto pad_taps = [&](bool in, int gy, int gx) {
+    unsigned inv = 0;
+    const int y0 = p.convt ? gy + py : 2 * gy - 1, x0 = p.convt ? gx + px : 2 * gx - 1;
+    for (int t = 0; t < p.ntaps; ++t) {
+      int dy, dx;
+      tap_rc((int)((tapl >> (4 * t)) & 15u), dy, dx);
+      const int iy = y0 + dy, ix = x0 + dx;
+      if (!(in && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)) inv |= 1u << t;
+    }
+    return inv;
+  };
+  unsigned a_off[2][AG], a_inv[AG];
+#pragma unroll
+  for (int g = 0; g < AG; ++g) {
+    const int m = m0 + (wave * AG + g) * 8 + prow;
+    const bool in = m < p.M;
+    const int mm = in ? m : 0;
+    const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
+    const int gy = fast_div(rem, p.GW, p.inv_gw), gx = rem - gy * p.GW;
+    const int y0 = p.convt ? gy + py : 2 * gy - 1, x0 = p.convt ? gx + px : 2 * gx - 1;
+    a_inv[g] = pad_taps(in, gy, gx);
+#pragma unroll
+    for (int si = 0; si < 2; ++si) {
+      const DeepSrc& q = si ? p.src[1] : p.src[0];
+      a_off[si][g] = (unsigned)(b * q.bs + (long long)y0 * q.rs + (long long)x0 * q.ps + q.co + 8 * schunk);
     }
   }
-
-  // ---- per-thread A rows (fixed over the K loop): GEMM row -> (image, grid y, grid x)
-  int a_row[AC], a_b[AC], a_gy[AC], a_gx[AC], a_cj[AC];
-  bool a_in[AC], a_pad[AC];
+  const __amdgpu_buffer_rsrc_t ra0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.src[0].p, (short)0, (int)p.src[0].bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.nsrc == 2 ? p.src[1].p : p.src[0].p), (short)0, (int)(p.nsrc == 2 ? p.src[1].bytes : p.src[0].bytes),
+      0x00020000);
+  const bf16* wph = p.w + (long long)ph * p.w_phase_stride;
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)wph, (short)0, (int)(p.w_phase_stride * 2), 0x00020000);
+  unsigned b_off[BG];
+#pragma unroll
+  for (int h = 0; h < BG; ++h) {
+    const int n = n0 + (wave * BG + h) * 8 + prow;
+    b_off[h] = n < p.N ? (unsigned)(n * p.w_taps * p.Cin + 8 * schunk) : OOB;
+  }
+  // K-step ks: K-tap index ti, packed tap, channel block cb, source
+  auto step_terms = [&](int ks, int& ti, int& tap, int& cb, bool& s1) {
+    ti = ks / cpt;
+    cb = (ks - ti * cpt) * 64;
+    tap = (int)((tapl >> (4 * ti)) & 15u);
+    s1 = p.nsrc == 2 && cb >= p.src[0].nc;
+  };
+  // the DMA pieces of K-step ks into stage st: A rows (padding and rows past M out of range: zeros), B rows
+  auto issue = [&](int ks, int st) {
+    int ti, tap, cb;
+    bool s1;
+    step_terms(ks, ti, tap, cb, s1);
+    int dy, dx;
+    tap_rc(tap, dy, dx);
+    const unsigned delta = (unsigned)((s1 ? p.src[1].rs : p.src[0].rs) * dy + (s1 ? p.src[1].ps : p.src[0].ps) * dx +
+                                      cb - (s1 ? p.src[0].nc : 0));
+    char* sA = smem + st * STAGE;
+#pragma unroll
+    for (int g = 0; g < AG; ++g) {
+      const unsigned off = ((s1 ? a_off[1][g] : a_off[0][g]) + delta) * 2u;
+      dma16(s1 ? ra1 : ra0, sA + (wave * AG + g) * 1024, off | (((a_inv[g] >> ti) & 1u) << 31));
+    }
+    char* sB = sA + BM * 128;
+    const unsigned bdelta = (unsigned)(tap * p.Cin + cb);
+#pragma unroll
+    for (int h = 0; h < BG; ++h) dma16(rw, sB + (wave * BG + h) * 1024, ((b_off[h] + bdelta) * 2u) | (b_off[h] & OOB));
+  };
+  // BatchNorm affine + activation of the staged A chunks of K-step ks (rows and taps that read padding stay zero)
+  int t_row[AC];
+  unsigned t_inv[AC];
 #pragma unroll
   for (int u = 0; u < AC; ++u) {
     const int ch = tid + u * 256;
-    a_row[u] = ch >> 3;
-    a_cj[u] = ch & 7;
-    const int m = m0 + a_row[u];
-    a_in[u] = m < p.M;
-    const int mm = a_in[u] ? m : 0;
-    const int GHW = p.GH * p.GW;
-    a_b[u] = fast_div(mm, GHW, p.inv_ghw);
-    const int rem = mm - a_b[u] * GHW;
-    a_gy[u] = fast_div(rem, p.GW, p.inv_gw);
-    a_gx[u] = rem - a_gy[u] * p.GW;
+    t_row[u] = ch >> 3;
+    const int m = m0 + t_row[u];
+    const bool in = m < p.M;
+    const int mm = in ? m : 0;
+    const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
+    const int gy = fast_div(rem, p.GW, p.inv_gw), gx = rem - gy * p.GW;
+    (void)b;
+    t_inv[u] = pad_taps(in, gy, gx);
   }
-  int b_row[BC], b_cj[BC];
-#pragma unroll
-  for (int u = 0; u < BC; ++u) {
-    const int ch = tid + u * 256;
-    b_row[u] = ch >> 3;
-    b_cj[u] = ch & 7;
-  }
-  const bf16* wph = p.w + (long long)ph * p.w_phase_stride;
-
-  // register ring: NS K-steps of A / B chunks in flight (one Regs per step, held by value: compile-time slots)
-  constexpr int NS = (AC + BC) <= 4 ? 3 : 2;
-  struct Regs {
-    uint4 a[AC], b[BC];
-    bool pad[AC];
-  };
-  const unsigned long long tapl = ph == 0 ? p.tapl[0] : (ph == 1 ? p.tapl[1] : (ph == 2 ? p.tapl[2] : p.tapl[3]));
-  auto load = [&](int ks) {
-    Regs r;
-    const int ti = ks / cpt, cb = (ks - ti * cpt) * 64;
-    const int tap = (int)((tapl >> (4 * ti)) & 15u);
-    int dy, dx;
-    if (p.convt) { dy = py - (tap >> 1); dx = px - (tap & 1); }
-    else { dy = (tap >> 2) - 1; dx = (tap & 3) - 1; }
-    // (source fields by a select, not a dynamic index into the parameter struct: no private copy of it)
-    const bool s1 = p.nsrc == 2 && cb >= p.src[0].nc;
-    const bf16* sp = s1 ? p.src[1].p : p.src[0].p;
-    const long long sbs = s1 ? p.src[1].bs : p.src[0].bs;
-    const int srs = s1 ? p.src[1].rs : p.src[0].rs, sps = s1 ? p.src[1].ps : p.src[0].ps;
-    const int c = (s1 ? p.src[1].co : p.src[0].co) + cb - (s1 ? p.src[0].nc : 0);
-#pragma unroll
-    for (int u = 0; u < AC; ++u) {
-      const int iy = p.convt ? a_gy[u] + dy : 2 * a_gy[u] + dy, ix = p.convt ? a_gx[u] + dx : 2 * a_gx[u] + dx;
-      const bool ok = a_in[u] && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW;
-      const int iyc = ok ? iy : 0, ixc = ok ? ix : 0;
-      // (clamped in-bounds address; the padding is zeroed when the chunk is staged -- a select on the loaded value
-      // here would wait for the load)
-      r.a[u] = *reinterpret_cast<const uint4*>(sp + (long long)a_b[u] * sbs + (long long)iyc * srs +
-                                               (long long)ixc * sps + c + 8 * a_cj[u]);
-      r.pad[u] = !ok;  // (padding: zero after the activation, not act(affine(0)))
-    }
-#pragma unroll
-    for (int u = 0; u < BC; ++u) {
-      const int n = min(n0 + b_row[u], p.N - 1);  // (rows past N: any row; their columns are not stored)
-      r.b[u] = *reinterpret_cast<const uint4*>(wph + ((long long)n * p.w_taps + tap) * p.Cin + cb + 8 * b_cj[u]);
-    }
-    return r;
-  };
-  auto stage_store = [&](int ks, const Regs r, char* st) {
-    const int cb = (ks % cpt) * 64;
-    const bool s1 = p.nsrc == 2 && cb >= p.src[0].nc;
-    const int mode = s1 ? p.src[1].mode : p.src[0].mode;
+  auto transform = [&](int ks, int st, bool& any) {
+    int ti, tap, cb;
+    bool s1;
+    step_terms(ks, ti, tap, cb, s1);
+    any = (s1 ? p.src[1].mode : p.src[0].mode) != 0;
+    if (!any) return;
     const float slope = s1 ? p.src[1].slope : p.src[0].slope;
+    char* sA = smem + st * STAGE;
+    unsigned addr[AC];
+    u32x4 v[AC];
+#pragma unroll
+    for (int u = 0; u < AC; ++u) addr[u] = lds_addr(sA + t_row[u] * 128 + ((tid + u * 256) & 7) * 16);
+    // (LDS reads and writes in inline asm: the compiler cannot tell this stage's slots from the LDS-DMA writes still
+    // in flight into the later stages, and would drain the whole ring -- vmcnt(0) -- before touching LDS here)
+    lds_read_wait<AC>(v, addr);
 #pragma unroll
     for (int u = 0; u < AC; ++u) {
-      uint4 v = r.pad[u] ? make_uint4(0u, 0u, 0u, 0u) : r.a[u];
-      if (mode && !r.pad[u]) {
-        const int kc = cb + 8 * a_cj[u];
-        const unsigned w[4] = {v.x, v.y, v.z, v.w};
-        unsigned o[4];
+      const int slot = (tid + u * 256) & 7, row = t_row[u];
+      const int kc = cb + 8 * (slot ^ (row & 7));
+      u32x4 o;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float lo = fmaf(__uint_as_float(w[q] << 16), tsc[kc + 2 * q], tsh[kc + 2 * q]);
-          const float hi = fmaf(__uint_as_float(w[q] & 0xffff0000u), tsc[kc + 2 * q + 1], tsh[kc + 2 * q + 1]);
-          o[q] = pack_bf16x2(act(lo, slope), act(hi, slope));
-        }
-        v = make_uint4(o[0], o[1], o[2], o[3]);
+      for (int e = 0; e < 4; ++e) {
+        const float lo = fmaf(__uint_as_float(v[u][e] << 16), tsc[kc + 2 * e], tsh[kc + 2 * e]);
+        const float hi = fmaf(__uint_as_float(v[u][e] & 0xffff0000u), tsc[kc + 2 * e + 1], tsh[kc + 2 * e + 1]);
+        o[e] = ((t_inv[u] >> ti) & 1u) ? 0u : pack_bf16x2(act(lo, slope), act(hi, slope));  // (padding stays zero)
       }
-      const int row = a_row[u];
-      *reinterpret_cast<uint4*>(st + row * 128 + ((a_cj[u] ^ (row & 7)) * 16)) = v;
-    }
-#pragma unroll
-    for (int u = 0; u < BC; ++u) {
-      const int row = b_row[u];
-      *reinterpret_cast<uint4*>(st + BM * 128 + row * 128 + ((b_cj[u] ^ (row & 7)) * 16)) = r.b[u];
+      asm volatile("ds_write_b128 %0, %1" ::"v"(addr[u]), "v"(o) : "memory");
     }
   };
 
@@ -296,36 +398,115 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
     }
   };
 
-  __syncthreads();  // (the prologue table)
-  if (ks0 < ks1) {
-    // (loads of steps past ks1 are clamped to the last step: harmless re-reads, no branch around a load)
-    Regs R0 = load(ks0), R1 = load(min(ks0 + 1, ks1 - 1)), R2;
-    if constexpr (NS == 3) R2 = load(min(ks0 + 2, ks1 - 1));
-    stage_store(ks0, R0, smem);
-    __syncthreads();
-    // step ks: its registers (slot (ks - ks0) % NS) were staged into LDS buffer (ks - ks0) & 1 by the previous step;
-    // refill the slot with step ks + NS, compute step ks, stage step ks + 1 into the other buffer, one barrier
-    auto step = [&](int base, auto dc, Regs& mine, const Regs& next) {
-      constexpr int d = decltype(dc)::value;
-      const int ks = base + d;
-      if (ks >= ks1) return;
-      mine = load(min(ks + NS, ks1 - 1));
-      compute(smem + ((ks - ks0) & 1) * STAGE);
-      if (ks + 1 < ks1) stage_store(ks + 1, next, smem + (((ks - ks0) & 1) ^ 1) * STAGE);
-      __syncthreads();
-    };
-    for (int base = ks0; base < ks1; base += NS) {
-      if constexpr (NS == 3) {
-        step(base, std::integral_constant<int, 0>{}, R0, R1);
-        step(base, std::integral_constant<int, 1>{}, R1, R2);
-        step(base, std::integral_constant<int, 2>{}, R2, R0);
-      } else {
-        step(base, std::integral_constant<int, 0>{}, R0, R1);
-        step(base, std::integral_constant<int, 1>{}, R1, R0);
-      }
+#if DEEP_REG
+  // ---- the K loop, register-staged: the A / B chunks of K-step s + 2 load into VGPRs while step s computes; at
+  // step s its chunks (loaded two steps earlier) get the sources' BatchNorm affine + activation in registers and go
+  // to LDS stage s & 1 with the DMA pieces' layout; one barrier per step (a stage is rewritten two steps after it was
+  // read, behind the barrier of the step between)
+  const int nsteps = ks1 - ks0;
+  struct Stg {
+    u32x4 a[AG], b[BG];
+  };
+  auto load = [&](int ks, Stg& r) {  // (a step past the block's K range loads zeros: the loop runs in pairs)
+    int ti, tap, cb;
+    bool s1;
+    step_terms(ks, ti, tap, cb, s1);
+    const unsigned past = ks >= ks1 ? OOB : 0u;
+    int dy, dx;
+    tap_rc(tap, dy, dx);
+    const unsigned delta = (unsigned)((s1 ? p.src[1].rs : p.src[0].rs) * dy + (s1 ? p.src[1].ps : p.src[0].ps) * dx +
+                                      cb - (s1 ? p.src[0].nc : 0));
+#pragma unroll
+    for (int g = 0; g < AG; ++g) {
+      const unsigned off = ((s1 ? a_off[1][g] : a_off[0][g]) + delta) * 2u;
+      r.a[g] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             s1 ? ra1 : ra0, off | (((a_inv[g] >> ti) & 1u) << 31) | past, 0, 0));
     }
+    const unsigned bdelta = (unsigned)(tap * p.Cin + cb);
+#pragma unroll
+    for (int h = 0; h < BG; ++h)
+      r.b[h] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, ((b_off[h] + bdelta) * 2u) | (b_off[h] & OOB) | past, 0, 0));
+  };
+  auto store = [&](int ks, const Stg& r, int st) {
+    int ti, tap, cb;
+    bool s1;
+    step_terms(ks, ti, tap, cb, s1);
+    char* sA = smem + st * STAGE;
+    char* sB = sA + BM * 128;
+    if ((s1 ? p.src[1].mode : p.src[0].mode) != 0) {
+      const float slope = s1 ? p.src[1].slope : p.src[0].slope;
+      const int kc = cb + 8 * schunk;
+      const float4 c0 = *reinterpret_cast<const float4*>(tsc + kc), c1 = *reinterpret_cast<const float4*>(tsc + kc + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(tsh + kc), h1 = *reinterpret_cast<const float4*>(tsh + kc + 4);
+      const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+      for (int g = 0; g < AG; ++g) {
+        // (padding stays zero: a mask, not a branch -- a branch here costs the loads' counted waits)
+        const unsigned keep = ((a_inv[g] >> ti) & 1u) | (ks >= ks1 ? 1u : 0u) ? 0u : 0xffffffffu;
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = fmaf(__uint_as_float(r.a[g][e] << 16), sc[2 * e], sh[2 * e]);
+          const float hi = fmaf(__uint_as_float(r.a[g][e] & 0xffff0000u), sc[2 * e + 1], sh[2 * e + 1]);
+          const float l2 = fmaxf(lo, 0.f) + slope * fminf(lo, 0.f), h2 = fmaxf(hi, 0.f) + slope * fminf(hi, 0.f);
+          o[e] = pack_bf16x2(l2, h2) & keep;
+        }
+        *reinterpret_cast<u32x4*>(sA + (wave * AG + g) * 1024 + lane * 16) = o;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < AG; ++g) *reinterpret_cast<u32x4*>(sA + (wave * AG + g) * 1024 + lane * 16) = r.a[g];
+    }
+#pragma unroll
+    for (int h = 0; h < BG; ++h) *reinterpret_cast<u32x4*>(sB + (wave * BG + h) * 1024 + lane * 16) = r.b[h];
+  };
+  Stg r0, r1;
+  load(ks0, r0);
+  load(ks0 + 1, r1);
+  fill_tables();
+  __syncthreads();  // (the tables)
+  DEEP_STAMP(1);
+  for (int s = 0; s < nsteps; s += 2) {  // (an odd count ends with one step of zeros)
+    store(ks0 + s, r0, 0);
+    load(ks0 + s + 2, r0);
+    __syncthreads();
+    compute(smem);
+    store(ks0 + s + 1, r1, 1);
+    load(ks0 + s + 3, r1);
+    __syncthreads();
+    compute(smem + STAGE);
   }
+#else
+  // ---- the K loop: an NSTG-stage LDS-DMA ring (steps ks0 .. ks0 + NSTG - 2 issued before the tables are staged);
+  // at step s wait for this wave's pieces of step s (counted vmcnt), barrier, the A transform (+ barrier), refill the
+  // stage step s - 1 read, MFMAs
+  const int nsteps = ks1 - ks0;
+#pragma unroll
+  for (int i = 0; i < NSTG - 1; ++i)
+    if (i < nsteps) issue(ks0 + i, i);
+  fill_tables();
+  __syncthreads();  // (the tables)
+  DEEP_STAMP(1);
+  int cur = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    wait_ahead<P>(min(NSTG - 2, nsteps - 1 - s));
+    __builtin_amdgcn_s_barrier();
+    bool tr;
+    transform(ks0 + s, cur, tr);
+    if (tr) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if (s + NSTG - 1 < nsteps) issue(ks0 + s + NSTG - 1, cur == 0 ? NSTG - 1 : cur - 1);
+    compute(smem + cur * STAGE);
+    cur = cur == NSTG - 1 ? 0 : cur + 1;
+  }
+#endif
+  __syncthreads();  // (the epilogue reuses the stages)
 
+  DEEP_STAMP(2);
   // ---- split-K: slab store, ticket, the last arriver reduces in split order
   unsigned* flag = reinterpret_cast<unsigned*>(tsh + 1024);  // (inside the one LDS array)
   if (p.ksplit > 1) {
@@ -335,22 +516,11 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j)
         *reinterpret_cast<floatx4*>(my + ((wave * FM + i) * FN + j) * 256 + lane * 4) = acc[i][j];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned old = __hip_atomic_fetch_add(p.tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = old == (unsigned)(p.ksplit - 1) ? 1u : 0u;
+    if (!deep_last_arriver(p.tickets + tile, (unsigned)p.ksplit, flag)) {
+      DEEP_STAMP(6);
+      return;
     }
-    __syncthreads();
-    if (*flag == 0u) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(p.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (next launch)
-    }
-    __syncthreads();
+    DEEP_STAMP(3);
     floatx4 sum[FM][FN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -390,7 +560,6 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
 
   // ---- epilogue: BatchNorm statistics of the tile (fp32 sums), bf16 tile through LDS -> 16-byte NHWC stores
   const int rq = 4 * (lane >> 4), cl = lane & 15;
-  const int GHW = p.GH * p.GW;
   if (p.stats) {
     float* red = reinterpret_cast<float*>(smem);  // [WM][BN][4] {S1, S2, shift, rows}
     int rows_w = min(TM, max(0, p.M - (m0 + wm * TM)));
@@ -444,8 +613,16 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
       *reinterpret_cast<float4*>(p.stats + (((long long)ph * p.mtiles + mt) * p.N + n) * 4) =
           make_float4(cnt, 0.f, m2, mean);
     }
+    // the last tile of this column of channels finalizes their BatchNorm (the next layer reads the table)
+    const long long ntiles_all = (long long)p.nphase * p.mtiles * p.ntiles;
+    if (deep_last_arriver(p.tickets + ntiles_all + nt, (unsigned)(p.nphase * p.mtiles), flag)) {
+      DEEP_STAMP(5);
+      for (int c = tid; c < BN; c += 256)
+        if (n0 + c < p.N) deep_finalize(p, n0 + c, nt == 0 && c == 0);
+    }
     __syncthreads();
   }
+  DEEP_STAMP(4);
   constexpr int PITCH = BN * 2 + 16;
   char* tl = smem;
 #pragma unroll
@@ -469,6 +646,7 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
     *reinterpret_cast<uint4*>(p.out + (long long)b * p.o_bs + (long long)oy * p.o_rs + (long long)ox * p.o_ps + p.o_co + n) =
         *reinterpret_cast<const uint4*>(tl + row * PITCH + cc * 16);
   }
+  DEEP_STAMP(6);
 }
 
 // ------------------------------------------------------------------------- host
@@ -537,7 +715,7 @@ static bool deep_plan(int convt, int B, int GH, int GW, int IH, int IW, int Cin,
 }
 
 // [two stages][scale / shift table of 1024 channels][flag]; the epilogue's tile and statistics area fit in the stages
-static size_t deep_lds(int BM, int BN) { return 2 * (size_t)(BM + BN) * 128 + 2 * 1024 * 4 + 16; }
+static size_t deep_lds(int BM, int BN) { return DEEP_NSTG * (size_t)(BM + BN) * 128 + 2 * 1024 * 4 + 16; }
 
 }  // namespace stc
 
@@ -547,18 +725,23 @@ static bool deep_shape_ok(int kind, int Cin, int Cout) {
   return (kind == STC_CONV_S2 || kind == STC_CONVT_S2) && Cin % 64 == 0 && Cin <= 1024 && Cout % 32 == 0 && Cout <= 2048;
 }
 
+static unsigned long long* g_deep_dbg = nullptr;  // (diagnostics: the next launch's stamps; one-shot)
+extern "C" int stc_deep_debug_next(void* stamps) {
+  g_deep_dbg = (unsigned long long*)stamps;
+  return 0;
+}
+
 extern "C" int stc_deep_conv_query(int kind, int B, int Hg, int Wg, int IH, int IW, int Cin, int Cout,
-                                   const int32_t* force_plan, int64_t* ws_bytes, int32_t* ntickets,
-                                   int32_t* stats_chunks, int32_t* plan_out) {
+                                   const int32_t* force_plan, int64_t* ws_bytes, int32_t* ntickets, int32_t* plan_out) {
   STC_REQUIRE(deep_shape_ok(kind, Cin, Cout), "stc_deep_conv_query: kind %d Cin %d Cout %d not supported", kind, Cin, Cout);
   DeepPlan pl;
   STC_REQUIRE(deep_plan(kind == STC_CONVT_S2, B, Hg, Wg, IH, IW, Cin, Cout, force_plan, pl),
               "stc_deep_conv_query: no plan for this shape");
   const int nph = kind == STC_CONVT_S2 ? 4 : 1;
   const long long tiles = (long long)nph * pl.mtiles * pl.ntiles;
-  if (ws_bytes) *ws_bytes = pl.ksplit > 1 ? tiles * pl.ksplit * pl.BM * pl.BN * 4 : 0;
-  if (ntickets) *ntickets = (int32_t)tiles;
-  if (stats_chunks) *stats_chunks = nph * pl.mtiles;
+  if (ws_bytes)
+    *ws_bytes = (pl.ksplit > 1 ? tiles * pl.ksplit * pl.BM * pl.BN * 4 : 0) + (long long)nph * pl.mtiles * Cout * 16;
+  if (ntickets) *ntickets = (int32_t)(tiles + pl.ntiles);
   if (plan_out) {
     plan_out[0] = pl.BM; plan_out[1] = pl.BN; plan_out[2] = pl.ksplit; plan_out[3] = pl.ntaps;
     plan_out[4] = (int32_t)(tiles * pl.ksplit);
@@ -567,8 +750,8 @@ extern "C" int stc_deep_conv_query(int kind, int B, int Hg, int Wg, int IH, int 
 }
 
 extern "C" int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src, const void* w_packed, int Cout,
-                             stc_view y, float* stats_part, int stats_chunks, const int32_t* force_plan,
-                             uint32_t* tickets, int ntickets, void* workspace, int64_t workspace_bytes, void* stream) {
+                             stc_view y, const stc_deep_bn* bn, const int32_t* force_plan, uint32_t* tickets,
+                             int ntickets, void* workspace, int64_t workspace_bytes, void* stream) {
   STC_REQUIRE(nsrc == 1 || nsrc == 2, "stc_deep_conv: 1 or 2 sources");
   const int IH = src[0].x.H, IW = src[0].x.W;
   int Cin = 0;
@@ -577,40 +760,46 @@ extern "C" int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src,
     STC_REQUIRE(v.p && v.H == IH && v.W == IW && v.cs == 1 && v.co % 8 == 0 && v.ps % 8 == 0 && v.rs % 8 == 0 &&
                     v.bs % 8 == 0 && ((uintptr_t)v.p & 15) == 0 && src[i].C % 64 == 0 && src[i].C > 0,
                 "stc_deep_conv: source %d must be a 16-byte NHWC bf16 view of a multiple of 64 channels", i);
+    STC_REQUIRE((src[i].scale == nullptr) == (src[i].shift == nullptr), "stc_deep_conv: scale / shift come together");
     Cin += src[i].C;
   }
   STC_REQUIRE(deep_shape_ok(kind, Cin, Cout), "stc_deep_conv: kind %d Cin %d Cout %d not supported", kind, Cin, Cout);
   const bool convt = kind == STC_CONVT_S2;
   const int GH = convt ? IH : y.H, GW = convt ? IW : y.W;
   if (convt) STC_REQUIRE(y.H == 2 * GH && y.W == 2 * GW, "stc_deep_conv: ConvT output %dx%d for input %dx%d", y.H, y.W, IH, IW);
-  else STC_REQUIRE(IH == 2 * GH || IH == 2 * GH - 1, "stc_deep_conv: conv input %d for output %d", IH, GH);
+  else STC_REQUIRE((IH == 2 * GH || IH == 2 * GH - 1) && (IW == 2 * GW || IW == 2 * GW - 1),
+                   "stc_deep_conv: conv input %dx%d for output %dx%d", IH, IW, GH, GW);
   STC_REQUIRE(y.cs == 1 && y.co % 8 == 0 && y.ps % 8 == 0 && y.rs % 8 == 0 && y.bs % 8 == 0 && ((uintptr_t)y.p & 15) == 0,
               "stc_deep_conv: output must be a 16-byte NHWC bf16 view");
   DeepPlan pl;
   STC_REQUIRE(deep_plan(convt, B, GH, GW, IH, IW, Cin, Cout, force_plan, pl), "stc_deep_conv: no plan for this shape");
   const int nph = convt ? 4 : 1;
   const long long tiles = (long long)nph * pl.mtiles * pl.ntiles;
-  STC_REQUIRE(tickets && ntickets >= tiles, "stc_deep_conv: %d tickets < %lld tiles", ntickets, tiles);
-  const long long need = pl.ksplit > 1 ? tiles * pl.ksplit * pl.BM * pl.BN * 4 : 0;
-  STC_REQUIRE(workspace_bytes >= need && (need == 0 || workspace), "stc_deep_conv: workspace %lld < %lld",
-              (long long)workspace_bytes, need);
-  if (stats_part) STC_REQUIRE(stats_chunks >= nph * pl.mtiles, "stc_deep_conv: stats chunks %d < %d", stats_chunks, nph * pl.mtiles);
+  STC_REQUIRE(tickets && ntickets >= tiles + pl.ntiles, "stc_deep_conv: %d tickets < %lld", ntickets, tiles + pl.ntiles);
+  const long long slab = pl.ksplit > 1 ? tiles * pl.ksplit * pl.BM * pl.BN * 4 : 0;
+  const long long need = slab + (long long)nph * pl.mtiles * Cout * 16;
+  STC_REQUIRE(workspace && workspace_bytes >= need, "stc_deep_conv: workspace %lld < %lld", (long long)workspace_bytes, need);
   DeepParams p{};
   p.nsrc = nsrc;
   for (int i = 0; i < nsrc; ++i) {
     const stc_deep_src& s = src[i];
     DeepSrc& d = p.src[i];
     d.p = (const bf16*)s.x.p; d.bs = s.x.bs; d.rs = (int)s.x.rs; d.ps = s.x.ps; d.co = s.x.co;
+    const long long bytes = ((long long)(B - 1) * s.x.bs + (long long)(s.x.H - 1) * s.x.rs + (long long)(s.x.W - 1) * s.x.ps +
+                             s.x.co + s.C) * 2;
+    STC_REQUIRE(bytes < (1ll << 31), "stc_deep_conv: source %d spans >= 2 GiB", i);
+    d.bytes = (unsigned)bytes;
     d.nc = s.C;
-    d.part = s.part; d.nch = s.nchunks;
-    STC_REQUIRE(!s.part || s.nchunks > 0, "stc_deep_conv: partials without chunks");
-    d.scale = s.scale; d.shift = s.shift; d.gamma = s.gamma; d.beta = s.beta;
-    d.eps = s.eps; d.momentum = s.momentum; d.slope = s.slope;
-    d.mode = (s.part || s.scale || s.slope != 1.f) ? 1 : 0;
-    d.mean_o = s.mean_out; d.rstd_o = s.rstd_out; d.scale_o = s.scale_out; d.shift_o = s.shift_out;
-    d.rmean = s.running_mean; d.rvar = s.running_var; d.nbt = (long long*)s.num_batches_tracked;
-    STC_REQUIRE(!d.mean_o || (s.part && d.rstd_o && d.scale_o && d.shift_o),
-                "stc_deep_conv: designated outputs need partials and all four tables");
+    d.scale = s.scale; d.shift = s.shift; d.slope = s.slope;
+    d.mode = (s.scale || s.slope != 1.f) ? 1 : 0;
+  }
+  if (bn) {
+    STC_REQUIRE(bn->mean_out && bn->rstd_out && bn->scale_out && bn->shift_out,
+                "stc_deep_conv: the output BatchNorm needs its four table outputs");
+    p.bn.gamma = bn->gamma; p.bn.beta = bn->beta; p.bn.eps = bn->eps; p.bn.momentum = bn->momentum;
+    p.bn.mean_o = bn->mean_out; p.bn.rstd_o = bn->rstd_out; p.bn.scale_o = bn->scale_out; p.bn.shift_o = bn->shift_out;
+    p.bn.rmean = bn->running_mean; p.bn.rvar = bn->running_var; p.bn.nbt = (long long*)bn->num_batches_tracked;
+    p.stats = (float*)((char*)workspace + slab);
   }
   p.convt = convt ? 1 : 0;
   p.IH = IH; p.IW = IW; p.GH = GH; p.GW = GW; p.M = B * GH * GW;
@@ -625,11 +814,13 @@ extern "C" int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src,
   p.w = (const bf16*)w_packed;
   p.w_taps = convt ? 4 : 16;
   p.w_phase_stride = (long long)Cout * p.w_taps * Cin;
+  STC_REQUIRE(p.w_phase_stride * 2 < (1ll << 31), "stc_deep_conv: weights");
   p.out = (bf16*)y.p; p.o_bs = y.bs; p.o_rs = (int)y.rs; p.o_ps = y.ps; p.o_co = y.co;
   p.slab = (float*)workspace;
   p.tickets = tickets;
-  p.stats = stats_part;
   p.nphase = nph; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.ksplit = pl.ksplit; p.kps = pl.kps;
+  p.dbg = g_deep_dbg;
+  g_deep_dbg = nullptr;
   const dim3 grid((unsigned)(tiles * pl.ksplit));
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = deep_lds(pl.BM, pl.BN);

@@ -356,16 +356,6 @@ def _gen_forward_deep(plan, sources, train, dt, cache, save, kd):
     def conv_bn(kind, xv, cin_, w, cout, yv, bn):
         return _conv_bn(kind, B, xv, cin_, w, cout, yv, dt, bn, train, dev)
 
-    def new_tables(C):
-        """(2, C) scale/shift table + (mean, rstd) tensors a deep launch writes as a source's designated outputs."""
-        t = torch.empty((2, C), dtype=torch.float32, device=dev)
-        return t, (torch.empty(C, dtype=torch.float32, device=dev), torch.empty(C, dtype=torch.float32, device=dev))
-
-    def eval_table(bn, C):
-        t = torch.empty((2, C), dtype=torch.float32, device=dev)
-        ops.bn_eval_table(C, bn, t[0], t[1])
-        return t
-
     # ---- down path: levels < kd as gen_forward
     w0 = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_FWD, co[0], cin_pad, dt)
     if ops.conv_act(L.CONV_S2, B, L.nhwc_view(xin), cin_pad, w0, co[0], L.nhwc_view(ad[0]), LRELU, dt,
@@ -381,54 +371,44 @@ def _gen_forward_deep(plan, sources, train, dt, cache, save, kd):
                                     plan.bnd[k])
         ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]), LRELU,
                      L.nhwc_view(cr[k], 0), 0.0)
-    # ---- deep levels: conv_k reads ad[kd - 1] (materialised above), then the raw rd[k - 1] + its statistics
-    P, Pu = {}, {}  # statistics partials (train) of rd[k] / rq[k]: (tensor, chunks)
-
-    def bn_src(xv, C, k, up, slope, designated):
-        """Source of a deep launch: raw level-k output (down: rd[k] / BN_d[k]; up: rq[k] / BN_u[k])."""
+    # ---- deep levels: conv_k reads ad[kd - 1] (materialised above), then the raw rd[k - 1] through BN_d[k - 1]'s
+    # table, which conv_{k-1}'s launch wrote (train) or bn_eval_table made (eval); convT_k likewise
+    def table_of(k, up):
+        """(BN table, deep_bn descriptor for the launch that produces the level's raw output (train) or None)."""
         bn = plan.bnu[k] if up else plan.bnd[k]
+        C = bn.num_features
         tabs, sts = (tab_u, st_u) if up else (tab_d, st_d)
+        t = torch.empty((2, C), dtype=torch.float32, device=dev)
+        tabs[k] = t
         if not train:
-            if k not in tabs:
-                tabs[k] = eval_table(bn, C)
-            return ops.deep_src(xv, C, table=(tabs[k][0], tabs[k][1]), slope=slope)
-        part, nch = (Pu if up else P)[k]
-        outs = None
-        if designated:
-            tabs[k], sts[k] = new_tables(C)
-            outs = (sts[k][0], sts[k][1], tabs[k][0], tabs[k][1])
-        return ops.deep_src(xv, C, part=part, nch=nch, bn=bn, slope=slope, outs=outs, running=designated)
+            ops.bn_eval_table(C, bn, t[0], t[1])
+            sts[k] = None
+            return None
+        sts[k] = (torch.empty(C, dtype=torch.float32, device=dev), torch.empty(C, dtype=torch.float32, device=dev))
+        return ops.deep_bn(bn, t, sts[k])
 
     for k in range(kd, Lv):
         wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
         if k == kd:
             src = ops.deep_src(L.nhwc_view(ad[k - 1]), co[k - 1])
-        else:  # the first reader of rd[k - 1] writes BN_d[k - 1]'s tables and running statistics
-            src = bn_src(L.nhwc_view(rd[k - 1]), co[k - 1], k - 1, False, LRELU, True)
-        stats = train and k < Lv - 1  # (the innermost level has no down-norm, STCGAN/networks.py:118-124)
-        part = ops.deep_conv(L.CONV_S2, B, [src], wk, co[k], L.nhwc_view(rd[k]), tickets, ("c", k), stats=stats)
-        if stats:
-            P[k] = part
+        else:
+            src = ops.deep_src(L.nhwc_view(rd[k - 1]), co[k - 1], table=(tab_d[k - 1][0], tab_d[k - 1][1]), slope=LRELU)
+        # (the innermost level has no down-norm, STCGAN/networks.py:118-124)
+        dbn = table_of(k, False) if k < Lv - 1 else None
+        ops.deep_conv(L.CONV_S2, B, [src], wk, co[k], L.nhwc_view(rd[k]), tickets, ("c", k), bn=dbn)
     # ---- deep up path: convT_k reads [ReLU(BN_d[k](rd[k])) | ReLU(BN_u[k + 1](rq[k + 1]))] (innermost: ReLU(rd))
     for k in range(Lv - 1, kd - 1, -1):
         wt = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_FWD, co[k - 1], cin_t(k), dt)
         if k == Lv - 1:
             srcs = [ops.deep_src(L.nhwc_view(rd[k]), co[k], slope=0.0)]
         else:
-            srcs = [bn_src(L.nhwc_view(rd[k]), co[k], k, False, 0.0, False),
-                    bn_src(L.nhwc_view(rq[k + 1], 0, *S[k + 1]), co[k], k + 1, True, 0.0, True)]
-        part = ops.deep_conv(L.CONVT_S2, B, srcs, wt, co[k - 1], L.nhwc_view(rq[k]), tickets, ("t", k), stats=train)
-        if train:
-            Pu[k] = part
-    # ---- BN_u[kd] (read by the per-layer convT_{kd-1}): finalize + apply into cr[kd - 1]'s up half
+            srcs = [ops.deep_src(L.nhwc_view(rd[k]), co[k], table=(tab_d[k][0], tab_d[k][1]), slope=0.0),
+                    ops.deep_src(L.nhwc_view(rq[k + 1], 0, *S[k + 1]), co[k], table=(tab_u[k + 1][0], tab_u[k + 1][1]),
+                                 slope=0.0)]
+        ops.deep_conv(L.CONVT_S2, B, srcs, wt, co[k - 1], L.nhwc_view(rq[k]), tickets, ("t", k), bn=table_of(k, True))
+    # ---- BN_u[kd] (table from convT_kd) applied into cr[kd - 1]'s up half, read by the per-layer convT_{kd-1}
     C = co[kd - 1]
-    t = torch.empty((2, C), dtype=torch.float32, device=dev)
-    if train:
-        st_u[kd] = ops.bn_finalize_part(Pu[kd][0], Pu[kd][1], C, plan.bnu[kd], t[0], t[1])
-    else:
-        ops.bn_eval_table(C, plan.bnu[kd], t[0], t[1])
-        st_u[kd] = None
-    tab_u[kd] = t
+    t = tab_u[kd]
     ops.bn_apply(B, L.nhwc_view(rq[kd], 0, *S[kd]), C, dt, (t[0], t[1]), L.nhwc_view(cr[kd - 1], C), 0.0)
     # ---- the deep levels' activations for the backward's weight gradients (side stream, joined at the end)
     side = None

@@ -305,77 +305,77 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
 
 
 def deep_query(kind, B, gh, gw, ih, iw, cin, cout, force=None):
-    """(workspace bytes, tickets, statistics chunks, plan) of stc_deep_conv for these shapes."""
+    """(workspace bytes, tickets, plan) of stc_deep_conv for these shapes."""
     key = ("dq", kind, B, gh, gw, ih, iw, cin, cout, None if force is None else tuple(force))
     r = _MEMO.get(key)
     if r is None:
-        ws, nt, nch = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
+        ws, nt = ctypes.c_int64(), ctypes.c_int32()
         po = (ctypes.c_int32 * 5)()
         fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
-        check(lib().stc_deep_conv_query(kind, B, gh, gw, ih, iw, cin, cout, fp, ctypes.byref(ws), ctypes.byref(nt),
-                                        ctypes.byref(nch), po), "stc_deep_conv_query")
-        r = _MEMO[key] = (ws.value, nt.value, nch.value, tuple(po))
+        check(lib().stc_deep_conv_query(kind, B, gh, gw, ih, iw, cin, cout, fp, ctypes.byref(ws), ctypes.byref(nt), po),
+              "stc_deep_conv_query")
+        r = _MEMO[key] = (ws.value, nt.value, tuple(po))
     return r
 
 
-def deep_src(xv, C, part=None, nch=0, table=None, bn=None, slope=1.0, outs=None, running=False):
-    """One stc_deep_conv source: the view ``xv`` (C channels), normalised by its BatchNorm ``bn`` from the statistics
-    partials ``part`` (or a ready (scale, shift) ``table``; neither: identity), then the activation ``slope``.
-    outs = (mean, rstd, scale, shift) tensors this launch writes (and, with ``running``, bn's running statistics)."""
+def deep_src(xv, C, table=None, slope=1.0):
+    """One stc_deep_conv source: the view ``xv`` (C channels), through its BatchNorm's (scale, shift) ``table``
+    (None: identity) and the activation ``slope``."""
     s = L.DeepSrc()
     s.x = xv
     s.C = C
     s.slope = float(slope)
-    keep = [xv]
-    if part is not None:
-        s.part, s.nchunks = part.data_ptr(), nch
-        s.gamma, s.beta = bn.weight.data_ptr(), bn.bias.data_ptr()
-        s.eps = float(bn.eps)
-        s.momentum = float(bn.momentum if bn.momentum is not None else BN_MOMENTUM)
-        keep += [part, bn.weight, bn.bias]
-    elif table is not None:
+    s._keep = [xv]
+    if table is not None:
         s.scale, s.shift = table[0].data_ptr(), table[1].data_ptr()
-        keep += list(table)
-    if outs is not None:
-        s.mean_out, s.rstd_out, s.scale_out, s.shift_out = (t.data_ptr() for t in outs)
-        keep += list(outs)
-        if running:
-            s.running_mean, s.running_var = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
-            s.num_batches_tracked = bn.num_batches_tracked.data_ptr()
-    s._keep = keep
+        s._keep += list(table)
     return s
 
 
-def deep_conv(kind, B, srcs, w_packed, cout, yv, tickets_cache, key, stats=True, force=None):
-    """The U-Net's innermost levels in one launch per layer (stc_deep_conv): returns (statistics partials, chunks)
-    of the output (None, 0 without statistics).  ``tickets_cache[key]``: the launch site's persistent tile tickets."""
+def deep_bn(bn, table, stats, running=True):
+    """The output BatchNorm of a stc_deep_conv launch: it writes ``table`` ((2, C): scale, shift) and ``stats``
+    ((mean, rstd)), and (``running``) updates bn's running statistics and batch count."""
+    d = L.DeepBN()
+    d.gamma, d.beta = bn.weight.data_ptr(), bn.bias.data_ptr()
+    d.eps = float(bn.eps)
+    d.momentum = float(bn.momentum if bn.momentum is not None else BN_MOMENTUM)
+    d.mean_out, d.rstd_out = stats[0].data_ptr(), stats[1].data_ptr()
+    d.scale_out, d.shift_out = table[0].data_ptr(), table[1].data_ptr()
+    if running:
+        d.running_mean, d.running_var = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
+        d.num_batches_tracked = bn.num_batches_tracked.data_ptr()
+    d._keep = [bn.weight, bn.bias, table, stats]
+    return d
+
+
+def deep_conv(kind, B, srcs, w_packed, cout, yv, tickets_cache, key, bn=None, force=None):
+    """The U-Net's innermost levels in one launch per layer (stc_deep_conv); ``bn``: a deep_bn() descriptor of the
+    output's BatchNorm (train mode) or None.  ``tickets_cache[key]``: the launch site's persistent tile tickets."""
     dev = w_packed.device
     ih, iw = srcs[0].x.H, srcs[0].x.W
     gh, gw = (ih, iw) if kind == L.CONVT_S2 else (yv.H, yv.W)
     cin = sum(s.C for s in srcs)
-    nbytes, ntk, nch, _ = deep_query(kind, B, gh, gw, ih, iw, cin, cout, force)
+    nbytes, ntk, plan = deep_query(kind, B, gh, gw, ih, iw, cin, cout, force)
     tk = tickets_cache.get(key)
     if tk is None or tk.numel() < ntk:
         tk = tickets_cache[key] = torch.zeros(max(ntk, 1), dtype=torch.int32, device=dev)
     ws, nb = _ws(nbytes, dev)
-    part = torch.empty((nch, cout, 4), dtype=torch.float32, device=dev) if stats else None
     arr = (L.DeepSrc * len(srcs))(*srcs)
     fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
     timer = _timer
     if timer is not None:
         e0, e1 = _main_events()
-    rc = lib().stc_deep_conv(kind, B, len(srcs), arr, ptr(w_packed), cout, yv, ptr(part), nch if stats else 0, fp,
-                             ptr(tk), tk.numel(), ptr(ws), nb, stream())
+    rc = lib().stc_deep_conv(kind, B, len(srcs), arr, ptr(w_packed), cout, yv,
+                             ctypes.byref(bn) if bn is not None else None, fp, ptr(tk), tk.numel(), ptr(ws), nb,
+                             stream())
     if timer is not None:
         _disarm()
     check(rc, "stc_deep_conv")
     if timer is not None:
-        _, _, _, plan = deep_query(kind, B, gh, gw, ih, iw, cin, cout, force)
         outs = B * gh * gw * (4 if kind == L.CONVT_S2 else 1)
         taps = 4 if kind == L.CONVT_S2 else 16  # (the conv's FLOPs, as every other launch counts them)
         timer.append((f"deep_conv_kernel<{plan[0]}, {plan[1]}>", True, 2.0 * outs * cout * taps * cin, e0, e1,
                       f"{['conv_s2', 'conv_s1', 'convT', 's1_dgrad'][kind]} B{B} grid{gh}x{gw} cin{cin} cout{cout}"))
-    return part, (nch if stats else 0)
 
 
 def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True):

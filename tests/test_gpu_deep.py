@@ -39,23 +39,15 @@ def _bn(C, g):
     return bn
 
 
-def _partials(x):
-    """Statistics partials of x (NHWC bf16) in the stc_conv_fwd_ex format, from stc_chan_stats."""
-    from stcgan_amd import _lib as L, ops
-    B, H, W, C = x.shape
-    nch = ops.stats_chunks(B, H, W)
-    part = torch.empty((nch, C, 4), dtype=torch.float32, device=DEV)
-    L.check(L.lib().stc_chan_stats(L.BF16, B, L.nhwc_view(x), C, L.ptr(part), nch, L.stream()), "stc_chan_stats")
-    return part, nch
-
-
-CASES = [  # kind, B, input H, W, Cin per source, Cout, sources with BN partials
-    ("conv", 32, 8, 8, [512], 512, True),       # e5-shaped (16 -> 8x8 -> 4x4 at 256x256)
+CASES = [  # kind, B, input H, W, Cin per source, Cout, sources with a BatchNorm table
+    ("conv", 32, 8, 8, [512], 512, False),      # e5-shaped (16 -> 8x8 -> 4x4 at 256x256): the activation as input
     ("conv", 32, 4, 4, [512], 512, True),       # e6
     ("conv", 32, 2, 2, [512], 512, True),       # e7 (1x1 output: 4 of 16 taps kept)
     ("convT", 32, 1, 1, [512], 512, False),     # d7 (1x1 input: one tap per phase)
     ("convT", 32, 2, 2, [512, 512], 512, True),  # d6 (concat of two sources)
     ("convT", 32, 4, 4, [512, 512], 512, True),  # d5
+    ("conv", 32, 16, 16, [512], 512, False),    # e4 / d4 shapes
+    ("convT", 32, 8, 8, [512, 512], 512, True),
     ("conv", 8, 15, 20, [256], 512, True),      # 480x640 shapes (odd input)
     ("convT", 8, 4, 5, [512, 512], 512, True),
     ("conv", 2, 4, 4, [64], 64, True),          # ngf=8 widths
@@ -66,37 +58,27 @@ CASES = [  # kind, B, input H, W, Cin per source, Cout, sources with BN partials
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-B{c[1]}-{c[2]}x{c[3]}-{'+'.join(map(str, c[4]))}" for c in CASES])
 def test_deep_conv_vs_torch(case):
     from stcgan_amd import _lib as L, ops
-    kind, B, H, W, cins, cout, use_part = case
+    kind, B, H, W, cins, cout, use_tab = case
     g = torch.Generator(device=DEV)
     g.manual_seed(H * 100 + W + sum(cins))
     cin = sum(cins)
     convt = kind == "convT"
-    # raw sources (bf16 NHWC), their BNs and activations
+    # raw sources (bf16 NHWC) with a (scale, shift) table and an activation each
     raws = [(torch.randn((B, H, W, c), generator=g, device=DEV) * 2 + 0.3).to(torch.bfloat16) for c in cins]
-    bns = [_bn(c, g) for c in cins]
-    slopes = [0.2, 0.0][:len(cins)] if not convt else [0.0] * len(cins)
-    srcs, srcs2, acts, outs = [], [], [], []
-    for i, (r, bn, sl) in enumerate(zip(raws, bns, slopes)):
+    slopes = ([0.2] if not convt else [0.0, 0.0])[:len(cins)]
+    srcs, acts = [], []
+    for r, sl in zip(raws, slopes):
+        C = r.shape[3]
         x = _nchw(r)
-        if use_part:
-            part, nch = _partials(r)
-            srcs2.append(ops.deep_src(L.nhwc_view(r), cins[i], part=part, nch=nch, bn=bn, slope=sl))
-            mean = x.mean(dim=(0, 2, 3))
-            var = x.var(dim=(0, 2, 3), unbiased=False)
-            tab_o = torch.empty((2, cins[i]), device=DEV)
-            st_o = (torch.empty(cins[i], device=DEV), torch.empty(cins[i], device=DEV))
-            o = (st_o[0], st_o[1], tab_o[0], tab_o[1])
-            outs.append((o, mean, var, bn, bn.running_mean.clone(), bn.running_var.clone()))
-            srcs.append(ops.deep_src(L.nhwc_view(r), cins[i], part=part, nch=nch, bn=bn, slope=sl, outs=o,
-                                     running=True))
-            sc = bn.weight.detach() / torch.sqrt(var + bn.eps)
-            sh = bn.bias.detach() - mean * sc
+        if use_tab:
+            sc = torch.rand(C, generator=g, device=DEV) + 0.5
+            sh = torch.rand(C, generator=g, device=DEV) - 0.5
+            srcs.append(ops.deep_src(L.nhwc_view(r), C, table=(sc, sh), slope=sl))
+            n = torch.addcmul(sh[None, :, None, None], x, sc[None, :, None, None])  # (one rounding, as fmaf)
         else:
-            srcs.append(ops.deep_src(L.nhwc_view(r), cins[i], slope=sl))
-            srcs2.append(ops.deep_src(L.nhwc_view(r), cins[i], slope=sl))
-            sc, sh = torch.ones(cins[i], device=DEV), torch.zeros(cins[i], device=DEV)
-        n = x * sc[None, :, None, None] + sh[None, :, None, None]
-        acts.append(F.leaky_relu(n, sl).to(torch.bfloat16).float())
+            srcs.append(ops.deep_src(L.nhwc_view(r), C, slope=sl if convt else 1.0))
+            n = x
+        acts.append(F.leaky_relu(n, sl if (use_tab or convt) else 1.0).to(torch.bfloat16).float())
     a = torch.cat(acts, 1)
     w = (torch.randn((cin, cout, 4, 4) if convt else (cout, cin, 4, 4), generator=g, device=DEV) * 0.02)
     wq = w.to(torch.bfloat16).float()
@@ -110,32 +92,35 @@ def test_deep_conv_vs_torch(case):
         kd = L.CONV_S2
     Ho, Wo = ref.shape[2], ref.shape[3]
     y = torch.empty((B, Ho, Wo, cout), dtype=torch.bfloat16, device=DEV)
+    bn = _bn(cout, g)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    tab = torch.empty((2, cout), device=DEV)
+    st = (torch.empty(cout, device=DEV), torch.empty(cout, device=DEV))
     tickets = {}
-    part, nch = ops.deep_conv(kd, B, srcs, wp, cout, L.nhwc_view(y), tickets, "k")
+    ops.deep_conv(kd, B, srcs, wp, cout, L.nhwc_view(y), tickets, "k", bn=ops.deep_bn(bn, tab, st))
     torch.cuda.synchronize()
     assert int(tickets["k"].abs().sum()) == 0  # (left zero for the next launch)
     got = _nchw(y)
     assert _rel(got, ref) < 1e-2
     assert float((got - ref).abs().max()) <= 0.02 * float(ref.abs().max()) + 1e-6
-    # the output's statistics partials merge to the fp32 output's batch statistics
-    t = torch.empty((2, cout), device=DEV)
-    bn_o = _bn(cout, g)
-    mean_o, rstd_o = ops.bn_finalize_part(part, nch, cout, bn_o, t[0], t[1], update_running=False)
-    assert _rel(mean_o, ref.mean(dim=(0, 2, 3))) < 2e-3
-    assert _rel(rstd_o, torch.rsqrt(ref.var(dim=(0, 2, 3), unbiased=False) + 1e-5)) < 2e-3
-    # designated outputs: tables and running statistics of each source's BatchNorm
-    for (o, mean, var, bn, rm0, rv0) in outs:
-        assert _rel(o[0], mean) < 1e-5 and _rel(o[1], torch.rsqrt(var + bn.eps)) < 1e-5
-        assert _rel(o[2], bn.weight.detach() * torch.rsqrt(var + bn.eps)) < 1e-5
-        n = B * H * W
-        assert torch.allclose(bn.running_mean, 0.9 * rm0 + 0.1 * mean, rtol=1e-5, atol=1e-6)
-        assert torch.allclose(bn.running_var, 0.9 * rv0 + 0.1 * var * n / (n - 1), rtol=1e-4, atol=1e-6)
-        assert int(bn.num_batches_tracked) == 1
-    # bit-identical on a second launch (fixed split order, whatever the arrival order)
+    # the output's BatchNorm: batch statistics of the fp32 conv output, table, running statistics, batch count
+    mean, var = ref.mean(dim=(0, 2, 3)), ref.var(dim=(0, 2, 3), unbiased=False)
+    assert _rel(st[0], mean) < 2e-3
+    assert _rel(st[1], torch.rsqrt(var + bn.eps)) < 2e-3
+    assert _rel(tab[0], bn.weight.detach() * torch.rsqrt(var + bn.eps)) < 2e-3
+    assert _rel(tab[1], bn.bias.detach() - mean * tab[0]) < 2e-3
+    n = B * Ho * Wo
+    assert torch.allclose(bn.running_mean, 0.9 * rm0 + 0.1 * mean, rtol=2e-3, atol=1e-5)
+    assert torch.allclose(bn.running_var, 0.9 * rv0 + 0.1 * var * n / (n - 1), rtol=2e-3, atol=1e-5)
+    assert int(bn.num_batches_tracked) == 1
+    # bit-identical on a second launch (fixed split and merge orders, whatever the arrival order)
     y2 = torch.empty_like(y)
-    part2, _ = ops.deep_conv(kd, B, srcs2, wp, cout, L.nhwc_view(y2), tickets, "k")
+    tab2 = torch.empty_like(tab)
+    st2 = (torch.empty_like(st[0]), torch.empty_like(st[1]))
+    ops.deep_conv(kd, B, srcs, wp, cout, L.nhwc_view(y2), tickets, "k", bn=ops.deep_bn(bn, tab2, st2, running=False))
     torch.cuda.synchronize()
-    assert torch.equal(y, y2) and torch.equal(part, part2)
+    assert torch.equal(y, y2) and torch.equal(tab, tab2) and torch.equal(st[0], st2[0])
+    assert int(tickets["k"].abs().sum()) == 0
 
 
 @pytest.mark.parametrize("ngf,B", [(64, 8), (8, 4)])
