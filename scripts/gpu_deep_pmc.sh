@@ -1,12 +1,15 @@
 #!/bin/bash
-# stc_deep_conv PMC passes (one launch set of scripts/deep_tune.py --phases --only $1): L2 hits / misses, HBM fetch
+# stc_deep_conv PMC passes over scripts/deep_tune.py --phases --only $1 (one pass per counter group)
 set -o pipefail
-O=gpurun_out/deep_pmc
-mkdir -p $O
-cd /tmp && export TMPDIR=/tmp
+O=gpurun_out/deep_pmc_${1:-e5}
 R=$GRAFT_REPO_ROOT
-timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $R/$O/trace -o run -- python3 $R/scripts/deep_tune.py --phases --only ${1:-e5} > $R/$O/trace.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/$O/p1 -o run -- python3 $R/scripts/deep_tune.py --phases --only ${1:-e5} > $R/$O/p1.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $R/$O/p2 -o run -- python3 $R/scripts/deep_tune.py --phases --only ${1:-e5} > $R/$O/p2.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE -d $R/$O/p3 -o run -- python3 $R/scripts/deep_tune.py --phases --only ${1:-e5} > $R/$O/p3.log 2>&1 || exit 1
+mkdir -p $R/$O
+cd /tmp && export TMPDIR=/tmp
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS" \
+           "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_WAVES" \
+           "SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_FLAT SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_SENDMSG"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $grp -d $R/$O/p$i -o run -- python3 $R/scripts/deep_tune.py --phases --only ${1:-e5} > $R/$O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $R/$O/p$i.log; }
+done
 echo done

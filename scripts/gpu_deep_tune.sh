@@ -13,7 +13,9 @@ if [ -z "$NO_SWEEP" ]; then
   timeout -k 10 500 python -u scripts/deep_tune.py ${TUNE_ARGS} > $O/tune.log 2>&1 || { tail -5 $O/tune.log; exit 1; }
   grep "==" $O/tune.log
 fi
-for d in 0 1; do
-  timeout -k 10 240 python scripts/fwd_timeline.py --reps 5 --deep $d > $O/fwd_deep$d.json 2> $O/fwd_deep$d.err || exit 1
-  echo "deep=$d $(cat $O/fwd_deep$d.json)"
+timeout -k 10 240 python scripts/fwd_timeline.py --reps 5 --deep 0 > $O/fwd_deep0.json 2> $O/fwd_deep0.err || exit 1
+echo "deep=0 $(cat $O/fwd_deep0.json)"
+for lv in ${LEVELS:-2 3}; do
+  timeout -k 10 240 python scripts/fwd_timeline.py --reps 5 --deep 1 --levels $lv > $O/fwd_deep1_l$lv.json 2> $O/fwd_deep1_l$lv.err || exit 1
+  echo "deep=1 levels=$lv $(cat $O/fwd_deep1_l$lv.json)"
 done

@@ -28,16 +28,13 @@
 
 namespace stc {
 
-#ifndef DEEP_REG  // 1: register-staged K loop (buffer loads -> VGPRs -> BatchNorm + activation -> ds_write); 0: LDS-DMA ring
-#define DEEP_REG 1
-#endif
-#ifndef DEEP_NSTG
-#define DEEP_NSTG (DEEP_REG ? 2 : 4)
+#ifndef DEEP_RING  // K-steps of register-staged loads in flight
+#define DEEP_RING 2
 #endif
 
 struct DeepSrc {
   const bf16* p;
-  unsigned bytes;       // extent of the source buffer (LDS-DMA range check)
+  unsigned bytes;       // extent of the source buffer (buffer-load range check: padding rows read zeros)
   long long bs;
   int rs, ps, co;
   int nc;               // K channels taken from this source
@@ -61,6 +58,7 @@ struct DeepParams {
   int IH, IW;               // A extent (both sources)
   int GH, GW, M;            // GEMM grid (conv: output, ConvT: input), rows per phase
   int N, Cin, ntaps;        // K = ntaps * Cin
+  int lg_cpt;               // log2(Cin / 64): K-steps per tap
   unsigned long long tapl[4];  // per phase: packed tap index of K-tap t in bits [4t, 4t + 4)
   const bf16* w;
   int w_taps;               // taps per phase in the packed layout (16 / 4)
@@ -73,6 +71,7 @@ struct DeepParams {
   float* stats;             // [nphase * mtiles][N][4] tile statistics partials, or null (no BatchNorm)
   DeepBN bn;
   int nphase, mtiles, ntiles, ksplit, kps;  // kps: K-steps (64) per split
+  int acquire;              // hand-offs also take the agent acquire (grids of more than one block per CU)
   float inv_ghw, inv_gw;
   unsigned long long* dbg;  // diagnostics (stc_deep_debug_next): per block 8 wall-clock stamps, or null
 };
@@ -82,89 +81,77 @@ struct DeepParams {
 #define DEEP_STAMP(i) \
   do { if (p.dbg && threadIdx.x == 0) p.dbg[(long long)blockIdx.x * 8 + (i)] = wall_clock64(); } while (0)
 
-// one agent-scope hand-off to the last arriver of a counter (Guideline 16 counter form): every wave's stores
-// drained, lane 0 releases and adds; returns (to every thread) whether this block drew the last ticket, after
-// which its loads of the other blocks' data are behind an acquire
-__device__ __forceinline__ bool deep_last_arriver(unsigned* counter, unsigned total, unsigned* flag) {
+// one in-launch hand-off to the last arriver of a counter (cdna_hip_programming.md Guideline 16, the write-through
+// form): the payload is stored sc1 (write-through to memory, no release fence) and EVERY load of it is an sc1 load
+// (past every L1 and L2, so no acquire); each wave drains its stores, the barrier joins them, lane 0 adds.
+// Returns (to every thread) whether this block drew the last ticket.  The last arriver leaves the counter zero.
+__device__ __forceinline__ bool deep_last_arriver(unsigned* counter, unsigned total, unsigned* flag, bool acquire) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = old == total - 1 ? 1u : 0u;
+    if (old == total - 1) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   const bool last = *flag != 0u;
-  if (last) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the sc1 loads below the ticket)
+  if (last && acquire) {  // (more than one block per CU: the measured sc1 form covers one; the agent acquire too)
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (left zero: the next launch)
     }
     __syncthreads();
   }
   return last;
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int SC1 = 16;  // buffer-op cache bits: sc1 (write-through stores, loads past the caches)
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, floatx4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, SC1);
+}
+__device__ __forceinline__ floatx4 ld_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, SC1));
+}
+
 // The column finisher: channel n's batch statistics from the column's tile partials {count, 0, M2, mean} (one per
 // (phase, m tile), merged in chunk order, fp64, the two passes of stc_bn_finalize), then table + running statistics.
-__device__ __forceinline__ void deep_finalize(const DeepParams& p, int n, bool count_batch) {
+__device__ __forceinline__ void deep_finalize(const DeepParams& p, __amdgpu_buffer_rsrc_t rst, int n, bool count_batch) {
   const int nch = p.nphase * p.mtiles;
   constexpr int G = 16;  // chunk loads in flight per group
   double nt = 0, sm = 0;
   for (int k0 = 0; k0 < nch; k0 += G) {
-    float4 v[G];
+    floatx4 v[G];
 #pragma unroll
     for (int u = 0; u < G; ++u)
-      v[u] = *reinterpret_cast<const float4*>(p.stats + ((long long)min(k0 + u, nch - 1) * p.N + n) * 4);
+      v[u] = ld_sc1(rst, (unsigned)((min(k0 + u, nch - 1) * p.N + n) * 16));
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-      if (k0 + u >= nch || v[u].x <= 0.f) continue;
-      nt += v[u].x;
-      sm += (double)v[u].x * v[u].w + (double)v[u].y;
+      if (k0 + u >= nch || v[u][0] <= 0.f) continue;
+      nt += v[u][0];
+      sm += (double)v[u][0] * v[u][3] + (double)v[u][1];
     }
   }
   const double mu = nt > 0 ? sm / nt : 0.0;
   double m2 = 0;
   for (int k0 = 0; k0 < nch; k0 += G) {
-    float4 v[G];
+    floatx4 v[G];
 #pragma unroll
     for (int u = 0; u < G; ++u)
-      v[u] = *reinterpret_cast<const float4*>(p.stats + ((long long)min(k0 + u, nch - 1) * p.N + n) * 4);
+      v[u] = ld_sc1(rst, (unsigned)((min(k0 + u, nch - 1) * p.N + n) * 16));
 #pragma unroll
     for (int u = 0; u < G; ++u) {
-      if (k0 + u >= nch || v[u].x <= 0.f) continue;
-      const double nb = v[u].x, s1 = v[u].y, r = s1 / nb;
-      double q = (double)v[u].z - s1 * r;
+      if (k0 + u >= nch || v[u][0] <= 0.f) continue;
+      const double nb = v[u][0], s1 = v[u][1], r = s1 / nb;
+      double q = (double)v[u][2] - s1 * r;
       if (q < 0) q = 0;
-      const double d = (double)v[u].w + r - mu;
+      const double d = (double)v[u][3] + r - mu;
       m2 += q + nb * d * d;
     }
   }
   bn_finalize_store(n, nt, mu, m2, p.bn.gamma, p.bn.beta, p.bn.rmean, p.bn.rvar, count_batch ? p.bn.nbt : nullptr,
                     p.bn.momentum, p.bn.eps, p.bn.mean_o, p.bn.rstd_o, p.bn.scale_o, p.bn.shift_o);
-}
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ unsigned lds_addr(const char* p) {
-  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
-}
-// N 16-byte LDS reads, all in flight, then one wait (the results are complete when the statement ends)
-template <int N>
-__device__ __forceinline__ void lds_read_wait(u32x4 (&v)[N], const unsigned (&a)[N]) {
-  if constexpr (N == 1) {
-    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v[0]) : "v"(a[0]) : "memory");
-  } else if constexpr (N == 2) {
-    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(v[0]), "=&v"(v[1]) : "v"(a[0]), "v"(a[1]) : "memory");
-  } else {
-    static_assert(N == 4, "1, 2 or 4 chunks per thread");
-    asm volatile(
-        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]) : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]) : "memory");
-  }
 }
 
 template <int BM, int BN>
@@ -173,7 +160,7 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int AC = BM * 8 / 256, BC = BN * 8 / 256;  // 16-byte chunks per thread per K-step (A / B)
   constexpr int STAGE = (BM + BN) * 128;
-  constexpr int NSTG = DEEP_NSTG;                      // LDS-DMA ring: NSTG - 1 K-steps in flight
+  constexpr int NSTG = 2;                              // LDS double buffer
   constexpr int AG = BM / 32, BG = BN / 32, P = AG + BG;  // 1 KiB DMA pieces per wave per K-step
   static_assert(FM >= 1 && FN >= 1 && AC >= 1 && BC >= 1, "tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -243,31 +230,20 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
     }
   };
 
-  // ---- LDS-DMA lane roles: piece = 8 rows x 128 B; lane -> row (lane >> 3) of the piece, LDS slot lane & 7, which
-  // holds source chunk slot ^ (row & 7) (the swizzle every 16-row fragment read is conflict-free with).  Per DMA row,
-  // computed once: the element offset of its tap-0 source pixel in each source and the set of taps that read
-  // padding (bit t: K-tap index t, all bits for rows past M) -- a K-step then costs one add and a bit test per row.
+  // ---- staging roles: a K-step stages BM + BN rows of 128 B (64 bf16 channels) as 8-row pieces; lane -> row
+  // lane >> 3 of a piece, LDS slot lane & 7 holding source chunk slot ^ (row & 7) (the swizzle the fragment reads
+  // are conflict-free with).  Per staged row, computed once: the byte offset of its tap-0 source pixel in each source
+  // and the taps that read padding (bit t: K-tap t; every bit for rows past M) -- a K-step then costs an add, a
+  // shift and an OR per row, its scalar terms shifts and table lookups (K-steps per tap a power of two).
   const int prow = lane >> 3, pslot = lane & 7;
-  const int schunk = pslot ^ (prow & 7);  // (piece rows start at multiples of 8: row & 7 == prow)
+  const int schunk = pslot ^ prow;  // (pieces start at multiples of 8 rows: row & 7 == prow)
   const int GHW = p.GH * p.GW;
   const unsigned long long tapl = ph == 0 ? p.tapl[0] : (ph == 1 ? p.tapl[1] : (ph == 2 ? p.tapl[2] : p.tapl[3]));
-  // tap t of the K order -> (row, column) offset of its source pixel from the tap-0 pixel's (conv: (+ky, +kx) from
-  // (2gy - 1, 2gx - 1); ConvT phase (py, px): (-ty, -tx) from (gy + py, gx + px))
+  // tap -> (row, column) offset of its source pixel from the tap-0 pixel's (conv: (+ky, +kx) from (2gy - 1, 2gx - 1);
+  // ConvT phase (py, px): (-ty, -tx) from (gy + py, gx + px))
   auto tap_rc = [&](int tap, int& dy, int& dx) {
     if (p.convt) { dy = -(tap >> 1); dx = -(tap & 1); }
     else { dy = tap >> 2; dx = tap & 3; }
-  };
-  // the in-range K taps of a grid point (bit t set: tap t reads padding)
-  auto pad_taps = [&](bool in, int gy, int gx) {
-    unsigned inv = 0;
-    const int y0 = p.convt ? gy + py : 2 * gy - 1, x0 = p.convt ? gx + px : 2 * gx - 1;
-    for (int t = 0; t < p.ntaps; ++t) {
-      int dy, dx;
-      tap_rc((int)((tapl >> (4 * t)) & 15u), dy, dx);
-      const int iy = y0 + dy, ix = x0 + dx;
-      if (!(in && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)) inv |= 1u << t;
-    }
-    return inv;
   };
   unsigned a_off[2][AG], a_inv[AG];
 #pragma unroll
@@ -278,11 +254,18 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
     const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
     const int gy = fast_div(rem, p.GW, p.inv_gw), gx = rem - gy * p.GW;
     const int y0 = p.convt ? gy + py : 2 * gy - 1, x0 = p.convt ? gx + px : 2 * gx - 1;
-    a_inv[g] = pad_taps(in, gy, gx);
+    unsigned inv = 0;
+    for (int t = 0; t < p.ntaps; ++t) {
+      int dy, dx;
+      tap_rc((int)((tapl >> (4 * t)) & 15u), dy, dx);
+      const int iy = y0 + dy, ix = x0 + dx;
+      if (!(in && iy >= 0 && iy < p.IH && ix >= 0 && ix < p.IW)) inv |= 1u << t;
+    }
+    a_inv[g] = inv;
 #pragma unroll
     for (int si = 0; si < 2; ++si) {
       const DeepSrc& q = si ? p.src[1] : p.src[0];
-      a_off[si][g] = (unsigned)(b * q.bs + (long long)y0 * q.rs + (long long)x0 * q.ps + q.co + 8 * schunk);
+      a_off[si][g] = 2u * (unsigned)(b * q.bs + (long long)y0 * q.rs + (long long)x0 * q.ps + q.co + 8 * schunk);
     }
   }
   const __amdgpu_buffer_rsrc_t ra0 =
@@ -297,80 +280,75 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
 #pragma unroll
   for (int h = 0; h < BG; ++h) {
     const int n = n0 + (wave * BG + h) * 8 + prow;
-    b_off[h] = n < p.N ? (unsigned)(n * p.w_taps * p.Cin + 8 * schunk) : OOB;
+    b_off[h] = n < p.N ? 2u * (unsigned)(n * p.w_taps * p.Cin + 8 * schunk) : OOB;
   }
-  // K-step ks: K-tap index ti, packed tap, channel block cb, source
+  // K-step ks: K-tap index ti, its packed tap, channel block cb (of the concatenated sources), source s1
   auto step_terms = [&](int ks, int& ti, int& tap, int& cb, bool& s1) {
-    ti = ks / cpt;
-    cb = (ks - ti * cpt) * 64;
+    ti = ks >> p.lg_cpt;
+    cb = (ks & ((1 << p.lg_cpt) - 1)) << 6;
     tap = (int)((tapl >> (4 * ti)) & 15u);
     s1 = p.nsrc == 2 && cb >= p.src[0].nc;
   };
-  // the DMA pieces of K-step ks into stage st: A rows (padding and rows past M out of range: zeros), B rows
-  auto issue = [&](int ks, int st) {
+
+  // ---- the K loop, register-staged: the A / B chunks of K-step s + R load into VGPRs while steps s .. s + R - 1
+  // compute; at step s its chunks get the source's BatchNorm affine + activation in registers and go to LDS stage
+  // s & 1; one barrier per step (a stage is rewritten two steps after it was read, behind the barrier between)
+  const int nsteps = ks1 - ks0;
+  struct Stg {
+    u32x4 a[AG], b[BG];
+  };
+  auto load = [&](int ks, Stg& r) {  // (a step past the block's K range loads zeros: the loop runs in groups of R)
     int ti, tap, cb;
     bool s1;
     step_terms(ks, ti, tap, cb, s1);
+    const unsigned past = ks >= ks1 ? OOB : 0u;
     int dy, dx;
     tap_rc(tap, dy, dx);
-    const unsigned delta = (unsigned)((s1 ? p.src[1].rs : p.src[0].rs) * dy + (s1 ? p.src[1].ps : p.src[0].ps) * dx +
-                                      cb - (s1 ? p.src[0].nc : 0));
-    char* sA = smem + st * STAGE;
+    const unsigned adelta = 2u * (unsigned)((s1 ? p.src[1].rs : p.src[0].rs) * dy +
+                                            (s1 ? p.src[1].ps : p.src[0].ps) * dx + cb - (s1 ? p.src[0].nc : 0));
 #pragma unroll
     for (int g = 0; g < AG; ++g) {
-      const unsigned off = ((s1 ? a_off[1][g] : a_off[0][g]) + delta) * 2u;
-      dma16(s1 ? ra1 : ra0, sA + (wave * AG + g) * 1024, off | (((a_inv[g] >> ti) & 1u) << 31));
+      const unsigned off = ((s1 ? a_off[1][g] : a_off[0][g]) + adelta) | ((a_inv[g] << (31 - ti)) & OOB) | past;
+      r.a[g] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(s1 ? ra1 : ra0, off, 0, 0));
     }
-    char* sB = sA + BM * 128;
-    const unsigned bdelta = (unsigned)(tap * p.Cin + cb);
+    const unsigned bdelta = 2u * (unsigned)(tap * p.Cin + cb);
 #pragma unroll
-    for (int h = 0; h < BG; ++h) dma16(rw, sB + (wave * BG + h) * 1024, ((b_off[h] + bdelta) * 2u) | (b_off[h] & OOB));
+    for (int h = 0; h < BG; ++h)
+      r.b[h] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, (b_off[h] + bdelta) | past, 0, 0));
   };
-  // BatchNorm affine + activation of the staged A chunks of K-step ks (rows and taps that read padding stay zero)
-  int t_row[AC];
-  unsigned t_inv[AC];
-#pragma unroll
-  for (int u = 0; u < AC; ++u) {
-    const int ch = tid + u * 256;
-    t_row[u] = ch >> 3;
-    const int m = m0 + t_row[u];
-    const bool in = m < p.M;
-    const int mm = in ? m : 0;
-    const int b = fast_div(mm, GHW, p.inv_ghw), rem = mm - b * GHW;
-    const int gy = fast_div(rem, p.GW, p.inv_gw), gx = rem - gy * p.GW;
-    (void)b;
-    t_inv[u] = pad_taps(in, gy, gx);
-  }
-  auto transform = [&](int ks, int st, bool& any) {
+  auto store = [&](int ks, const Stg& r, int st) {
     int ti, tap, cb;
     bool s1;
     step_terms(ks, ti, tap, cb, s1);
-    any = (s1 ? p.src[1].mode : p.src[0].mode) != 0;
-    if (!any) return;
-    const float slope = s1 ? p.src[1].slope : p.src[0].slope;
     char* sA = smem + st * STAGE;
-    unsigned addr[AC];
-    u32x4 v[AC];
+    char* sB = sA + BM * 128;
+    if ((s1 ? p.src[1].mode : p.src[0].mode) != 0) {
+      const float slope = s1 ? p.src[1].slope : p.src[0].slope;  // (in [0, 1]: act(x) = max(x, slope x))
+      const int kc = cb + 8 * schunk;
+      const float4 c0 = *reinterpret_cast<const float4*>(tsc + kc), c1 = *reinterpret_cast<const float4*>(tsc + kc + 4);
+      const float4 h0 = *reinterpret_cast<const float4*>(tsh + kc), h1 = *reinterpret_cast<const float4*>(tsh + kc + 4);
+      const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
-    for (int u = 0; u < AC; ++u) addr[u] = lds_addr(sA + t_row[u] * 128 + ((tid + u * 256) & 7) * 16);
-    // (LDS reads and writes in inline asm: the compiler cannot tell this stage's slots from the LDS-DMA writes still
-    // in flight into the later stages, and would drain the whole ring -- vmcnt(0) -- before touching LDS here)
-    lds_read_wait<AC>(v, addr);
+      for (int g = 0; g < AG; ++g) {
+        // (padding stays zero: a mask, not a branch -- a branch here costs the loads' counted waits)
+        const unsigned keep = ((a_inv[g] >> ti) & 1u) | (ks >= ks1 ? 1u : 0u) ? 0u : 0xffffffffu;
+        u32x4 o;
 #pragma unroll
-    for (int u = 0; u < AC; ++u) {
-      const int slot = (tid + u * 256) & 7, row = t_row[u];
-      const int kc = cb + 8 * (slot ^ (row & 7));
-      u32x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float lo = fmaf(__uint_as_float(v[u][e] << 16), tsc[kc + 2 * e], tsh[kc + 2 * e]);
-        const float hi = fmaf(__uint_as_float(v[u][e] & 0xffff0000u), tsc[kc + 2 * e + 1], tsh[kc + 2 * e + 1]);
-        o[e] = ((t_inv[u] >> ti) & 1u) ? 0u : pack_bf16x2(act(lo, slope), act(hi, slope));  // (padding stays zero)
+        for (int e = 0; e < 4; ++e) {
+          const float lo = fmaf(__uint_as_float(r.a[g][e] << 16), sc[2 * e], sh[2 * e]);
+          const float hi = fmaf(__uint_as_float(r.a[g][e] & 0xffff0000u), sc[2 * e + 1], sh[2 * e + 1]);
+          o[e] = pack_bf16x2(fmaxf(lo, slope * lo), fmaxf(hi, slope * hi)) & keep;
+        }
+        *reinterpret_cast<u32x4*>(sA + (wave * AG + g) * 1024 + lane * 16) = o;
       }
-      asm volatile("ds_write_b128 %0, %1" ::"v"(addr[u]), "v"(o) : "memory");
+    } else {
+#pragma unroll
+      for (int g = 0; g < AG; ++g) *reinterpret_cast<u32x4*>(sA + (wave * AG + g) * 1024 + lane * 16) = r.a[g];
     }
+#pragma unroll
+    for (int h = 0; h < BG; ++h) *reinterpret_cast<u32x4*>(sB + (wave * BG + h) * 1024 + lane * 16) = r.b[h];
   };
-
   floatx4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -398,125 +376,36 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
     }
   };
 
-#if DEEP_REG
-  // ---- the K loop, register-staged: the A / B chunks of K-step s + 2 load into VGPRs while step s computes; at
-  // step s its chunks (loaded two steps earlier) get the sources' BatchNorm affine + activation in registers and go
-  // to LDS stage s & 1 with the DMA pieces' layout; one barrier per step (a stage is rewritten two steps after it was
-  // read, behind the barrier of the step between)
-  const int nsteps = ks1 - ks0;
-  struct Stg {
-    u32x4 a[AG], b[BG];
-  };
-  auto load = [&](int ks, Stg& r) {  // (a step past the block's K range loads zeros: the loop runs in pairs)
-    int ti, tap, cb;
-    bool s1;
-    step_terms(ks, ti, tap, cb, s1);
-    const unsigned past = ks >= ks1 ? OOB : 0u;
-    int dy, dx;
-    tap_rc(tap, dy, dx);
-    const unsigned delta = (unsigned)((s1 ? p.src[1].rs : p.src[0].rs) * dy + (s1 ? p.src[1].ps : p.src[0].ps) * dx +
-                                      cb - (s1 ? p.src[0].nc : 0));
+  constexpr int R = DEEP_RING;  // K-steps of loads in flight
+  Stg r[R];
 #pragma unroll
-    for (int g = 0; g < AG; ++g) {
-      const unsigned off = ((s1 ? a_off[1][g] : a_off[0][g]) + delta) * 2u;
-      r.a[g] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             s1 ? ra1 : ra0, off | (((a_inv[g] >> ti) & 1u) << 31) | past, 0, 0));
-    }
-    const unsigned bdelta = (unsigned)(tap * p.Cin + cb);
-#pragma unroll
-    for (int h = 0; h < BG; ++h)
-      r.b[h] = __builtin_bit_cast(
-          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, ((b_off[h] + bdelta) * 2u) | (b_off[h] & OOB) | past, 0, 0));
-  };
-  auto store = [&](int ks, const Stg& r, int st) {
-    int ti, tap, cb;
-    bool s1;
-    step_terms(ks, ti, tap, cb, s1);
-    char* sA = smem + st * STAGE;
-    char* sB = sA + BM * 128;
-    if ((s1 ? p.src[1].mode : p.src[0].mode) != 0) {
-      const float slope = s1 ? p.src[1].slope : p.src[0].slope;
-      const int kc = cb + 8 * schunk;
-      const float4 c0 = *reinterpret_cast<const float4*>(tsc + kc), c1 = *reinterpret_cast<const float4*>(tsc + kc + 4);
-      const float4 h0 = *reinterpret_cast<const float4*>(tsh + kc), h1 = *reinterpret_cast<const float4*>(tsh + kc + 4);
-      const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-      for (int g = 0; g < AG; ++g) {
-        // (padding stays zero: a mask, not a branch -- a branch here costs the loads' counted waits)
-        const unsigned keep = ((a_inv[g] >> ti) & 1u) | (ks >= ks1 ? 1u : 0u) ? 0u : 0xffffffffu;
-        u32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float lo = fmaf(__uint_as_float(r.a[g][e] << 16), sc[2 * e], sh[2 * e]);
-          const float hi = fmaf(__uint_as_float(r.a[g][e] & 0xffff0000u), sc[2 * e + 1], sh[2 * e + 1]);
-          const float l2 = fmaxf(lo, 0.f) + slope * fminf(lo, 0.f), h2 = fmaxf(hi, 0.f) + slope * fminf(hi, 0.f);
-          o[e] = pack_bf16x2(l2, h2) & keep;
-        }
-        *reinterpret_cast<u32x4*>(sA + (wave * AG + g) * 1024 + lane * 16) = o;
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < AG; ++g) *reinterpret_cast<u32x4*>(sA + (wave * AG + g) * 1024 + lane * 16) = r.a[g];
-    }
-#pragma unroll
-    for (int h = 0; h < BG; ++h) *reinterpret_cast<u32x4*>(sB + (wave * BG + h) * 1024 + lane * 16) = r.b[h];
-  };
-  Stg r0, r1;
-  load(ks0, r0);
-  load(ks0 + 1, r1);
+  for (int u = 0; u < R; ++u) load(ks0 + u, r[u]);
   fill_tables();
   __syncthreads();  // (the tables)
   DEEP_STAMP(1);
-  for (int s = 0; s < nsteps; s += 2) {  // (an odd count ends with one step of zeros)
-    store(ks0 + s, r0, 0);
-    load(ks0 + s + 2, r0);
-    __syncthreads();
-    compute(smem);
-    store(ks0 + s + 1, r1, 1);
-    load(ks0 + s + 3, r1);
-    __syncthreads();
-    compute(smem + STAGE);
-  }
-#else
-  // ---- the K loop: an NSTG-stage LDS-DMA ring (steps ks0 .. ks0 + NSTG - 2 issued before the tables are staged);
-  // at step s wait for this wave's pieces of step s (counted vmcnt), barrier, the A transform (+ barrier), refill the
-  // stage step s - 1 read, MFMAs
-  const int nsteps = ks1 - ks0;
+  for (int s = 0; s < nsteps; s += R) {  // (a count that is not a multiple of R ends with steps of zeros)
 #pragma unroll
-  for (int i = 0; i < NSTG - 1; ++i)
-    if (i < nsteps) issue(ks0 + i, i);
-  fill_tables();
-  __syncthreads();  // (the tables)
-  DEEP_STAMP(1);
-  int cur = 0;
-  for (int s = 0; s < nsteps; ++s) {
-    wait_ahead<P>(min(NSTG - 2, nsteps - 1 - s));
-    __builtin_amdgcn_s_barrier();
-    bool tr;
-    transform(ks0 + s, cur, tr);
-    if (tr) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+    for (int u = 0; u < R; ++u) {
+      store(ks0 + s + u, r[u], u & 1);
+      load(ks0 + s + u + R, r[u]);
+      __syncthreads();
+      compute(smem + (u & 1) * STAGE);
     }
-    if (s + NSTG - 1 < nsteps) issue(ks0 + s + NSTG - 1, cur == 0 ? NSTG - 1 : cur - 1);
-    compute(smem + cur * STAGE);
-    cur = cur == NSTG - 1 ? 0 : cur + 1;
   }
-#endif
   __syncthreads();  // (the epilogue reuses the stages)
 
   DEEP_STAMP(2);
   // ---- split-K: slab store, ticket, the last arriver reduces in split order
   unsigned* flag = reinterpret_cast<unsigned*>(tsh + 1024);  // (inside the one LDS array)
   if (p.ksplit > 1) {
-    float* my = p.slab + ((long long)tile * p.ksplit + split) * (BM * BN);
+    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.slab + (long long)tile * p.ksplit * (BM * BN)), (short)0, p.ksplit * BM * BN * 4, 0x00020000);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        *reinterpret_cast<floatx4*>(my + ((wave * FM + i) * FN + j) * 256 + lane * 4) = acc[i][j];
-    if (!deep_last_arriver(p.tickets + tile, (unsigned)p.ksplit, flag)) {
+        st_sc1(rsl, (unsigned)((split * (BM * BN) + ((wave * FM + i) * FN + j) * 256 + lane * 4) * 4), acc[i][j]);
+    if (!deep_last_arriver(p.tickets + tile, (unsigned)p.ksplit, flag, p.acquire)) {
       DEEP_STAMP(6);
       return;
     }
@@ -526,10 +415,9 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) sum[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* base = p.slab + (long long)tile * p.ksplit * (BM * BN);
     // every slab loaded (the own one too: no per-element register-or-load select), groups of RG slabs in flight,
     // summed in split order
-    constexpr int RG = FM * FN <= 4 ? 4 : 2;
+    constexpr int RG = FM * FN <= 1 ? 16 : (FM * FN <= 2 ? 8 : (FM * FN <= 4 ? 4 : 2));  // (<= 64 VGPRs in flight)
     const int S = p.ksplit;
     for (int s0 = 0; s0 < S; s0 += RG) {
       floatx4 v[RG][FM][FN];
@@ -540,8 +428,7 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            v[g][i][j] = *reinterpret_cast<const floatx4*>(base + (long long)s * (BM * BN) +
-                                                           ((wave * FM + i) * FN + j) * 256 + lane * 4);
+            v[g][i][j] = ld_sc1(rsl, (unsigned)((s * (BM * BN) + ((wave * FM + i) * FN + j) * 256 + lane * 4) * 4));
       }
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
@@ -595,6 +482,8 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
       }
     }
     __syncthreads();
+    const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.stats, (short)0, p.nphase * p.mtiles * p.N * 16, 0x00020000);
     for (int c = tid; c < BN; c += 256) {
       const int n = n0 + c;
       if (n >= p.N) continue;
@@ -610,15 +499,14 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
         m2 += m2w + dl * dl * (cnt * nw / ntot);
         cnt = ntot;
       }
-      *reinterpret_cast<float4*>(p.stats + (((long long)ph * p.mtiles + mt) * p.N + n) * 4) =
-          make_float4(cnt, 0.f, m2, mean);
+      st_sc1(rst, (unsigned)(((ph * p.mtiles + mt) * p.N + n) * 16), floatx4{cnt, 0.f, m2, mean});
     }
     // the last tile of this column of channels finalizes their BatchNorm (the next layer reads the table)
     const long long ntiles_all = (long long)p.nphase * p.mtiles * p.ntiles;
-    if (deep_last_arriver(p.tickets + ntiles_all + nt, (unsigned)(p.nphase * p.mtiles), flag)) {
+    if (deep_last_arriver(p.tickets + ntiles_all + nt, (unsigned)(p.nphase * p.mtiles), flag, p.acquire)) {
       DEEP_STAMP(5);
       for (int c = tid; c < BN; c += 256)
-        if (n0 + c < p.N) deep_finalize(p, n0 + c, nt == 0 && c == 0);
+        if (n0 + c < p.N) deep_finalize(p, rst, n0 + c, nt == 0 && c == 0);
     }
     __syncthreads();
   }
@@ -695,12 +583,14 @@ static bool deep_plan(int convt, int B, int GH, int GW, int IH, int IW, int Cin,
       const long long blocks = tiles * s;
       if (!force && (blocks > 1024 || (blocks < 128 && s * 2 <= nks))) continue;
       const int kps = (nks + s - 1) / s;
-      // cost model (us): waves of blocks x (operand bytes per block at ~100 GB/s per CU + MFMA time) + the
-      // reducer's slab read + the launch's fixed latency
-      const double per_block = (double)(BM + BN) * kps * 128 / 100e3 + (double)BM * BN * kps * 64 * 2 / 9.8e6;
-      const double waves = (double)((blocks + 511) / 512);
-      const double red = s > 1 ? (double)s * BM * BN * 4 / 100e3 + 2.0 : 0.0;
-      const double cost = waves * per_block * (blocks > 256 ? 2.0 : 1.0) + red;
+      // cost model (us, fitted to the plan sweeps of scripts/deep_tune.py): a K-step costs a block ~0.25 us of
+      // issue and waits plus ~3.5 ns per staged row (a second block per CU overlaps little: rounds of 256 blocks),
+      // the reducer reads its tile's slabs (~40 GB/s per block) after a ~1.5 us hand-off; the loop runs whole
+      // groups of DEEP_RING steps
+      const int kpr = (kps + DEEP_RING - 1) / DEEP_RING * DEEP_RING;
+      const double rounds = (double)((blocks + 255) / 256);
+      const double red = s > 1 ? 1.5 + (double)s * BM * BN * 4 / 40e3 : 0.0;
+      const double cost = rounds * kpr * (0.25 + 0.0035 * (BM + BN)) + red;
       if (cost < best) { best = cost; bi = t; bs = s; }
     }
   }
@@ -715,14 +605,16 @@ static bool deep_plan(int convt, int B, int GH, int GW, int IH, int IW, int Cin,
 }
 
 // [two stages][scale / shift table of 1024 channels][flag]; the epilogue's tile and statistics area fit in the stages
-static size_t deep_lds(int BM, int BN) { return DEEP_NSTG * (size_t)(BM + BN) * 128 + 2 * 1024 * 4 + 16; }
+static size_t deep_lds(int BM, int BN) { return 2 * (size_t)(BM + BN) * 128 + 2 * 1024 * 4 + 16; }
 
 }  // namespace stc
 
 using namespace stc;
 
 static bool deep_shape_ok(int kind, int Cin, int Cout) {
-  return (kind == STC_CONV_S2 || kind == STC_CONVT_S2) && Cin % 64 == 0 && Cin <= 1024 && Cout % 32 == 0 && Cout <= 2048;
+  const int cpt = Cin / 64;  // (K-steps per tap: a power of two, the kernel's step terms are shifts)
+  return (kind == STC_CONV_S2 || kind == STC_CONVT_S2) && Cin % 64 == 0 && Cin <= 1024 && (cpt & (cpt - 1)) == 0 &&
+         Cout % 32 == 0 && Cout <= 2048;
 }
 
 static unsigned long long* g_deep_dbg = nullptr;  // (diagnostics: the next launch's stamps; one-shot)
@@ -792,6 +684,7 @@ extern "C" int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src,
     d.nc = s.C;
     d.scale = s.scale; d.shift = s.shift; d.slope = s.slope;
     d.mode = (s.scale || s.slope != 1.f) ? 1 : 0;
+    STC_REQUIRE(!d.mode || (s.slope >= 0.f && s.slope <= 1.f), "stc_deep_conv: activation slope %g not in [0, 1]", s.slope);
   }
   if (bn) {
     STC_REQUIRE(bn->mean_out && bn->rstd_out && bn->scale_out && bn->shift_out,
@@ -807,6 +700,7 @@ extern "C" int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src,
   p.inv_ghw = 1.0f / (float)(GH * GW);
   p.inv_gw = 1.0f / (float)GW;
   p.N = Cout; p.Cin = Cin; p.ntaps = pl.ntaps;
+  p.lg_cpt = __builtin_ctz((unsigned)(Cin / 64));
   for (int a = 0; a < 4; ++a) {
     p.tapl[a] = 0;
     for (int b = 0; b < pl.ntaps; ++b) p.tapl[a] |= (unsigned long long)(pl.taps[a][b] & 15) << (4 * b);
@@ -821,6 +715,16 @@ extern "C" int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src,
   p.nphase = nph; p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.ksplit = pl.ksplit; p.kps = pl.kps;
   p.dbg = g_deep_dbg;
   g_deep_dbg = nullptr;
+  static int ncu = 0;  // (CUs of the device: one process drives one GPU)
+  if (ncu == 0) {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      ncu = n;
+    else
+      ncu = 256;
+  }
+  p.acquire = tiles * pl.ksplit > ncu ? 1 : 0;
   const dim3 grid((unsigned)(tiles * pl.ksplit));
   hipStream_t st = (hipStream_t)stream;
   const size_t lds = deep_lds(pl.BM, pl.BN);
