@@ -42,13 +42,14 @@ constexpr int HB_BM = 256, HB_BN = 128;  // block tile: 256 GEMM rows (whole out
 //             4-wave blocks per CU would leave half the CUs empty)
 // LDS: [B pair 0][A slot 0][A slot 1][A slot 2][B pair 1].  The masked edge lanes of A slot 0 / 2 address one pixel
 // before / after it: inside the neighbouring B pair, never outside the block's LDS.
-template <int RB, int BN = HB_BN> struct HaloGeom {
+template <int RB, int BN = HB_BN, int NB = 2> struct HaloGeom {  // NB: B K-steps per super-step (a pair / a quad)
   static constexpr int A = HB_BM * RB, B = BN * RB;
-  static constexpr int A0 = 2 * B, B1 = A0 + 3 * A, LDS = 4 * B + 3 * A;
+  static constexpr int A0 = NB * B, B1 = A0 + 3 * A, LDS = 2 * NB * B + 3 * A;
   static constexpr int CH = RB / 16;        // 16-byte chunks per row
   static constexpr int PR = 1024 / RB;      // rows per 1 KiB DMA piece
 };
 static_assert(HaloGeom<64>::LDS <= 81920 && HaloGeom<128>::LDS <= 163840, "LDS");
+static_assert(HaloGeom<64, 64, 4>::LDS <= 81920, "LDS");
 
 // chunk c of LDS row P sits in slot c ^ swz(P): RB = 128: P & 7; RB = 64: 2 * ((P >> 2) & 1) -- for both, every
 // ds_read_b128 lane group of a 16-row fragment is conflict-free for ANY first row (the d-shifted A fragments)
@@ -66,24 +67,29 @@ template <int RB> __device__ __forceinline__ int hswz(int row) {
 // Tap (ky, kx) reads A row y + SG * ky + OF, column x + SG * kx + OF (SG, OF = 1, -1 / -1, 1): the stage of ky
 // holds the rows oy0 + r + SG * ky + OF and its four taps read positions r * GW + x + d, d = SG * kx + OF, in two
 // super-steps of two taps (every staged pixel serves four taps).
+// GEOM 4: ConvTranspose2d k4 s2 with the TWO phases of one row parity per block, (py, 0) and (py, 1): they read the
+// same input rows (gy + py - ty) and differ only in the column shift d = px - tx, so one A stage feeds both phases'
+// taps -- four B K-steps (a quad) per super-step, two accumulator sets, half GEOM 1's A stream per output.
 template <int GEOM, int GW, int BN, bool BNB, int RB, int WM, int WN>
 __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(const GParams p) {
-  using G = HaloGeom<RB, BN>;
+  constexpr bool T2 = GEOM == 4;                             // two ConvT phases per block
+  constexpr int NB = T2 ? 4 : 2, NPH = T2 ? 2 : 1;           // B K-steps per super-step, accumulator sets
+  using G = HaloGeom<RB, BN, NB>;
   constexpr int BM = HB_BM, NW = WM * WN;
   constexpr int TM = BM / WM, TN = BN / WN;                  // wave tile: 128 x 64 / 64 x 64
   constexpr int FM = TM / 16, FN = TN / 16;                  // fragments of 16 x 16
   constexpr int KK = RB / 64;                                // 32-deep MFMA steps per K-step
   constexpr int AG = BM / (G::PR * NW), BG = BN / (G::PR * NW);  // DMA pieces per wave: A stage / B K-step
   constexpr int HALVES = 128 / RB;                           // stages per 64-channel chunk and (ky, parity) / ty
-  constexpr bool S1 = GEOM >= 2;
+  constexpr bool S1 = GEOM == 2 || GEOM == 3;
   constexpr int SG = GEOM == 3 ? -1 : 1, OF = GEOM == 3 ? 1 : -1;
-  constexpr int SPC = (GEOM == 1 ? 2 : 8) * HALVES;          // super-steps per 64-channel chunk
+  constexpr int SPC = (GEOM == 1 || T2 ? 2 : 8) * HALVES;    // super-steps per 64-channel chunk
   constexpr int TH = BM / GW;
   constexpr int AH = S1 ? AG / 2 : AG;                       // A pieces per super-step (S1: a stage over two)
-  constexpr int NP = 2 * BG + AH, NG = 2 * KK * FM / 2;      // DMA pieces / 8-MFMA groups per super-step and wave
+  constexpr int NP = NB * BG + AH, NG = NB * KK * FM / 2;    // DMA pieces / 8-MFMA groups per super-step and wave
   static_assert(GW % 16 == 0 && BM % GW == 0 && TM % GW == 0 && FN == 4 && FM % 2 == 0 && BG >= 1,
                 "whole output rows per tile and per wave, 16-row fragments inside an output row");
-  static_assert(S1 ? AG % 2 == 0 : NP >= NG, "every MFMA group issues a piece (S1: whole halves of a stage)");
+  static_assert(S1 ? AG % 2 == 0 : (T2 || NP >= NG), "every MFMA group issues a piece (S1: whole halves of a stage)");
   static_assert(BM * (BN * 2 + 16) + WM * BN * 16 <= G::LDS, "epilogue tile + statistics merge area");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -93,14 +99,15 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   // XCD-aware bijective remap (blocks b, b + 8, ... share an XCD): consecutive ids -- the 4 phases of a ConvT tile
   // (the same input rows), the N tiles of one A tile, vertically adjacent row tiles (overlapping stages) -- run on
   // one XCD's L2
-  const int nwg = p.mtiles * p.ntiles * (GEOM == 1 ? 4 : 1);
+  const int nwg = p.mtiles * p.ntiles * (GEOM == 1 ? 4 : (T2 ? 2 : 1));
   int bid = blockIdx.x;
   {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  const int ph = GEOM == 1 ? (bid & 3) : 0;  // phase (py, px) = (ph >> 1, ph & 1)
+  const int ph = GEOM == 1 ? (bid & 3) : (T2 ? 2 * (bid & 1) : 0);  // phase (py, px) = (ph >> 1, ph & 1) (T2: px 0)
   if (GEOM == 1) bid >>= 2;
+  if (T2) bid >>= 1;
   const int py = ph >> 1, px = ph & 1;
   const int mt = bid / p.ntiles, nt = bid % p.ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -152,7 +159,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
       odd = (t & 1) ^ 1;
       ky = (t >> 1) & 3;
       ch = t >> 3;
-    } else if constexpr (GEOM == 1) {  // (ky = ty)
+    } else if constexpr (GEOM == 1 || T2) {  // (ky = ty)
       odd = 0;
       ky = t & 1;
       ch = t >> 1;
@@ -168,7 +175,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
     if constexpr (GEOM == 0) {
       delta = (unsigned)((ky - 1) * p.a_rs + odd * p.a_ps + ch * 64 + half * 32);
       pen = ky == 0 ? top : (ky == 3 ? bot : 0u);
-    } else if constexpr (GEOM == 1) {
+    } else if constexpr (GEOM == 1 || T2) {
       const int dy = py - ky;
       delta = (unsigned)(dy * p.a_rs + ch * 64 + half * 32);
       pen = dy < 0 ? top : (dy > 0 ? bot : 0u);
@@ -183,6 +190,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   auto b_k0 = [&](int ss, int j) {
     int half, odd, ky, ch;
     ss_terms(S1 ? ss >> 1 : ss, half, odd, ky, ch);
+    if constexpr (T2)  // K-step j = 2 px + tx of the quad: phase (py, px) (its weights one phase stride on), tap (ty, tx)
+      return (unsigned)((j >> 1) * p.b_phase_stride + (2 * ky + (j & 1)) * cin + ch * 64 + half * 32);
     const int tap = GEOM == 0 ? 4 * ky + (odd ? 2 * j : 2 * j + 1) : (GEOM == 1 ? 2 * ky + j : 4 * ky + 2 * (ss & 1) + j);
     return (unsigned)(tap * cin + ch * 64 + half * 32);
   };
@@ -200,18 +209,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   };
   auto issue_b = [&](int ss) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NB; ++j) {
       const unsigned k0 = b_k0(ss, j);
 #pragma unroll
       for (int h = 0; h < BG; ++h) piece_b(smem + ((ss & 1) ? G::B1 : 0), k0, j, h);
     }
   };
 
-  floatx4 acc[FM][FN];
+  floatx4 acc[NPH][FM][FN];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int h = 0; h < NPH; ++h)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[h][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // fragment read offsets: row (l & 15) of the fragment, chunk KK * 4 * kk... = 4 kk + (l >> 4); A rows shifted by
   // d = di - 2 (fragment i adds 16 i rows, which keeps hswz: 16 is a multiple of 8)
@@ -233,8 +244,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   // D = DRT: the shift is the runtime value dr in [-1, 1] (the ConvT taps: d = px - tx, block-uniform), one code
   // path for both phase columns
   constexpr int DRT = 9;
-  auto kstep = [&](const char* sA, const char* sBj, auto Dc, auto dma, int dr = 0) {
+  using P_0 = std::integral_constant<int, 0>;
+  auto kstep = [&](const char* sA, const char* sBj, auto Dc, auto Pc, auto dma, int dr = 0) {
     constexpr int D = decltype(Dc)::value;
+    constexpr int PH = decltype(Pc)::value;  // accumulator set (T2: the phase of the pair)
     constexpr bool RT = D == DRT;
     // edge lanes: the first -d (d < 0) / last d (d > 0) rows of an output row read padding
     const bool mlo = RT ? (dr < 0 && rl == 0) : (D < 0 && rl < -D);
@@ -262,7 +275,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
 #pragma unroll
         for (int i = 2 * q; i < 2 * q + 2; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = exp_mfma(fa[i], fb[j], acc[i][j]);
+          for (int j = 0; j < FN; ++j) acc[PH][i][j] = exp_mfma(fa[i], fb[j], acc[PH][i][j]);
         dma(kk * (FM / 2) + q);
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * FN, 0);  // these 8 MFMAs, then the group's pieces
         __builtin_amdgcn_sched_group_barrier(0x020, (NP + NG - 1) / NG, 0);
@@ -295,16 +308,18 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
     const char* sB = smem + ((U & 1) ? G::B1 : 0);
     char* rB = smem + ((U & 1) ? 0 : G::B1);  // B(s + 1): the other pair
     char* rA = smem + G::A0 + (aslot == 0 ? 2 : aslot - 1) * G::A;
-    const unsigned bk0 = b_k0(s + 1, 0), bk1 = b_k0(s + 1, 1);
+    unsigned bk[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) bk[j] = b_k0(s + 1, j);
     unsigned adelta, apen;
     a_terms(st + 2, adelta, apen);
-    // pieces per super-step and wave: B(s + 1) = 2 K-steps x BG, then A(s + 2) = AG; MFMA group gi issues pieces
+    // pieces per super-step and wave: B(s + 1) = NB K-steps x BG, then A(s + 2) = AG; MFMA group gi issues pieces
     // [gi * NP / NG, (gi + 1) * NP / NG)
     auto piece = [&](int k) {
-      if (k < 2 * BG) {
-        if (nb) piece_b(rB, k < BG ? bk0 : bk1, k / BG, k % BG);
+      if (k < NB * BG) {
+        if (nb) piece_b(rB, bk[k / BG], k / BG, k % BG);
       } else {
-        if (na) piece_a(rA, adelta, apen, TP * AH + k - 2 * BG);
+        if (na) piece_a(rA, adelta, apen, TP * AH + k - NB * BG);
       }
     };
     auto group = [&](int gi) {
@@ -315,21 +330,27 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
     using D_p1 = std::integral_constant<int, 1>;
     if constexpr (GEOM == 0) {
       if constexpr (U / HALVES == 0) {  // odd parity: taps 0 (d = -1), 2 (d = 0)
-        kstep(sA, sB, D_m1{}, [&](int k) { group(k); });
-        kstep(sA, sB + G::B, D_0{}, [&](int k) { group(NG / 2 + k); });
+        kstep(sA, sB, D_m1{}, P_0{}, [&](int k) { group(k); });
+        kstep(sA, sB + G::B, D_0{}, P_0{}, [&](int k) { group(NG / 2 + k); });
       } else {  // even parity: taps 1 (d = 0), 3 (d = +1)
-        kstep(sA, sB, D_0{}, [&](int k) { group(k); });
-        kstep(sA, sB + G::B, D_p1{}, [&](int k) { group(NG / 2 + k); });
+        kstep(sA, sB, D_0{}, P_0{}, [&](int k) { group(k); });
+        kstep(sA, sB + G::B, D_p1{}, P_0{}, [&](int k) { group(NG / 2 + k); });
       }
     } else if constexpr (GEOM == 1) {  // ConvT: taps tx = 0 (d = px), 1 (d = px - 1)
       using D_rt = std::integral_constant<int, DRT>;
-      kstep(sA, sB, D_rt{}, [&](int k) { group(k); }, px);
-      kstep(sA, sB + G::B, D_rt{}, [&](int k) { group(NG / 2 + k); }, px - 1);
+      kstep(sA, sB, D_rt{}, P_0{}, [&](int k) { group(k); }, px);
+      kstep(sA, sB + G::B, D_rt{}, P_0{}, [&](int k) { group(NG / 2 + k); }, px - 1);
+    } else if constexpr (T2) {  // phase (py, 0): taps tx = 0 (d = 0), 1 (d = -1); phase (py, 1): d = +1, 0
+      using P_1 = std::integral_constant<int, 1>;
+      kstep(sA, sB, D_0{}, P_0{}, [&](int k) { group(k); });
+      kstep(sA, sB + G::B, D_m1{}, P_0{}, [&](int k) { group(NG / 4 + k); });
+      kstep(sA, sB + 2 * G::B, D_p1{}, P_1{}, [&](int k) { group(NG / 2 + k); });
+      kstep(sA, sB + 3 * G::B, D_0{}, P_1{}, [&](int k) { group(3 * NG / 4 + k); });
     } else {  // S1: taps kx = 2 TP, 2 TP + 1
       using D_a = std::integral_constant<int, SG * (2 * TP) + OF>;
       using D_b = std::integral_constant<int, SG * (2 * TP + 1) + OF>;
-      kstep(sA, sB, D_a{}, [&](int k) { group(k); });
-      kstep(sA, sB + G::B, D_b{}, [&](int k) { group(NG / 2 + k); });
+      kstep(sA, sB, D_a{}, P_0{}, [&](int k) { group(k); });
+      kstep(sA, sB + G::B, D_b{}, P_0{}, [&](int k) { group(NG / 2 + k); });
     }
     if (!S1 || TP == 1) aslot = aslot == 2 ? 0 : aslot + 1;
   };
@@ -348,12 +369,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) s_ += acc[i][j][0] + acc[i][j][3];
+      for (int j = 0; j < FN; ++j) s_ += acc[0][i][j][0] + acc[NPH - 1][i][j][3];
     if (s_ == 1.2345f) p.ws[threadIdx.x] = s_;
     return;
   }
 #endif
-  igemm_epilogue<BM, BN, WM, WN, BNB>(p, acc, m0, n0, ph, mt, 0, smem);
+  igemm_epilogue<BM, BN, WM, WN, BNB>(p, acc[0], m0, n0, ph, mt, 0, smem);
+  if constexpr (T2) igemm_epilogue<BM, BN, WM, WN, BNB>(p, acc[1], m0, n0, ph + 1, mt, 0, smem);
 }
 
 // ------------------------------------------------------------------------- host
@@ -423,7 +445,11 @@ int halo_chunks(int kind, int B, int GH, int GW) {
 // p: filled by bf16_conv_fwd (geometry, operands, output, epilogue options; vec_out set).  shape: 0 automatic,
 // 1 the 8-wave 160 KiB block, 2 the 4-wave 80 KiB block, 3 (conv-s2) the 4-wave 256 x 64 block (force_plan
 // {HALO_CFG, shape}: tests / A/B; N <= 64 ConvTs always take the 4-wave 256 x 64 block), 4 the 8-wave 256 x 64
-// block (the automatic conv-s2 N-64 block; grids 64 wide keep 4 waves).
+// block (the automatic conv-s2 N-64 block; grids 64 wide keep 4 waves), 5 (ConvT, N <= 64) one phase per block
+// (GEOM 1) instead of the automatic phase pair (GEOM 4, the 4-wave 256 x 64 block; automatic when its grid has >= 256
+// blocks), 6 (ConvT, N <= 64) the phase pair at any size.  (N = 128 ConvTs keep one phase per block: the phase pair
+// needs 8 waves of 64 x 64 there -- two 4-wave accumulator sets of 128 x 64 do not fit -- and measured 75 us against
+// 65 for d2 at bs 32, profiles/r05/halo_t2/.)
 int halo_launch(GParams& p, hipStream_t st, int shape) {
   const bool convt = p.nphase == 4;
   const int geom = convt ? 1 : (p.in_stride == 2 ? 0 : (p.stepy > 0 ? 2 : 3));
@@ -442,7 +468,10 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
   p.ksplit = 1;
   p.kchunk = p.K;
   p.phase_major = 0;
-  const int blocks = p.mtiles * p.ntiles * p.nphase;
+  // ConvT: the two phases of a row parity per block (GEOM 4) when that still fills the chip (shape 5: one phase per
+  // block, GEOM 1 -- tests / A/B)
+  const bool t2 = convt && bn == 64 && (shape == 6 || (shape != 5 && p.mtiles * p.ntiles * 2 >= 256));
+  const int blocks = p.mtiles * p.ntiles * (t2 ? 2 : p.nphase);
   const dim3 grid((unsigned)blocks);
   const bool bnb = p.part2 != nullptr;
   // >= 512 blocks: the 4-wave 80 KiB block, two per CU; fewer: the 8-wave block (one per CU, all CUs busy)
@@ -455,7 +484,7 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
   const bool n64_8w = shape != 3;
 #define STC_HK(G_, GW_, BN_, B_, RB_, WM_, WN_)                                                               \
   hipLaunchKernelGGL((halo_conv_kernel<G_, GW_, BN_, B_, RB_, WM_, WN_>), grid, dim3(64 * WM_ * WN_),         \
-                     (HaloGeom<RB_, BN_>::LDS), st, p)
+                     (HaloGeom<RB_, BN_, (G_ == 4 ? 4 : 2)>::LDS), st, p)
 #define STC_HB(G_, GW_, BN_, RB_, WM_, WN_) \
   if (bnb) STC_HK(G_, GW_, BN_, true, RB_, WM_, WN_); else STC_HK(G_, GW_, BN_, false, RB_, WM_, WN_);
 #define STC_H(GW_)                                          \
@@ -467,6 +496,8 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
       }                                                     \
       else if (two) { STC_HB(0, GW_, 128, 64, 2, 2) }       \
       else { STC_HB(0, GW_, 128, 128, 4, 2) }               \
+    } else if (t2) {                                        \
+      STC_HB(4, GW_, 64, 64, 4, 1)                          \
     } else if (bn == 64) {                                  \
       STC_HB(1, GW_, 64, 64, 4, 1)                          \
     } else {                                                \

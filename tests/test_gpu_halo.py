@@ -24,6 +24,8 @@ HALO = (ops.HALO_CFG, 1)   # the 8-wave block (one per CU)
 HALO2 = (ops.HALO_CFG, 2)  # the 4-wave block (two per CU)
 HALO64 = (ops.HALO_CFG, 3)  # the 4-wave 256 x 64 block (conv-s2)
 HALO64W8 = (ops.HALO_CFG, 4)  # the 8-wave 256 x 64 block (conv-s2, grids <= 32 wide; else the 4-wave one)
+HALO_G1 = (ops.HALO_CFG, 5)  # ConvT: one phase per block
+HALO_T2 = (ops.HALO_CFG, 6)  # ConvT: the two phases of a row parity per block, at any size
 
 
 def nhwc(t):
@@ -229,7 +231,7 @@ TCASES = [  # B, Cin, Cout, GH, GW (input grid)
 ]
 
 
-@pytest.mark.parametrize("shape", [HALO, HALO2], ids=["8wave", "4wave"])
+@pytest.mark.parametrize("shape", [HALO, HALO2, HALO_T2], ids=["8wave", "4wave", "phase_pair"])
 @pytest.mark.parametrize("case", TCASES, ids=lambda c: "x".join(map(str, c)))
 def test_halo_convT(case, shape):
     B, Cin, Cout, GH, GW = case
@@ -242,6 +244,21 @@ def test_halo_convT(case, shape):
     y2, _, _, plan2 = run_t(B, x, w, Cin, Cout, GH, GW, (0, 1))
     assert plan2[4] == 0
     assert float((y - y2).abs().max()) <= 1e-2 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("case", [(32, 256, 64, 64, 64), (32, 128, 64, 64, 64)], ids=["d1", "e2_dgrad_geometry"])
+def test_halo_convT_phase_pair_equals_single_phase(case):
+    """The phase-pair block (GEOM 4, automatic at these train-step sizes) sums every phase's taps in the single-phase
+    block's order (the same 4 x 1 waves of 64 x 64): outputs and BatchNorm partials bit-identical to GEOM 1, and
+    within bf16 rounding of torch."""
+    B, Cin, Cout, GH, GW = case
+    x = q(rnd(B, Cin, GH, GW, seed=21, dev=DEV))
+    w = q(rnd(Cin, Cout, 4, 4, seed=22, scale=0.05, dev=DEV))
+    y1, m1, v1, _ = run_t(B, x, w, Cin, Cout, GH, GW, None)
+    y2, m2, v2, _ = run_t(B, x, w, Cin, Cout, GH, GW, HALO_G1)
+    assert torch.equal(y1, y2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    ref = F.conv_transpose2d(x, w, None, 2, 1)
+    check(y1, ref, m1, v1, f"halo convT phase pair {case}")
 
 
 def test_halo_convT_plan_automatic_at_train_sizes():
