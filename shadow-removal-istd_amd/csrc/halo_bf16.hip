@@ -199,7 +199,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
     dma16(ra, sA + (wave * AG + g) * 1024, ((a_off[g] + delta) * 2u) | (((pen >> g) & 1u) << 31));
   };
   auto piece_b = [&](char* sB, unsigned k0, int j, int h) {
+#if !STC_EXP_NOBDMA  // (diagnostic builds: the B stream compiled out)
     dma16(rb, sB + j * G::B + (wave * BG + h) * 1024, ((b_off[h] + k0) * 2u) | (b_off[h] & OOB));
+#endif
   };
   auto issue_a = [&](int ss, int aslot) {
     unsigned delta, pen;
@@ -238,6 +240,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
     b_rd[kk] = (wn * TN + rl) * RB + (((4 * kk + kq) ^ hswz<RB>(rl)) * 16);
   }
   const bf16x8_t zero8 = {};
+#if STC_EXP_NOBREAD
+  bf16x8_t fb0[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) fb0[j] = reinterpret_cast<const bf16x8_t*>(p.b)[(lane + 64 * j) & 255];
+#endif
 
   // one K-step (RB / 2 deep) from A stage sA / B K-step sBj, A rows shifted by D in [-2, 2]; dma(k) issues LDS-DMA
   // piece k of the future stages after each 8 MFMAs
@@ -256,8 +263,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
     for (int kk = 0; kk < KK; ++kk) {
       const int ard = RT ? (dr < 0 ? a_rd[1][kk] : (dr > 0 ? a_rd[3][kk] : a_rd[2][kk])) : a_rd[(RT ? 0 : D) + 2][kk];
       bf16x8_t fa[FM], fb[FN];
+#if STC_EXP_NOBREAD  // (diagnostic builds: B fragments from registers -- no LDS reads of B)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = fb0[j];
+#else
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8_t*>(sBj + b_rd[kk] + j * 16 * RB);
+#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         fa[i] = *reinterpret_cast<const bf16x8_t*>(sA + ard + i * 16 * RB);

@@ -375,9 +375,16 @@ class Adam(torch.optim.Optimizer):
         """Host step counts of group ``gi`` from its device counter: parameters whose update of this step already
         ran (``updated``: ids) get the count this step reaches, the others the count before it."""
         d, f = self._dev.get(gi), self._fast.get(gi)
-        if d is None or f is None:  # (no steady-state record, e.g. after load_state_dict: the host state rules)
+        if d is None:
             return
         s = int(d["step"].item())
+        if f is None:  # (no steady-state record, e.g. after load_state_dict -- which set the counter -- and replays)
+            for p in self.param_groups[gi]["params"]:
+                st = self.state.get(p)
+                if st and "step" in st:
+                    st["step"].fill_(float(s))
+                    self._steps.pop(id(p), None)
+            return
         if gi in self._ov_coef:  # this step's advance already happened (overlapped bucket updates)
             s -= 1
         for p, st in zip(f["plist"], f["step_tensors"]):
@@ -393,7 +400,12 @@ class Adam(torch.optim.Optimizer):
         for gi, d in self._dev.items():
             s = int(d["step"].item())
             f = self._fast.get(gi)
-            if f is None:
+            if f is None:  # (no steady-state record -- e.g. replays after load_state_dict: every state of the group)
+                for p in self.param_groups[gi]["params"]:
+                    st = self.state.get(p)
+                    if st and "step" in st:
+                        st["step"].fill_(float(s))
+                        self._steps.pop(id(p), None)
                 continue
             f["step"] = s
             for p, st in zip(f["plist"], f["step_tensors"]):

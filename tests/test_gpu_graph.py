@@ -134,3 +134,10 @@ def test_replay_after_optimizer_state_load():
     replay()
     bad = _same(_state(eager), _state(graphed))
     assert not bad, bad[:8]
+    # then a replay and an eager (general-path) step of the captured trainer: the step counts carry over
+    eager.train_step(x, m, y)
+    replay()
+    eager.train_step(x, m, y)
+    graphed.train_step(x, m, y)
+    bad = _same(_state(eager), _state(graphed))
+    assert not bad, bad[:8]
