@@ -6,7 +6,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
-ad = [i for i, v in enumerate(iv) if v[2].startswith("stc::adam_pack")]
+ad = [i for i, v in enumerate(iv) if "adam_pack" in v[2]]
 seg = iv[ad[-3]:ad[-1] + 1]
 t0 = seg[0][1]
 cur_e, gaps = seg[0][1], []
