@@ -42,6 +42,10 @@ struct WbParams {
   // (b0, oy0, ox0), advanced in scalar registers, plus a per-lane constant -- no per-step VALU division.
   int pmode, lg_gw, lg_ghw;
   int mtiles, ntiles;
+  // column order of the Gcol operand: 0 tap-major (col = tap*Cg + ci: a tile column range = one tap's channels);
+  // 1 channel-group-major (col = (ci/8)*128 + tap*8 + ci%8: a 128-column tile = 8 channels x all 16 taps, whose
+  // dW[r][ci][tap] rows are one contiguous 512-byte run -- stored from the tile, no transposing reduce)
+  int cmajor;
   float* ws;
   float* dW;
 };
@@ -102,6 +106,32 @@ __device__ __forceinline__ void wgrad_store(const WbParams& p, floatx4 (&acc)[BM
     if (slab) slab[(long long)r * p.Ncol + n] = v;
     else if (cc < p.Cg_out) p.dW[((long long)r * p.Cg_out + cc) * 16 + tt] = v;
   };
+  if constexpr (!SWAP) {
+    if (p.cmajor) {
+      // channel-group-major columns (one split): the tile through LDS ([BM][BN + 4] fp32, the stages' space), then
+      // every dW row's 512-byte runs as 16-byte stores: dest float 16 c8 + t of group g = tile column 128 g + 8 t + c8
+      extern __shared__ __attribute__((aligned(16))) char smem[];
+      float* tl = reinterpret_cast<float*>(smem);
+      constexpr int PT = BN + 4, NT = 64 * WM * WN;
+      __syncthreads();  // (the compute waves are done with the stages; loader waves have left)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) tl[(wm * TM + 16 * i + rq + e) * PT + wn * TN + 16 * j + cl] = acc[i][j][e];
+      __syncthreads();
+      for (int idx = (int)threadIdx.x; idx < BM * BN / 4; idx += NT) {
+        const int row = idx / (BN / 4), d = (idx - row * (BN / 4)) * 4;  // d: dest float of the row's BN
+        const int g = d >> 7, c8 = (d >> 4) & 7, t0 = d & 15;
+        const int r = a0 + row, ch = ((b0 >> 7) + g) * 8 + c8;
+        if (r >= p.R || ch >= p.Cg_out || b0 + 128 * g >= p.Ncol) continue;
+        const float* q = tl + row * PT + 128 * g + 8 * t0 + c8;
+        *reinterpret_cast<float4*>(p.dW + ((long long)r * p.Cg_out + ch) * 16 + t0) = make_float4(q[0], q[8], q[16], q[24]);
+      }
+      return;
+    }
+  }
   if (!SWAP && slab) {  // the common split case: plain row-major slab, no tap decomposition
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -121,7 +151,7 @@ __device__ __forceinline__ void wgrad_store(const WbParams& p, floatx4 (&acc)[BM
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = b0 + wn * TN + 16 * j + cl;
-      const int tt = n / p.Cg, cc = n - tt * p.Cg;
+      const int tt = p.cmajor ? (n >> 3) & 15 : n / p.Cg, cc = p.cmajor ? ((n >> 7) << 3) + (n & 7) : n - tt * p.Cg;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -204,8 +234,8 @@ __device__ __forceinline__ void wgrad_bf16_body(const WbParams& p) {
       ro.pen = r < p.R ? 0u : OOBV;
     } else {
       const int col = first + chunk * 8;
-      const int tap = col / p.Cg;
-      ro.chan_off = p.g_co + col - tap * p.Cg;
+      const int tap = p.cmajor ? (col >> 3) & 15 : col / p.Cg;
+      ro.chan_off = p.g_co + (p.cmajor ? (col >> 7) << 3 : col - tap * p.Cg);
       ro.dy = (tap >> 2) - 1;
       ro.dx = (tap & 3) - 1;
       ro.pen = col < p.Ncol ? 0u : OOBV;
@@ -719,7 +749,8 @@ constexpr int kNumWbCfg = sizeof(kWbCfg) / sizeof(kWbCfg[0]);
 
 struct WbPlan {
   int cfg, BM, BN, mtiles, ntiles, nsplit, pchunk;
-  bool slab;  // partial sums go to fp32 slabs + the ordered reduce (always when nsplit > 1)
+  bool slab;    // partial sums go to fp32 slabs + the ordered reduce (always when nsplit > 1)
+  bool cmajor;  // channel-group-major columns (WbParams::cmajor): one split whose tiles store torch layout directly
 };
 
 // The halo tile (cfg WB_HALO) takes the stride-2 geometry on a D grid of width 16..128 (power of two; a K-step
@@ -735,7 +766,8 @@ static bool wb_halo_ok(int GH, int GW, int stride, int R, int Cg) {
   return GH % (64 / std::min(GW, 64)) == 0;
 }
 
-// force (optional, per call: stc_conv_wgrad_ex / stc_conv_wgrad_query): {tile config, pixel splits (0 = auto)};
+// force (optional, per call: stc_conv_wgrad_ex / stc_conv_wgrad_query): {tile config, pixel splits (0 = auto; -1 =
+// auto without the channel-group-major direct store)};
 // NULL or an unknown config = the automatic plan (also the halo config where the geometry does not allow it)
 static WbPlan wb_plan(int B, int GH, int GW, int stride, int R, int Cg, const int32_t* force) {
   WbPlan pl{};
@@ -784,6 +816,12 @@ static WbPlan wb_plan(int B, int GH, int GW, int stride, int R, int Cg, const in
   // range covers every tap of its channels (16*Cg <= BN); otherwise those stores are 4-byte scatters at
   // a 64-byte stride (measured ~30 us for a 16.8 MB dW) and the slab + coalesced transposing reduce wins.
   pl.slab = pl.nsplit > 1 || (!c.swap && 16LL * Cg > c.BN && cfg != WB_HALO);
+  // ... unless the tile width is a multiple of 128 columns = 8 channels x 16 taps: with the channel-group-major
+  // column order each tile row is whole 512-byte runs of dW (the deep levels' single-split gradients: no reduce)
+  pl.cmajor = pl.nsplit == 1 && pl.slab && !c.swap && cfg != WB_HALO && c.BN % 128 == 0 && Cg % 8 == 0 &&
+              (long long)c.stages * WB_BK * (c.BM + c.BN) * 2 >= (long long)c.BM * (c.BN + 4) * 4 &&  // (LDS tile)
+              !(force && force[1] < 0);  // (force {cfg, -1}: the tap-major slab + reduce -- tests / A/B)
+  if (pl.cmajor) pl.slab = false;
   return pl;
 }
 static int64_t wb_ws(const WbPlan& pl, int R, int Cg) { return pl.slab ? (int64_t)pl.nsplit * R * 16LL * Cg * 4 : 0; }
@@ -839,6 +877,7 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
     p.P = B * p.GH * p.GW;
   }
   p.mtiles = pl.mtiles; p.ntiles = pl.ntiles; p.nsplit = pl.nsplit; p.pchunk = pl.pchunk;
+  p.cmajor = pl.cmajor ? 1 : 0;
   dim3 grid(pl.mtiles * pl.ntiles, 1, pl.nsplit);
   const int htc = std::min(p.GW, 64);
   const size_t lds = pl.cfg == WB_HALO

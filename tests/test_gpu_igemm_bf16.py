@@ -403,6 +403,29 @@ def test_wgrad_bf16_forced_tiles(case, cfg, ns):
     test_wgrad_bf16_dma(case, force=(cfg, ns))
 
 
+@pytest.mark.parametrize("case", [("convT", 2, 2, 1024, 512, 2, 2), ("conv", 2, 4, 512, 512, 4, 4),
+                                  ("convT", 2, 32, 1024, 512, 4, 4), ("conv", 2, 32, 512, 512, 8, 8),
+                                  ("conv", 2, 3, 32, 96, 10, 14)],
+                         ids=lambda c: "_".join(map(str, c)))
+def test_wgrad_channel_major_direct_store(case):
+    """Single-split weight gradients whose tiles are wider than one tap's channels store torch layout from the tile
+    with channel-group-major columns (8 channels x 16 taps per 128 columns, no transposing reduce): bit-identical
+    to the tap-major slab + reduce (force {-1, -1}), and the plan reports no slab."""
+    kind, s, B, Cin, Cout, H, W = case
+    x = nhwc(q(rnd(B, Cin, H, W, seed=71))).to(DEV, BF)
+    if kind == "conv":
+        Ho, Wo = (H + 1) // 2, (W + 1) // 2
+        dy = nhwc(q(rnd(B, Cout, Ho, Wo, seed=72))).to(DEV, BF)
+        D, R, G, Cg = dy, Cout, x, Cin
+    else:
+        dy = nhwc(q(rnd(B, Cout, 2 * H, 2 * W, seed=73))).to(DEV, BF)
+        D, R, G, Cg = x, Cin, dy, Cout
+    a = ops.wgrad(B, s, L.nhwc_view(D), R, L.nhwc_view(G), Cg, Cg, BF, device=DEV)
+    b = ops.wgrad(B, s, L.nhwc_view(D), R, L.nhwc_view(G), Cg, Cg, BF, device=DEV, force=(-1, -1))
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B,Cin,H,W,rows,dt", [(4, 512, 31, 31, 1, BF), (2, 64, 9, 13, 2, BF), (3, 128, 17, 5, 1, torch.float32),
                                               (1, 64, 6, 7, 2, torch.float32), (32, 512, 31, 31, 1, BF)])
 def test_wgrad_rows_narrow_s1(B, Cin, H, W, rows, dt):
