@@ -239,6 +239,8 @@ def kernel_name(kind, B, gh, gw, cin, cout, dt, bnb=False):
         blocks = B * vh * vw // 256 * ((cout + bn - 1) // bn) * (4 if convt else 1)
         if bn == 64:  # (csrc/halo_bf16.hip halo_launch: conv-s2 grids <= 32 wide take the 8-wave 256 x 64 block)
             rb, wm, wn = (128, 8, 1) if (kind == L.CONV_S2 and vw <= 32) else (64, 4, 1)
+            if convt and blocks // 2 >= 256:  # (the ConvT phase pair, GEOM 4: two phases per block)
+                geom = 4
         else:
             rb, wm, wn = (64, 2, 2) if blocks >= 512 else (128, 4, 2)
         return (f"halo_conv_kernel<{geom}, {vw}, {bn}, {str(bnb).lower()}, {rb}, {wm}, {wn}>", True)
