@@ -87,8 +87,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   constexpr int TH = BM / GW;
   constexpr int AH = S1 ? AG / 2 : AG;                       // A pieces per super-step (S1: a stage over two)
   constexpr int NP = NB * BG + AH, NG = NB * KK * FM / 2;    // DMA pieces / 8-MFMA groups per super-step and wave
-  static_assert(GW % 16 == 0 && BM % GW == 0 && TM % GW == 0 && FN == 4 && FM % 2 == 0 && BG >= 1,
-                "whole output rows per tile and per wave, 16-row fragments inside an output row");
+  static_assert((GW % 16 == 0 || GW == 8) && BM % GW == 0 && TM % GW == 0 && FN == 4 && FM % 2 == 0 && BG >= 1,
+                "whole output rows per tile and per wave; 16-row fragments inside an output row or two whole 8-wide rows");
   static_assert(S1 ? AG % 2 == 0 : (T2 || NP >= NG), "every MFMA group issues a piece (S1: whole halves of a stage)");
   static_assert(BM * (BN * 2 + 16) + WM * BN * 16 <= G::LDS, "epilogue tile + statistics merge area");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -111,8 +111,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   const int py = ph >> 1, px = ph & 1;
   const int mt = bid / p.ntiles, nt = bid % p.ntiles;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int tiles_img = p.GH / TH;
-  const int img = mt / tiles_img, oy0 = (mt - img * tiles_img) * TH;
+  // (a tile = TH whole grid rows; an 8-wide grid's 32-row tile spans GH-row images: image and row per DMA row below)
 
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, (short)0, (int)p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, (int)p.b_bytes, 0x00020000);
@@ -130,7 +129,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
   for (int g = 0; g < AG; ++g) {
     const int pos = (wave * AG + g) * G::PR + prow;
     const int r = pos / GW, c = pos % GW;
-    const int oy = oy0 + r;
+    const int gr = mt * TH + r;  // grid row of the whole batch
+    const int img = gr / p.GH, oy = gr - img * p.GH;
     const int s_ = GEOM == 0 ? 2 : 1;  // input rows / columns per grid step
     a_off[g] = (unsigned)(img * p.a_bs + p.a_co) + (unsigned)(s_ * oy) * (unsigned)p.a_rs +
                (unsigned)(s_ * c) * (unsigned)p.a_ps + (unsigned)(schunk * 8);
@@ -257,8 +257,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
     constexpr int PH = decltype(Pc)::value;  // accumulator set (T2: the phase of the pair)
     constexpr bool RT = D == DRT;
     // edge lanes: the first -d (d < 0) / last d (d > 0) rows of an output row read padding
-    const bool mlo = RT ? (dr < 0 && rl == 0) : (D < 0 && rl < -D);
-    const bool mhi = RT ? (dr > 0 && rl == 15) : (D > 0 && rl >= 16 - D);
+    // (GW = 8: a fragment is two grid rows -- lanes 0 / 8 start one, 7 / 15 end one)
+    constexpr int RM = GW < 16 ? GW : 16;
+    const bool mlo = RT ? (dr < 0 && rl % RM == 0) : (D < 0 && rl % RM < -D);
+    const bool mhi = RT ? (dr > 0 && rl % RM == RM - 1) : (D > 0 && rl % RM >= RM - D);
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       const int ard = RT ? (dr < 0 ? a_rd[1][kk] : (dr > 0 ? a_rd[3][kk] : a_rd[2][kk])) : a_rd[(RT ? 0 : D) + 2][kk];
@@ -276,10 +278,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
         // the fragment's first (d = -1) / last (d = +1) row is an output row's left / right edge: that lane's
         // operand is the zero padding, not the neighbouring row's pixel it addressed
         if constexpr (RT || D < 0) {
-          if ((16 * i) % GW == 0) fa[i] = mlo ? zero8 : fa[i];
+          if (GW < 16 || (16 * i) % GW == 0) fa[i] = mlo ? zero8 : fa[i];
         }
         if constexpr (RT || D > 0) {
-          if ((16 * i + 16) % GW == 0) fa[i] = mhi ? zero8 : fa[i];
+          if (GW < 16 || (16 * i + 16) % GW == 0) fa[i] = mhi ? zero8 : fa[i];
         }
       }
 #pragma unroll
@@ -401,7 +403,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 8 / (WM * WN)) halo_conv_kernel(
 // 256 x 64 block, 8 waves of 32 x 64); force shapes 3 / 4 take the 64-channel tile (4 / 8 waves) for any conv-s2
 // layer (tests / A/B).
 static int halo_bn(int kind, long long mtiles, int Cout, int shape) {
-  if (kind == STC_CONVT_S2) return Cout <= 64 ? 64 : HB_BN;
+  // (ConvT: 64 channels for N <= 64, and where 128-channel tiles leave the chip below 256 blocks while 64-channel
+  // ones fill it -- the 8 x 8 grid at bs 32: d4 and the input gradient of the 16 -> 8 conv)
+  if (kind == STC_CONVT_S2)
+    return Cout <= 64 || (mtiles * 4 * ((Cout + HB_BN - 1) / HB_BN) < 256 && mtiles * 4 * ((Cout + 63) / 64) >= 256) ? 64
+                                                                                                                       : HB_BN;
   if (kind != STC_CONV_S2 || shape == 1 || shape == 2) return HB_BN;
   if (shape == 3 || shape == 4) return 64;
   return mtiles * ((Cout + HB_BN - 1) / HB_BN) < 256 && mtiles * ((Cout + 63) / 64) >= 256 ? 64 : HB_BN;
@@ -418,7 +424,13 @@ bool halo_geometry_ok(int kind, int B, int GH, int GW, int Cin, int Cout) {
   if (kind != STC_CONV_S2 && kind != STC_CONVT_S2 && kind != STC_CONV_S1 && kind != STC_CONV_S1_DGRAD) return false;
   if (Cin % 64 != 0 || Cout % 8 != 0 || Cout > 2048) return false;
   halo_grid(kind, GH, GW);
-  if (!(GW == 16 || GW == 32 || GW == 64) || GH % (HB_BM / GW) != 0) return false;
+  // (8-wide grids: a 256-row tile is 32 grid rows, spanning images -- the conv-s2 / ConvT geometries only)
+  if (GW == 8) {
+    if (kind != STC_CONV_S2 && kind != STC_CONVT_S2) return false;
+    if ((long long)B * GH * GW % HB_BM != 0) return false;
+  } else if (!(GW == 16 || GW == 32 || GW == 64) || GH % (HB_BM / GW) != 0) {
+    return false;
+  }
   if ((kind == STC_CONV_S1 || kind == STC_CONV_S1_DGRAD) && GW != 32) return false;
   return 16ll * Cin * Cout * 2 < (1ll << 31);
 }
@@ -529,6 +541,7 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
     }
   } else {
     switch (p.GW) {
+      STC_H(8)
       STC_H(16)
       STC_H(32)
       STC_H(64)

@@ -80,6 +80,8 @@ CASES = [  # B, Cin, Cout, GH, GW
     (1, 256, 512, 16, 16),   # 16 rows per tile (a whole 16x16 image), 4 chunks (e4)
     (3, 64, 96, 4, 64),      # ragged N (96 of a 128 tile), 3 images
     (1, 192, 40, 8, 32),     # 3 chunks, N = 40
+    (4, 128, 128, 8, 8),     # 8-wide grid: a 256-row tile = 4 whole 8 x 8 images
+    (8, 64, 64, 4, 8),       # 8-wide grid, 4-row images: a tile spans 8 images
 ]
 
 
@@ -228,6 +230,8 @@ TCASES = [  # B, Cin, Cout, GH, GW (input grid)
     (3, 64, 96, 4, 64),      # ragged N
     (2, 128, 64, 8, 64),     # N = 64: the 256 x 64 tile
     (1, 192, 40, 8, 32),     # N = 40 on the 256 x 64 tile, 3 chunks
+    (4, 128, 128, 8, 8),     # 8-wide grid (tiles span images): the d4 geometry
+    (8, 64, 64, 4, 8),
 ]
 
 
@@ -267,7 +271,10 @@ def test_halo_convT_plan_automatic_at_train_sizes():
     for (gh, cin, cout) in ((32, 512, 128), (16, 1024, 256), (64, 256, 64), (32, 256, 128), (16, 512, 256),
                             (64, 128, 64)):
         assert ops.conv_query(L.CONVT_S2, 32, gh, gh, cin, cout, BF)[2][4] == ops.HALO_CFG, (gh, cin, cout)
-    for (gh, cin, cout) in ((128, 128, 1), (8, 1024, 512), (4, 1024, 512)):
+    # d4 (8 x 8 grid, 1024 -> 512): the 256 x 64 block (256 blocks; 128-channel tiles would leave half the chip idle)
+    plan = ops.conv_query(L.CONVT_S2, 32, 8, 8, 1024, 512, BF)[2]
+    assert plan[4] == ops.HALO_CFG and plan[1] == 64
+    for (gh, cin, cout) in ((128, 128, 1), (4, 1024, 512)):
         assert ops.conv_query(L.CONVT_S2, 32, gh, gh, cin, cout, BF)[2][4] != ops.HALO_CFG, (gh, cin, cout)
 
 

@@ -320,6 +320,20 @@ def test_gather_scatter_roundtrip():
     close(outs[2], y, tol=0.0, what="scatter y")
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("chans,H,W", [((3,), 16, 32), ((3, 1), 32, 64), ((3, 1, 3), 16, 16), ((4,), 64, 12)])
+def test_gather_runs(dt, chans, H, W):
+    """The vectorised gather (gather4: W % 4 == 0, aligned planes): NCHW fp32 sources -> NHWC [B, H, W, Cpad], exact
+    (bf16: the round-to-nearest-even cast), padding channels zero."""
+    B = 3
+    srcs = [rnd(B, c, H, W, seed=200 + i) for i, c in enumerate(chans)]
+    cpad = 8 if dt == torch.bfloat16 or sum(chans) > 4 else 4
+    dst = torch.full((B, H, W, cpad), float("nan"), device=DEV, dtype=dt)
+    ops.gather([t.to(DEV) for t in srcs], dst, dt)
+    ref = torch.cat(srcs + [torch.zeros(B, cpad - sum(chans), H, W)], 1).to(dt)
+    assert torch.equal(nchw(dst).cpu(), ref)
+
+
 def test_tanh_bias_bwd_and_chan_sum():
     y = torch.tanh(rnd(2, 3, 8, 8, seed=101))
     gy = rnd(2, 3, 8, 8, seed=102)
