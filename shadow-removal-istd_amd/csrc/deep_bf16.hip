@@ -181,18 +181,10 @@ __global__ void __launch_bounds__(256) deep_conv_kernel(const DeepParams p) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-#ifndef DEEP_ORDER
-#define DEEP_ORDER 0
-#endif
   const int split = bid % p.ksplit;
   const int tq = bid / p.ksplit;  // (phase, column, row tile)
-#if DEEP_ORDER == 0
   const int mt = tq % p.mtiles;
   const int nt = (tq / p.mtiles) % p.ntiles;
-#else  // (experiment: row-major tiles, the column fastest)
-  const int nt = tq % p.ntiles;
-  const int mt = (tq / p.ntiles) % p.mtiles;
-#endif
   const int ph = tq / (p.mtiles * p.ntiles);
   const int tile = (ph * p.mtiles + mt) * p.ntiles + nt;  // (slab / ticket index)
   const int py = ph >> 1, px = ph & 1;

@@ -186,6 +186,10 @@ __global__ void __launch_bounds__(256) stem_conv_kernel(const GParams p) {
             }
           }
         } else {
+#if STC_EXP_NOSTORE  // (diagnostic builds: the output stores compiled out -- what the stream of stores costs)
+          if (tv.x == 0x12345678u) *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + o1) = act_bf16x8(tv, p.act_s1);
+          continue;
+#endif
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + o1) = act_bf16x8(tv, p.act_s1);
           if constexpr (MODE == 2) {
             const long long o2 = (long long)img * p.c2_bs + (long long)oy * p.c2_rs + (long long)oxs * p.c2_ps + p.c2_co +
