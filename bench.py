@@ -67,6 +67,7 @@ def parse():
     ap.add_argument("--dtype", default=os.environ.get("STC_BENCH_DTYPE", "bf16"), choices=["fp32", "bf16"])
     ap.add_argument("--graph", action="store_true", help="replay the step captured as one HIP graph "
                     "(STCGAN.capture; the same kernels, bit-identical results) instead of eager steps")
+    ap.add_argument("--no-lanes", action="store_true", help="discriminators on the main stream (no side lanes; A/B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the parity / other-config measurements")
     ap.add_argument("--cpu-batch", type=int, default=32, help="batch of the timed CPU train step (C3: 32)")
@@ -473,10 +474,12 @@ def main():
     for net in (tr.G1, tr.G2, tr.D1, tr.D2):
         net.train()
 
-    step, mode = (lambda: tr.train_step(x, m, y)), "eager"
+    if args.no_lanes:
+        tr.streams = False
+    step, mode = (lambda: tr.train_step(x, m, y)), "eager" + ("-nolanes" if args.no_lanes else "")
     if args.graph:
         try:  # (a capture failure, e.g. a backend that cannot be captured, falls back to eager steps)
-            step, mode = tr.capture(x, m, y, warmup=1), "hip-graph"
+            step, mode = tr.capture(x, m, y, warmup=1), "hip-graph" + ("-nolanes" if args.no_lanes else "")
         except Exception as e:  # noqa: BLE001
             print(f"bench: graph capture failed ({type(e).__name__}: {e}); eager steps", file=sys.stderr)
             torch.cuda.synchronize()

@@ -190,6 +190,11 @@ int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src, const void
 /* diagnostics (scripts/deep_tune.py --phases): the next stc_deep_conv launch writes 8 wall-clock stamps per block
  * (start, tables, K loop done, reduce, statistics, finalize, end) into stamps[blocks][8]; NULL clears.          */
 int stc_deep_debug_next(void* stamps);
+/* split-K forward / input-gradient GEMMs (bf16): 1 (default) = the slabs are combined inside the launch by each
+ * tile's last-arriving block (a ticket per tile) and it runs the epilogue; 0 = a separate reduction launch (A/B).
+ * on < 0 only queries.  Returns the previous setting.  Workspace sizes and statistics chunk counts
+ * (stc_conv_fwd_query / stc_conv_bwd_bn_chunks) follow the setting: query after changing it.                     */
+int stc_set_splitk_inlaunch(int on);
 
 /* ---- weight gradient ---------------------------------------------------------
  * dW[r][ci][kh][kw] = sum_{b,oy,ox} D[b,oy,ox,r] * G[b, oy*s+kh-1, ox*s+kw-1, ci]

@@ -12,7 +12,7 @@ import types
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VARIANTS = ["one_stream", "wgrad_lane", "lanes", "lanes_no_optim", "lanes_ngf16_fp32", "lanes_forward_only",
-            "lanes_no_wgrad_lane"]
+            "lanes_no_wgrad_lane", "lanes_side"]
 
 
 def run(variant):
@@ -21,6 +21,7 @@ def run(variant):
     from stcgan_amd import engine
     from stcgan_amd.stcgan import STCGAN
     engine.WGRAD_OVERLAP = variant not in ("one_stream", "lanes_no_wgrad_lane")
+    engine.SIDE_IN_CAPTURE = variant == "lanes_side"  # the lanes' weight-gradient side streams kept in the capture
     ngf, dt = (16, "fp32") if variant.endswith("fp32") else (64, "bf16")
     a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5, beta2=0.999,
                               D_loss_fn="standard", D_loss_type="normal", ngf=ngf, dtype=dt,

@@ -9,6 +9,8 @@
 // Backward: dn = g1*act1'(n) + g2*act2'(n) is recomputed on the fly from the raw
 // input (n = x*scale + shift), reduced to sum(dn), sum(dn*xhat), then applied.
 // All reductions are fixed-order => bitwise reproducible.
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace stc {
@@ -175,20 +177,16 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int
                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  double n = 0, sm = 0, m2 = 0;
-  if (nchunks <= 1024) {
-    // one load: every thread keeps its (up to) 4 chunk partials in registers for both passes
-    float4 pp[4];
-    load4(threadIdx.x, pp);
+  const BnPre pre = bn_pre(c, gamma, beta, rmean, rvar);  // (issued with the partials' loads)
+  auto sum1 = [&](const float4* pp, double& n, double& sm) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (pp[u].x <= 0.f) continue;
       n += pp[u].x;
       sm += (double)pp[u].x * pp[u].w + (double)pp[u].y;  // n_b * m_b = n_b*shift + S1
     }
-    const double N = block_sum256(n, sh);
-    const double S = block_sum256(sm, sh);
-    const double mu = N > 0 ? S / N : 0.0;
+  };
+  auto sum2 = [&](const float4* pp, double mu, double& m2) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (pp[u].x <= 0.f) continue;
@@ -198,42 +196,50 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* part, int
       const double d = (double)pp[u].w + r - mu;
       m2 += q + nb * d * d;
     }
-    n = N;
+  };
+  // up to 4096 chunks: every thread loads its (up to) 4 groups of 4 partials at once and keeps them in registers
+  // for both passes (one memory latency); the sums run in the loop's order below, so the results are the same
+  auto in_regs = [&](auto Gc, double& n, double& sm, double& m2) {
+    constexpr int G = decltype(Gc)::value;
+    float4 pp[G][4];
+#pragma unroll
+    for (int g = 0; g < G; ++g) load4(threadIdx.x + 1024 * g, pp[g]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) sum1(pp[g], n, sm);
+    n = block_sum256(n, sh);
+    sm = block_sum256(sm, sh);
+    const double mu = n > 0 ? sm / n : 0.0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) sum2(pp[g], mu, m2);
     sm = mu;
+  };
+  double n = 0, sm = 0, m2 = 0;
+  if (nchunks <= 1024) {
+    in_regs(std::integral_constant<int, 1>{}, n, sm, m2);
+  } else if (nchunks <= 2048) {
+    in_regs(std::integral_constant<int, 2>{}, n, sm, m2);
+  } else if (nchunks <= 4096) {
+    in_regs(std::integral_constant<int, 4>{}, n, sm, m2);
   } else {
     for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {
       float4 pp[4];
       load4(k0, pp);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (pp[u].x <= 0.f) continue;
-        n += pp[u].x;
-        sm += (double)pp[u].x * pp[u].w + (double)pp[u].y;
-      }
+      sum1(pp, n, sm);
     }
-    const double N = block_sum256(n, sh);
-    const double S = block_sum256(sm, sh);
-    const double mu = N > 0 ? S / N : 0.0;
+    n = block_sum256(n, sh);
+    sm = block_sum256(sm, sh);
+    const double mu = n > 0 ? sm / n : 0.0;
     for (int k0 = threadIdx.x; k0 < nchunks; k0 += 1024) {
       float4 pp[4];
       load4(k0, pp);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (pp[u].x <= 0.f) continue;
-        const double nb = pp[u].x, s1 = pp[u].y, r = s1 / nb;
-        double q = (double)pp[u].z - s1 * r;
-        if (q < 0) q = 0;
-        const double d = (double)pp[u].w + r - mu;
-        m2 += q + nb * d * d;
-      }
+      sum2(pp, mu, m2);
     }
-    n = N;
     sm = mu;
   }
   const double N = n, mu = sm;
   const double M2 = block_sum256(m2, sh);
   if (threadIdx.x == 0)
-    bn_finalize_store(c, N, mu, M2, gamma, beta, rmean, rvar, nbt, momentum, eps, mean_o, rstd_o, scale, shift);
+    bn_finalize_store(c, N, mu, M2, pre, rmean, rvar, nbt, momentum, eps, mean_o, rstd_o, scale, shift);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -260,23 +266,16 @@ __global__ void __launch_bounds__(256) bn_finalize_wave_kernel(const float* part
                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  double n = 0, sm = 0;
-  for (int k0 = lane; k0 < nchunks; k0 += 256) {
-    float4 pp[4];
-    load4(k0, pp);
+  const BnPre pre = bn_pre(c, gamma, beta, rmean, rvar);  // (issued with the partials' loads)
+  auto sum1 = [&](const float4* pp, double& n, double& sm) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (pp[u].x <= 0.f) continue;
       n += pp[u].x;
       sm += (double)pp[u].x * pp[u].w + (double)pp[u].y;
     }
-  }
-  const double N = wave_sum(n), S = wave_sum(sm);
-  const double mu = N > 0 ? S / N : 0.0;
-  double m2 = 0;
-  for (int k0 = lane; k0 < nchunks; k0 += 256) {
-    float4 pp[4];
-    load4(k0, pp);
+  };
+  auto sum2 = [&](const float4* pp, double mu, double& m2) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (pp[u].x <= 0.f) continue;
@@ -286,10 +285,47 @@ __global__ void __launch_bounds__(256) bn_finalize_wave_kernel(const float* part
       const double d = (double)pp[u].w + r - mu;
       m2 += q + nb * d * d;
     }
+  };
+  // up to 1024 chunks: every lane loads its (up to) 4 groups of 4 partials at once and keeps them in registers for
+  // both passes (one memory latency); the sums run in the loop's order below, so the results are the same
+  auto in_regs = [&](auto Gc, double& n, double& sm, double& m2) {
+    constexpr int G = decltype(Gc)::value;
+    float4 pp[G][4];
+#pragma unroll
+    for (int g = 0; g < G; ++g) load4(lane + 256 * g, pp[g]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) sum1(pp[g], n, sm);
+    n = wave_sum(n);
+    sm = wave_sum(sm);
+    const double mu = n > 0 ? sm / n : 0.0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) sum2(pp[g], mu, m2);
+    return mu;
+  };
+  double n = 0, sm = 0, m2 = 0, mu;
+  if (nchunks <= 256) {
+    mu = in_regs(std::integral_constant<int, 1>{}, n, sm, m2);
+  } else if (nchunks <= 512) {
+    mu = in_regs(std::integral_constant<int, 2>{}, n, sm, m2);
+  } else if (nchunks <= 1024) {
+    mu = in_regs(std::integral_constant<int, 4>{}, n, sm, m2);
+  } else {
+    for (int k0 = lane; k0 < nchunks; k0 += 256) {
+      float4 pp[4];
+      load4(k0, pp);
+      sum1(pp, n, sm);
+    }
+    n = wave_sum(n);
+    sm = wave_sum(sm);
+    mu = n > 0 ? sm / n : 0.0;
+    for (int k0 = lane; k0 < nchunks; k0 += 256) {
+      float4 pp[4];
+      load4(k0, pp);
+      sum2(pp, mu, m2);
+    }
   }
   const double M2 = wave_sum(m2);
-  if (lane == 0)
-    bn_finalize_store(c, N, mu, M2, gamma, beta, rmean, rvar, nbt, momentum, eps, mean_o, rstd_o, scale, shift);
+  if (lane == 0) bn_finalize_store(c, n, mu, M2, pre, rmean, rvar, nbt, momentum, eps, mean_o, rstd_o, scale, shift);
 }
 
 // eval-mode table from running statistics
@@ -840,7 +876,7 @@ extern "C" int stc_bn_finalize(const float* part, int nchunks, int C, const floa
     hipLaunchKernelGGL(bn_eval_table_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, running_mean,
                        running_var, eps, scale, shift);
   } else {
-    if (nchunks <= 256)  // one 4-load group per lane; more chunks: a block per channel keeps more loads in flight
+    if (nchunks <= 1024)  // up to 4 load groups per lane in registers; more chunks: a block per channel
       hipLaunchKernelGGL(bn_finalize_wave_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, nchunks, C, gamma, beta,
                          running_mean, running_var, (long long*)num_batches_tracked, momentum, eps, mean, rstd, scale,
                          shift);

@@ -172,22 +172,36 @@ static inline Geometry geometry(int kind) {
   return g;
 }
 
+// channel c's affine parameters and running statistics, loaded before the merge (off its latency chain)
+struct BnPre {
+  float g, bt, rm, rv;
+};
+__device__ __forceinline__ BnPre bn_pre(int c, const float* gamma, const float* beta, const float* rmean,
+                                        const float* rvar) {
+  return BnPre{gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, rmean ? rmean[c] : 0.f, rvar ? rvar[c] : 0.f};
+}
+
 // mean / rstd / affine table / running statistics of channel c from the merged N, mean, M2
+__device__ __forceinline__ void bn_finalize_store(int c, double N, double mu, double M2, const BnPre& q, float* rmean,
+                                                  float* rvar, long long* nbt, float momentum, float eps,
+                                                  float* mean_o, float* rstd_o, float* scale, float* shift) {
+  const double var = N > 0 ? M2 / N : 0.0;
+  const float rs = (float)(1.0 / sqrt(var + (double)eps));
+  if (mean_o) mean_o[c] = (float)mu;
+  if (rstd_o) rstd_o[c] = rs;
+  const float sc = q.g * rs;
+  scale[c] = sc;
+  shift[c] = q.bt - (float)mu * sc;
+  if (rmean) rmean[c] = (1.f - momentum) * q.rm + momentum * (float)mu;
+  if (rvar) rvar[c] = (1.f - momentum) * q.rv + momentum * (float)(N > 1 ? M2 / (N - 1) : var);
+  if (nbt && c == 0) nbt[0] += 1;
+}
 __device__ __forceinline__ void bn_finalize_store(int c, double N, double mu, double M2, const float* gamma,
                                                   const float* beta, float* rmean, float* rvar, long long* nbt,
                                                   float momentum, float eps, float* mean_o, float* rstd_o,
                                                   float* scale, float* shift) {
-  const double var = N > 0 ? M2 / N : 0.0;
-  const float rs = (float)(1.0 / sqrt(var + (double)eps));
-  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  if (mean_o) mean_o[c] = (float)mu;
-  if (rstd_o) rstd_o[c] = rs;
-  const float sc = g * rs;
-  scale[c] = sc;
-  shift[c] = bt - (float)mu * sc;
-  if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mu;
-  if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)(N > 1 ? M2 / (N - 1) : var);
-  if (nbt && c == 0) nbt[0] += 1;
+  bn_finalize_store(c, N, mu, M2, bn_pre(c, gamma, beta, rmean, rvar), rmean, rvar, nbt, momentum, eps, mean_o,
+                    rstd_o, scale, shift);
 }
 
 }  // namespace stc

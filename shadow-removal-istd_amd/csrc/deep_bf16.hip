@@ -81,38 +81,9 @@ struct DeepParams {
 #define DEEP_STAMP(i) \
   do { if (p.dbg && threadIdx.x == 0) p.dbg[(long long)blockIdx.x * 8 + (i)] = wall_clock64(); } while (0)
 
-// one in-launch hand-off to the last arriver of a counter (cdna_hip_programming.md Guideline 16, the write-through
-// form): the payload is stored sc1 (write-through to memory, no release fence) and EVERY load of it is an sc1 load
-// (past every L1 and L2, so no acquire); each wave drains its stores, the barrier joins them, lane 0 adds.
-// Returns (to every thread) whether this block drew the last ticket.  The last arriver leaves the counter zero.
+// the in-launch hand-offs: last_arriver / st_sc1 / ld_sc1 (igemm_bf16.hpp)
 __device__ __forceinline__ bool deep_last_arriver(unsigned* counter, unsigned total, unsigned* flag, bool acquire) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = old == total - 1 ? 1u : 0u;
-    if (old == total - 1) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const bool last = *flag != 0u;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the sc1 loads below the ticket)
-  if (last && acquire) {  // (more than one block per CU: the measured sc1 form covers one; the agent acquire too)
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-  }
-  return last;
-}
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int SC1 = 16;  // buffer-op cache bits: sc1 (write-through stores, loads past the caches)
-__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, floatx4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, SC1);
-}
-__device__ __forceinline__ floatx4 ld_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, SC1));
+  return last_arriver(counter, total, flag, acquire);
 }
 
 // The column finisher: channel n's batch statistics from the column's tile partials {count, 0, M2, mean} (one per

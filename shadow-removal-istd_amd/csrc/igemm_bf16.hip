@@ -17,6 +17,9 @@
 //     squares, in fp32 from the accumulators) -> part[tile][n] = {count, 0, M2, mean},
 //     the format stc_bn_finalize merges (Chan's parallel variance).
 
+#include <mutex>
+#include <unordered_map>
+
 #include "igemm_bf16.hpp"
 
 namespace stc {
@@ -290,6 +293,10 @@ __device__ __forceinline__ void igemm_bf16_body(const GParams& p) {
     return;
   }
 #endif
+  if (p.tickets) {  // in-launch split-K: the tile's last arriver runs the epilogue on the summed slabs
+    __syncthreads();  // (every wave is done with the stage buffers: the hand-off flag lives in LDS)
+    if (!splitk_combine<BM, BN, WM, WN>(p, acc, (ph * p.mtiles + mt) * p.ntiles + nt, split, smem)) return;
+  }
   igemm_epilogue<BM, BN, WM, WN, BNB>(p, acc, m0, n0, ph, mt, z, smem);
 }
 
@@ -642,8 +649,52 @@ struct Bf16Problem {
   int64_t ws_bytes;
   int stats_chunks;
   int reduce_rows;
-  bool wide;  // split-K reduction by splitk_reduce_wide_kernel (a chunk per row)
+  bool wide;      // split-K reduction by splitk_reduce_wide_kernel (a chunk per row)
+  bool inlaunch;  // split-K combined in the launch (GParams::slab / tickets): the tile statistics of one launch
 };
+
+// In-launch split-K (igemm_bf16_body / splitk_combine) for the split layers that are not reduced by the wide kernel;
+// false: every split layer takes the separate reduction launch (A/B)
+static bool g_splitk_inlaunch = true;
+extern "C" int stc_set_splitk_inlaunch(int on) {
+  const int old = g_splitk_inlaunch ? 1 : 0;
+  if (on >= 0) g_splitk_inlaunch = on != 0;
+  return old;
+}
+
+// Ticket counters of the in-launch split-K, one region per stream (launches on one stream run one after another, and
+// every launch leaves its counters zero): carved from one zeroed allocation made outside any graph capture.
+constexpr int kTicketRegion = 4096, kTicketRegions = 128;
+static unsigned* splitk_tickets(hipStream_t st, int tiles) {
+  static std::mutex mu;
+  static std::unordered_map<unsigned long long, int> region;  // (device, stream) -> region
+  static unsigned* pool[64] = {};
+  if (tiles > kTicketRegion) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!pool[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    void* q = nullptr;
+    const size_t bytes = (size_t)kTicketRegion * kTicketRegions * sizeof(unsigned);
+    if (hipMalloc(&q, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(q, 0, bytes) != hipSuccess) return nullptr;
+    pool[dev] = (unsigned*)q;
+  }
+  const unsigned long long key = ((unsigned long long)dev << 56) ^ (unsigned long long)(uintptr_t)st;
+  auto it = region.find(key);
+  int r;
+  if (it != region.end()) {
+    r = it->second;
+  } else {
+    int used = 0;
+    for (const auto& kv : region) used += (int)(kv.first >> 56) == dev ? 1 : 0;
+    if (used >= kTicketRegions) return nullptr;
+    r = region[key] = used;
+  }
+  return pool[dev] + (size_t)r * kTicketRegion;
+}
 
 // Shared planning for query and launch.
 static Bf16Problem bf16_problem(int M, int N, int K, int nphase, const int32_t* force, bool vec_out) {
@@ -657,6 +708,14 @@ static Bf16Problem bf16_problem(int M, int N, int K, int nphase, const int32_t* 
     pr.wide = pr.pl.ksplit >= 16 && rows * (N / 8) <= 16384;  // a wave per unit pays off with >= 16 splits
     pr.reduce_rows = reduce_rows_per_block(rows, N);
     pr.stats_chunks = pr.wide ? (int)rows : (int)((rows + pr.reduce_rows - 1) / pr.reduce_rows);
+    const long long tiles = (long long)nphase * pr.pl.mtiles * pr.pl.ntiles;
+    // (up to 4 splits: with 8 the last arrivers' slab reads outweigh the reduction launch -- the 4 x 4 / 2 x 2 deep
+    // layers measured 22.0 / 16.1 us in-launch against 13.7 + 6.6 / 6.6 + 6.3 us with the reduction kernel)
+    pr.inlaunch = g_splitk_inlaunch && !pr.wide && vec_out && pr.pl.ksplit <= 4 && tiles <= kTicketRegion;
+    if (pr.inlaunch) {
+      pr.ws_bytes = tiles * pr.pl.ksplit * (int64_t)pr.pl.BM * pr.pl.BN * 4;
+      pr.stats_chunks = nphase * pr.pl.mtiles;
+    }
   } else {
     pr.ws_bytes = 0;
     pr.stats_chunks = nphase * pr.pl.mtiles;
@@ -688,11 +747,22 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
   p.stats = nullptr;
   p.ws = nullptr;
   float* part2 = p.part2;
+  p.slab = nullptr;
+  p.tickets = nullptr;
+  p.acquire = 0;
   if (pl.ksplit > 1) {
     STC_REQUIRE(ws && ws_bytes >= pr.ws_bytes, "bf16 igemm: workspace %lld < %lld bytes", (long long)ws_bytes,
                 (long long)pr.ws_bytes);
-    p.ws = (float*)ws;
-    p.part2 = nullptr;  // computed by the split-K reduction
+    if (pr.inlaunch) {
+      p.tickets = splitk_tickets(st, pl.mtiles * pl.ntiles * p.nphase);
+      STC_REQUIRE(p.tickets, "bf16 igemm: no split-K ticket region for this stream (first use inside a capture?)");
+      p.slab = (float*)ws;
+      p.acquire = 1;
+      p.stats = stats;  // (the last arriver's epilogue: tile statistics / fused BN-backward sums)
+    } else {
+      p.ws = (float*)ws;
+      p.part2 = nullptr;  // computed by the split-K reduction
+    }
   } else {
     p.stats = stats;
   }
@@ -761,7 +831,7 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
 #undef STC_BL
   main_timer_end(st);
   STC_CHECK_LAUNCH();
-  if (pl.ksplit > 1) {
+  if (pl.ksplit > 1 && !pr.inlaunch) {
     STC_REQUIRE(p.vec_out, "bf16 igemm: split-K needs a 16-byte aligned NHWC bf16 output");
     p.stats = stats;
     p.part2 = part2;

@@ -60,6 +60,12 @@ struct GParams {
   // Padded GEMM grid (halo Conv2d k4 s1: the 31 x 31 output computed on its 32 x 32 input grid): vmask = 1 keeps
   // only the grid points y < vh, x < vw -- the others are neither stored nor counted in the statistics.
   int vmask, vh, vw;
+  // In-launch split-K (igemm_bf16_body): each split stores its tile's fp32 accumulators to slab
+  // [tile][ksplit][BM * BN] (write-through), takes the tile's ticket, and the last arriver sums the slabs in split
+  // order and runs the epilogue -- no reduction launch.  tickets: one counter per tile, zero between launches.
+  float* slab;
+  unsigned* tickets;
+  int acquire;  // the hand-off also takes the agent acquire (cdna_hip_programming.md Guideline 16)
 };
 
 // 8 bf16 (one uint4) -> act(v, slope) per element, rounded back to bf16 (as stc_bn_apply with no table)
@@ -103,6 +109,86 @@ __device__ __forceinline__ void bnb_accum(const GParams& p, int b, int oy, int o
 }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+// One in-launch hand-off to the last arriver of a counter (cdna_hip_programming.md Guideline 16, the write-through
+// form): the payload is stored sc1 (write-through to memory, no release fence) and EVERY load of it is an sc1 load
+// (past every L1 and L2, so no acquire); each wave drains its stores, the barrier joins them, lane 0 adds.
+// Returns (to every thread) whether this block drew the last ticket.  The last arriver leaves the counter zero.
+__device__ __forceinline__ bool last_arriver(unsigned* counter, unsigned total, unsigned* flag, bool acquire) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = old == total - 1 ? 1u : 0u;
+    if (old == total - 1) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const bool last = *flag != 0u;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the sc1 loads below the ticket)
+  if (last && acquire) {  // (more than one block per CU: the measured sc1 form covers one; the agent acquire too)
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+  return last;
+}
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int SC1 = 16;  // buffer-op cache bits: sc1 (write-through stores, loads past the caches)
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, floatx4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, SC1);
+}
+__device__ __forceinline__ floatx4 ld_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, SC1));
+}
+
+// In-launch split-K combine of one tile (GParams::slab / tickets): this split's accumulators to its slab, the
+// tile's ticket; the last arriver replaces acc by slab 0 + slab 1 + ... (split order -- the order of
+// splitk_reduce_stats_kernel, so the sums are the same) and returns true, the others false.
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ bool splitk_combine(const GParams& p, floatx4 (&acc)[BM / WM / 16][BN / WN / 16], int tile,
+                                               int split, char* smem) {
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.slab + (long long)tile * p.ksplit * (BM * BN)), (short)0, p.ksplit * BM * BN * 4, 0x00020000);
+  auto off = [&](int s, int i, int j) { return (unsigned)((s * (BM * BN) + ((wave * FM + i) * FN + j) * 256 + lane * 4) * 4); };
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) st_sc1(rsl, off(split, i, j), acc[i][j]);
+  if (!last_arriver(p.tickets + tile, (unsigned)p.ksplit, reinterpret_cast<unsigned*>(smem), p.acquire != 0))
+    return false;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // every slab loaded (the own one too), groups of RG slabs in flight, summed in split order
+  constexpr int RG = FM * FN <= 2 ? 8 : (FM * FN <= 4 ? 4 : 2);  // (<= 64 VGPRs in flight)
+  const int S = p.ksplit;
+  for (int s0 = 0; s0 < S; s0 += RG) {
+    floatx4 v[RG][FM][FN];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      const int s = min(s0 + g, S - 1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) v[g][i][j] = ld_sc1(rsl, off(s, i, j));
+    }
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      if (s0 + g >= S) break;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += v[g][i][j];
+    }
+  }
+  return true;
+}
 using lds_vptr = __attribute__((address_space(3))) void*;
 
 constexpr unsigned OOB = 0x80000000u;

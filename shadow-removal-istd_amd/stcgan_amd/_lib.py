@@ -74,6 +74,7 @@ _SIGS = {
     "stc_conv_fwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View]),
     "stc_conv_fwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _f32, View, _f32, _vp, _vp, _i64, _vp]),
     "stc_deep_debug_next": (_i32, [_vp]),
+    "stc_set_splitk_inlaunch": (_i32, [_i32]),
     "stc_deep_conv_query": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "stc_deep_conv": (_i32, [_i32, _i32, _i32, _vp, _vp, _i32, View, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,

@@ -61,6 +61,10 @@ _WG_SIDE = {}
 # lane, itself forked from the capturing stream, made the capture's end fault on this ROCm (round-3 probe:
 # scripts/graph_capture_probe.py -- lanes alone and side streams of the main stream alone capture fine).
 NO_SIDE_IN_CAPTURE = set()
+# True: STCGAN.capture keeps the lanes' weight-gradient side streams too (probe switch only: hipStreamEndCapture
+# segfaults on this ROCm with them, also when they first fork from the capturing stream and every fork has its own
+# event -- profiles/r05/graph_ab/late/)
+SIDE_IN_CAPTURE = False
 
 
 _set_stream = torch._C._cuda_setStream
@@ -92,8 +96,9 @@ class _WgradLane:
             return fn()
         self.last_side = True
         side, cur = self.side, self.cur
-        self._ev.record(cur)
-        side.wait_event(self._ev)
+        ev = self._ev if not SIDE_IN_CAPTURE else torch.cuda.Event()  # (capture probe: a fresh event per fork)
+        ev.record(cur)
+        side.wait_event(ev)
         for t in reads:
             t.record_stream(side)
         _set_stream(side.stream_id, side.device_index, side.device_type)

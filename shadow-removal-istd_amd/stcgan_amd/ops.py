@@ -78,6 +78,15 @@ def _conv_ws_bytes(kind, B, gh, gw, cin, cout, dt):
     return v
 
 
+def set_splitk_inlaunch(on):
+    """Split-K combined inside the GEMM launch (True, the default) or by a separate reduction launch (False; A/B):
+    stc_set_splitk_inlaunch.  The workspace sizes and statistics chunk counts follow it, so the memoised queries
+    are dropped.  Returns the previous setting."""
+    old = bool(lib().stc_set_splitk_inlaunch(1 if on else 0))
+    _MEMO.clear()
+    return old
+
+
 def plan_of(kind, B, gh, gw, cin, cout, dt):
     out = (ctypes.c_int32 * 4)()
     check(lib().stc_conv_fwd_plan(L.dtype_code(dt), kind, B, gh, gw, cin, cout, out), "stc_conv_fwd_plan")

@@ -424,8 +424,11 @@ class STCGAN(object):
             raise RuntimeError("STCGAN.capture: multi-process capture needs the nccl (RCCL) backend")
         from . import engine
         main, l1, l2 = self._lanes()
-        if l1 is not None:  # (see engine.NO_SIDE_IN_CAPTURE)
-            engine.NO_SIDE_IN_CAPTURE.update((l1.cuda_stream, l2.cuda_stream))
+        if l1 is not None:  # (see engine.NO_SIDE_IN_CAPTURE; pooled stream handles recur across trainers)
+            if engine.SIDE_IN_CAPTURE:
+                engine.NO_SIDE_IN_CAPTURE.difference_update((l1.cuda_stream, l2.cuda_stream))
+            else:
+                engine.NO_SIDE_IN_CAPTURE.update((l1.cuda_stream, l2.cuda_stream))
         cap = torch.cuda.Stream(self.device)
         cap.wait_stream(main)
         with torch.cuda.stream(cap):
@@ -443,6 +446,14 @@ class STCGAN(object):
         graph = torch.cuda.CUDAGraph()
         self._lanes_stale = True  # inside the capture the lanes must fork from the capturing stream
         with torch.cuda.graph(graph, stream=cap):
+            if l1 is not None and engine.SIDE_IN_CAPTURE:
+                # the lanes' weight-gradient side streams join the capture from the capturing stream itself, before
+                # their first wait on a lane (a side stream whose first capture edge came from a lane, itself
+                # forked from the capturing stream, crashed the capture on this ROCm: scripts/graph_capture_probe.py)
+                for ln in (l1, l2):
+                    ent = engine._WG_SIDE.get(ln.cuda_stream)
+                    if ent is not None:
+                        ent[0].wait_stream(cap)
             self.train_step(x, m, y)
         self._graph = graph
         # the optimisers' device pointer tables the captured launches read: kept alive even when a later eager

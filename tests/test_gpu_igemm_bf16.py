@@ -131,6 +131,37 @@ def test_channel_offset_view_and_bias(force):
     check(y, ref, mean, var, f"offset view {force}")
 
 
+@pytest.mark.parametrize("case", [(L.CONV_S2, 4, 512, 512, 4, 4, (12, 4)), (L.CONV_S2, 2, 128, 256, 16, 16, (0, 2)),
+                                  (L.CONVT_S2, 2, 512, 256, 4, 4, (5, 4)), (L.CONV_S2, 3, 64, 96, 10, 14, (11, 2)),
+                                  (L.CONV_S2, 32, 512, 512, 8, 8, None), (L.CONVT_S2, 32, 1024, 512, 4, 4, None)],
+                         ids=lambda c: "x".join(map(str, c[:6])) + ("" if c[6] is None else f"_cfg{c[6][0]}ks{c[6][1]}"))
+def test_splitk_inlaunch_matches_reduction_launch(case):
+    """Split-K combined in the launch (each tile's last arriver sums the slabs in split order and runs the epilogue)
+    against the separate reduction launch: the same outputs bit for bit (same sums in the same order, no bias), the
+    BatchNorm statistics from other chunks (tile partials vs reduction-block partials) within fp32 rounding."""
+    kind, B, Cin, Cout, Hg, Wg, force = case
+    if kind == L.CONVT_S2:
+        x = q(rnd(B, Cin, Hg, Wg, seed=11))
+        w = q(rnd(Cin, Cout, 4, 4, seed=12, scale=0.05))
+        out = (2 * Hg, 2 * Wg)
+    else:
+        x = q(rnd(B, Cin, 2 * Hg, 2 * Wg, seed=11))
+        w = q(rnd(Cout, Cin, 4, 4, seed=12, scale=0.05))
+        out = (Hg, Wg)
+    _, _, plan = ops.conv_query(kind, B, Hg, Wg, Cin, Cout, BF, force=force)
+    assert plan[2] > 1, f"not a split-K plan: {plan}"
+    old = ops.set_splitk_inlaunch(True)
+    try:
+        y1, m1, v1 = run(kind, B, x, w, Cin, Cout, out, force=force)
+        ops.set_splitk_inlaunch(False)
+        y0, m0, v0 = run(kind, B, x, w, Cin, Cout, out, force=force)
+    finally:
+        ops.set_splitk_inlaunch(old)
+    assert torch.equal(y1, y0)
+    assert float((m1 - m0).abs().max()) <= 1e-5 * (float(v0.max()) ** 0.5 + 1e-12)
+    assert float(((v1 - v0).abs() / (v0 + 1e-12)).max()) <= 1e-4
+
+
 def test_plan_query_consistent():
     for kind, gh in ((L.CONV_S2, 64), (L.CONVT_S2, 8), (L.CONV_S1, 31)):
         ws, nch, plan = ops.conv_query(kind, 32, gh, gh, 256, 512, BF)
