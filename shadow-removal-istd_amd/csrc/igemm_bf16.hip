@@ -570,6 +570,15 @@ static size_t bf16_lds_bytes(int cfg) {
   return std::max(stage, epi);
 }
 
+// In-launch split-K (igemm_bf16_body / splitk_combine) for the split layers that are not reduced by the wide kernel;
+// false: every split layer takes the separate reduction launch (A/B)
+static bool g_splitk_inlaunch = true;
+extern "C" int stc_set_splitk_inlaunch(int on) {
+  const int old = g_splitk_inlaunch ? 1 : 0;
+  if (on >= 0) g_splitk_inlaunch = on != 0;
+  return old;
+}
+
 // Tile / split-K choice (fitted to the sweep of scripts/tune_bf16.py over one train step, see
 // profiles/): prefer the largest tile that still gives a full wave of workgroups (about one
 // 8-wave block or two 4-wave blocks per CU), splitting K only when no tile does.
@@ -652,15 +661,6 @@ struct Bf16Problem {
   bool wide;      // split-K reduction by splitk_reduce_wide_kernel (a chunk per row)
   bool inlaunch;  // split-K combined in the launch (GParams::slab / tickets): the tile statistics of one launch
 };
-
-// In-launch split-K (igemm_bf16_body / splitk_combine) for the split layers that are not reduced by the wide kernel;
-// false: every split layer takes the separate reduction launch (A/B)
-static bool g_splitk_inlaunch = true;
-extern "C" int stc_set_splitk_inlaunch(int on) {
-  const int old = g_splitk_inlaunch ? 1 : 0;
-  if (on >= 0) g_splitk_inlaunch = on != 0;
-  return old;
-}
 
 // Ticket counters of the in-launch split-K, one region per stream (launches on one stream run one after another, and
 // every launch leaves its counters zero): carved from one zeroed allocation made outside any graph capture.
