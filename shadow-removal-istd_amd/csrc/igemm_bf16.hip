@@ -679,7 +679,9 @@ static unsigned* splitk_tickets(hipStream_t st, int tiles) {
     void* q = nullptr;
     const size_t bytes = (size_t)kTicketRegion * kTicketRegions * sizeof(unsigned);
     if (hipMalloc(&q, bytes) != hipSuccess) return nullptr;
-    if (hipMemset(q, 0, bytes) != hipSuccess) return nullptr;
+    // (hipMemset of device memory is asynchronous to the host and ordered on the null stream only: the device-wide
+    // synchronize makes the zeros visible to a first launch on any other stream -- once per device)
+    if (hipMemset(q, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
     pool[dev] = (unsigned*)q;
   }
   const unsigned long long key = ((unsigned long long)dev << 56) ^ (unsigned long long)(uintptr_t)st;

@@ -51,6 +51,9 @@ def _global_batches(n=2, bs=4, seed=2100):
 def _trainer(loss_type, ngf, dtype, family):
     from fixture_init import fixture_state
     from stcgan_amd.stcgan import STCGAN
+    if os.environ.get("STC_TEST_SPLITK_INLAUNCH") == "0":  # (diagnostic A/B of the in-launch split-K)
+        from stcgan_amd import ops
+        ops.set_splitk_inlaunch(False)
     torch.manual_seed(5)
     a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2e-5, beta1=0.5, beta2=0.999,
                               D_loss_fn="standard", D_loss_type=loss_type, ngf=ngf, dtype=dtype,
