@@ -664,7 +664,7 @@ struct Bf16Problem {
 
 // Ticket counters of the in-launch split-K, one region per stream (launches on one stream run one after another, and
 // every launch leaves its counters zero): carved from one zeroed allocation made outside any graph capture.
-constexpr int kTicketRegion = 4096, kTicketRegions = 128;
+constexpr int kTicketRegion = 4096, kTicketRegions = 512;  // (8 MiB per device: streams are pooled)
 static unsigned* splitk_tickets(hipStream_t st, int tiles) {
   static std::mutex mu;
   static std::unordered_map<unsigned long long, int> region;  // (device, stream) -> region
