@@ -17,7 +17,9 @@
 //     squares, in fp32 from the accumulators) -> part[tile][n] = {count, 0, M2, mean},
 //     the format stc_bn_finalize merges (Chan's parallel variance).
 
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <unordered_map>
 
 #include "igemm_bf16.hpp"
@@ -662,40 +664,41 @@ struct Bf16Problem {
   bool inlaunch;  // split-K combined in the launch (GParams::slab / tickets): the tile statistics of one launch
 };
 
-// Ticket counters of the in-launch split-K, one region per stream (launches on one stream run one after another, and
-// every launch leaves its counters zero): carved from one zeroed allocation made outside any graph capture.
+// Ticket counters of the in-launch split-K.  A region belongs to one (device, stream, capture): launches on one stream
+// run one after another and every launch leaves its counters zero, so eager launches on a stream share its region; a
+// launch made while the stream is being captured gets a region of that capture (the graph's replays may run beside
+// eager work on the same stream handle, or on another stream), kept for the process lifetime.  A region is zeroed on
+// the stream that first uses it (hipMemsetAsync: ordered before that launch -- inside a capture it becomes the graph's
+// memset node), so no device-wide synchronisation.  The pool itself is allocated outside any capture (the eager
+// warm-up steps of STCGAN.capture make the first split-K launch).
 constexpr int kTicketRegion = 4096, kTicketRegions = 512;  // (8 MiB per device: streams are pooled)
 static unsigned* splitk_tickets(hipStream_t st, int tiles) {
   static std::mutex mu;
-  static std::unordered_map<unsigned long long, int> region;  // (device, stream) -> region
+  static std::map<std::tuple<int, uintptr_t, unsigned long long>, int> region;  // (device, stream, capture) -> region
   static unsigned* pool[64] = {};
+  static int used[64] = {};
   if (tiles > kTicketRegion) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long cap_id = 0;
+  if (hipStreamGetCaptureInfo(st, &cs, &cap_id) != hipSuccess) return nullptr;
+  const unsigned long long cap = cs == hipStreamCaptureStatusActive ? cap_id + 1 : 0;
   std::lock_guard<std::mutex> lk(mu);
   if (!pool[dev]) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
     void* q = nullptr;
-    const size_t bytes = (size_t)kTicketRegion * kTicketRegions * sizeof(unsigned);
-    if (hipMalloc(&q, bytes) != hipSuccess) return nullptr;
-    // (hipMemset of device memory is asynchronous to the host and ordered on the null stream only: the device-wide
-    // synchronize makes the zeros visible to a first launch on any other stream -- once per device)
-    if (hipMemset(q, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+    if (hipMalloc(&q, (size_t)kTicketRegion * kTicketRegions * sizeof(unsigned)) != hipSuccess) return nullptr;
     pool[dev] = (unsigned*)q;
   }
-  const unsigned long long key = ((unsigned long long)dev << 56) ^ (unsigned long long)(uintptr_t)st;
+  const auto key = std::make_tuple(dev, (uintptr_t)st, cap);
   auto it = region.find(key);
-  int r;
-  if (it != region.end()) {
-    r = it->second;
-  } else {
-    int used = 0;
-    for (const auto& kv : region) used += (int)(kv.first >> 56) == dev ? 1 : 0;
-    if (used >= kTicketRegions) return nullptr;
-    r = region[key] = used;
-  }
-  return pool[dev] + (size_t)r * kTicketRegion;
+  if (it != region.end()) return pool[dev] + (size_t)it->second * kTicketRegion;
+  if (used[dev] >= kTicketRegions) return nullptr;
+  unsigned* r = pool[dev] + (size_t)used[dev] * kTicketRegion;
+  if (hipMemsetAsync(r, 0, (size_t)kTicketRegion * sizeof(unsigned), st) != hipSuccess) return nullptr;
+  region[key] = used[dev]++;
+  return r;
 }
 
 // Shared planning for query and launch.
@@ -769,7 +772,8 @@ int bf16_igemm_launch(GParams& p, const int32_t* force, void* ws, int64_t ws_byt
     p.stats = stats;
   }
   if (stats || part2)
-    STC_REQUIRE(stats_chunks >= pr.stats_chunks, "bf16 igemm: stats chunks %d < %d", stats_chunks, pr.stats_chunks);
+    STC_REQUIRE(stats_chunks == pr.stats_chunks, "bf16 igemm: stats chunks %d != %d (query again after changing the "
+                "split-K mode)", stats_chunks, pr.stats_chunks);
   p.phase_major = (p.nphase > 1 && pl.ksplit == 1) ? 1 : 0;
   dim3 grid = p.phase_major ? dim3(pl.mtiles * pl.ntiles * p.nphase, 1, 1)
                             : dim3(pl.mtiles * pl.ntiles, 1, p.nphase * pl.ksplit);
@@ -977,7 +981,7 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
   }
   if (!act_n && p.vec_out && halo_plan(force, kind, B, p.GH, p.GW, Cin, Cout) && halo_eligible(kind, B, x, Cin, Cout, y)) {
     const int need = halo_chunks(kind, B, p.GH, p.GW);
-    if (stats || part2) STC_REQUIRE(stats_chunks >= need, "bf16 conv: stats chunks %d < %d", stats_chunks, need);
+    if (stats || part2) STC_REQUIRE(stats_chunks == need, "bf16 conv: stats chunks %d != %d", stats_chunks, need);
     p.stats = stats;
     p.ws = nullptr;
     return halo_launch(p, st, force && force[0] == HALO_CFG ? force[1] : 0);

@@ -69,6 +69,27 @@ SIDE_IN_CAPTURE = False
 
 _set_stream = torch._C._cuda_setStream
 
+# Events recorded or waited on while a HIP graph is being captured, kept alive until the capture has ended
+# (STCGAN.capture sets a list here and drops it after capture_end).  torch's Stream.wait_stream and a fork's local
+# event are otherwise destroyed inside the open capture, while capture edges still refer to them: the first suspect
+# of the hipStreamEndCapture fault with the lanes' weight-gradient side streams (profiles/r05/graph_ab/late/).
+CAPTURE_EVENTS = None
+
+
+def hold(ev):
+    """ev, kept alive until the open capture ends (no-op outside a capture)."""
+    if CAPTURE_EVENTS is not None:
+        CAPTURE_EVENTS.append(ev)
+    return ev
+
+
+def wait_stream(waiter, src):
+    """waiter.wait_stream(src) whose event outlives an open capture."""
+    ev = torch.cuda.Event()
+    ev.record(src)
+    waiter.wait_event(ev)
+    hold(ev)
+
 
 class _WgradLane:
     def __init__(self):
@@ -96,7 +117,7 @@ class _WgradLane:
             return fn()
         self.last_side = True
         side, cur = self.side, self.cur
-        ev = self._ev if not SIDE_IN_CAPTURE else torch.cuda.Event()  # (capture probe: a fresh event per fork)
+        ev = self._ev if not SIDE_IN_CAPTURE else hold(torch.cuda.Event())  # (capture probe: a fresh event per fork)
         ev.record(cur)
         side.wait_event(ev)
         for t in reads:
@@ -109,7 +130,7 @@ class _WgradLane:
 
     def join(self):
         if self.side is not None:
-            self.cur.wait_stream(self.side)
+            wait_stream(self.cur, self.side)
 
 
 class GradWriter:
@@ -422,7 +443,7 @@ def _gen_forward_deep(plan, sources, train, dt, cache, save, kd):
         side = cache.get("__deep_side__")
         if side is None:
             side = cache["__deep_side__"] = torch.cuda.Stream(dev)
-        side.wait_stream(main)
+        wait_stream(side, main)
         with torch.cuda.stream(side):
             for k in range(kd, Lv):
                 for tns in (rd[k], cr[k], ad[k], rq[k + 1] if k + 1 < Lv else None):
@@ -449,7 +470,7 @@ def _gen_forward_deep(plan, sources, train, dt, cache, save, kd):
     ops.conv(L.CONVT_S2, B, L.nhwc_view(cr[0]), 2 * co[0], wt0, plan.out_c, L.nchw_view(y), dt,
              bias=plan.convT[0].bias, tanh=True, out_f32=True)
     if side is not None:
-        torch.cuda.current_stream(dev).wait_stream(side)
+        wait_stream(torch.cuda.current_stream(dev), side)
     saved = None
     if save:
         saved = dict(S=S, xin=xin, rd=rd, ad=ad, cr=cr, rq=rq, tab_d=tab_d, tab_u=tab_u, st_d=st_d, st_u=st_u,

@@ -27,6 +27,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from . import engine
 from . import networks
 from . import parallel
 from .loss import AdversarialLoss, DataLoss, d_objective, g_objective
@@ -318,15 +319,15 @@ class STCGAN(object):
             if self._lanes_stale or not self.lane_carry:
                 # D state written on the main stream outside the step (construction, broadcasts, checkpoint
                 # loads, a validation pass): the lanes start after it
-                l1.wait_stream(main)
-                l2.wait_stream(main)
+                engine.wait_stream(l1, main)
+                engine.wait_stream(l2, main)
                 self._lanes_stale = False
             elif inputs_ready is not None:
                 l1.wait_event(inputs_ready)
                 l2.wait_event(inputs_ready)
             elif not same:
-                l1.wait_stream(main)
-                l2.wait_stream(main)
+                engine.wait_stream(l1, main)
+                engine.wait_stream(l2, main)
             self._lane_inputs = ((x, m, y), tuple(t._version for t in (x, m, y)))
             self.D1.grad_consumer = self.D2.grad_consumer = main
         # each discriminator sees the same real and fake inputs in the D and the G step: gather them once
@@ -344,14 +345,14 @@ class STCGAN(object):
             C1_real = self._on(l1, self.D1, [x, m])
             C2_real = self._on(l2, self.D2, [x, m, y])
             m_pred = self.G1(x)
-            ev_m = main.record_event() if l1 is not None else None
+            ev_m = engine.hold(main.record_event()) if l1 is not None else None
             C1_fake = self._on(l1, self.D1, [x, m_pred.detach()], after=ev_m)
             y_pred = self.G2([x, m_pred])
-            ev_y = main.record_event() if l1 is not None else None
+            ev_y = engine.hold(main.record_event()) if l1 is not None else None
             C2_fake = self._on(l2, self.D2, [x, m_pred.detach(), y_pred.detach()], after=ev_y)
             if l1 is not None:
-                main.wait_stream(l1)
-                main.wait_stream(l2)
+                engine.wait_stream(main, l1)
+                engine.wait_stream(main, l2)
             if self.d_loss_type == "normal" and self.fused_objectives:  # one node (loss.d_objective)
                 D_loss, D1_loss, D2_loss = d_objective(self.adv_loss, C1_fake, C1_real, C2_fake, C2_real,
                                                        self.lambda2, self.lambda3)
@@ -370,8 +371,8 @@ class STCGAN(object):
             self.D2.requires_grad_(False)
             if training:  # D is not updated when validating
                 if l1 is not None:  # after optim_D.step
-                    l1.wait_stream(main)
-                    l2.wait_stream(main)
+                    engine.wait_stream(l1, main)
+                    engine.wait_stream(l2, main)
                 # loss type "normal": the G objective does not read C_real; the calls still run (the reference
                 # makes them, STCGAN/stcgan.py:269-272) for their BatchNorm running statistics, minus the
                 # logits layer (engine: stats_only)
@@ -385,8 +386,8 @@ class STCGAN(object):
                 C1_fake = self._on(l1, self.D1, [x, m_pred])
                 C2_fake = self._on(l2, self.D2, [x, m_pred, y_pred])
                 if l1 is not None:
-                    main.wait_stream(l1)
-                    main.wait_stream(l2)
+                    engine.wait_stream(main, l1)
+                    engine.wait_stream(main, l2)
             if self.d_loss_type == "normal" and self.fused_objectives:
                 G_loss, G1_loss, G2_loss, data1_loss, data2_loss = g_objective(
                     self.adv_loss, m_pred, m, y_pred, y, C1_fake, C2_fake, self.lambda1, self.lambda2, self.lambda3)
@@ -401,8 +402,8 @@ class STCGAN(object):
                 self._finish_exchange(("G2", "G1"))
                 self.optim_G.step()
         if l1 is not None:  # nothing on the side lanes outlives the step
-            main.wait_stream(l1)
-            main.wait_stream(l2)
+            engine.wait_stream(main, l1)
+            engine.wait_stream(main, l2)
         vals = dict(D1=D1_loss.detach(), D2=D2_loss.detach(), D=D_loss.detach(), G1=G1_loss.detach(),
                     G2=G2_loss.detach(), data1=data1_loss.detach(), data2=data2_loss.detach(), G=G_loss.detach())
         if acc is not None:
@@ -422,7 +423,6 @@ class STCGAN(object):
         import torch.distributed as dist
         if parallel.world() > 1 and dist.get_backend() != "nccl":
             raise RuntimeError("STCGAN.capture: multi-process capture needs the nccl (RCCL) backend")
-        from . import engine
         main, l1, l2 = self._lanes()
         if l1 is not None:  # (see engine.NO_SIDE_IN_CAPTURE; pooled stream handles recur across trainers)
             if engine.SIDE_IN_CAPTURE:
@@ -430,7 +430,7 @@ class STCGAN(object):
             else:
                 engine.NO_SIDE_IN_CAPTURE.update((l1.cuda_stream, l2.cuda_stream))
         cap = torch.cuda.Stream(self.device)
-        cap.wait_stream(main)
+        engine.wait_stream(cap, main)
         with torch.cuda.stream(cap):
             for _ in range(max(1, warmup)):  # steady state: packed operands, tables, streams, flat gradients
                 self.train_step(x, m, y)
@@ -441,20 +441,15 @@ class STCGAN(object):
             # gradient operands appear in the first G step -- sends the next step down the full path)
             for _ in range(2):
                 self.train_step(x, m, y)
-        main.wait_stream(cap)
+        engine.wait_stream(main, cap)
         torch.cuda.synchronize(self.device)
         graph = torch.cuda.CUDAGraph()
         self._lanes_stale = True  # inside the capture the lanes must fork from the capturing stream
-        with torch.cuda.graph(graph, stream=cap):
-            if l1 is not None and engine.SIDE_IN_CAPTURE:
-                # the lanes' weight-gradient side streams join the capture from the capturing stream itself, before
-                # their first wait on a lane (a side stream whose first capture edge came from a lane, itself
-                # forked from the capturing stream, crashed the capture on this ROCm: scripts/graph_capture_probe.py)
-                for ln in (l1, l2):
-                    ent = engine._WG_SIDE.get(ln.cuda_stream)
-                    if ent is not None:
-                        ent[0].wait_stream(cap)
-            self.train_step(x, m, y)
+        engine.CAPTURE_EVENTS = []  # every event recorded / waited in the capture lives until it has ended
+        try:
+            self._capture_into(graph, cap, x, m, y, l1, l2)
+        finally:
+            engine.CAPTURE_EVENTS = None
         self._graph = graph
         # the optimisers' device pointer tables the captured launches read: kept alive even when a later eager
         # step on the general path replaces them (freed, their memory could be reused under the graph)
@@ -466,6 +461,18 @@ class STCGAN(object):
                 o.sync_lr()
             graph.replay()
         return replay
+
+    def _capture_into(self, graph, cap, x, m, y, l1, l2):
+        with torch.cuda.graph(graph, stream=cap):
+            if l1 is not None and engine.SIDE_IN_CAPTURE:
+                # the lanes' weight-gradient side streams join the capture from the capturing stream itself, before
+                # their first wait on a lane (a side stream whose first capture edge came from a lane, itself
+                # forked from the capturing stream, crashed the capture on this ROCm: scripts/graph_capture_probe.py)
+                for ln in (l1, l2):
+                    ent = engine._WG_SIDE.get(ln.cuda_stream)
+                    if ent is not None:
+                        engine.wait_stream(ent[0], cap)
+            self.train_step(x, m, y)
 
     def run_epoch(self, training=True):
         for net in (self.G1, self.G2, self.D1, self.D2):

@@ -141,3 +141,41 @@ def test_replay_after_optimizer_state_load():
     graphed.train_step(x, m, y)
     bad = _same(_state(eager), _state(graphed))
     assert not bad, bad[:8]
+
+
+def test_splitk_tickets_graph_replay_beside_eager_on_capture_stream():
+    """In-launch split-K ticket regions belong to (stream, capture): a graph captured on a stream keeps its own
+    region, so its replays (here on another stream) and eager launches on the capture stream's handle never share
+    counters.  Both must give the eager result, bit for bit, every time (csrc/igemm_bf16.hip splitk_tickets)."""
+    from stcgan_amd import _lib as L
+    from stcgan_amd import ops
+    BF = torch.bfloat16
+    B, Cin, Cout, Hg = 32, 512, 1024, 8
+    _, _, plan = ops.conv_query(L.CONV_S2, B, Hg, Hg, Cin, Cout, BF)
+    assert 2 <= plan[2] <= 4, plan
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn((B, 2 * Hg, 2 * Hg, Cin), generator=g, device="cuda").to(BF)
+    w = ops.pack(L.PACK_CONV_FWD, torch.randn((Cout, Cin, 4, 4), generator=g, device="cuda") * 0.05, Cout, Cin, BF)
+    cap = torch.cuda.Stream()
+    other = torch.cuda.Stream()
+    ref = torch.empty((B, Hg, Hg, Cout), device="cuda", dtype=BF)
+    with torch.cuda.stream(cap):
+        pref, _ = ops.conv_stats(L.CONV_S2, B, L.nhwc_view(x), Cin, w, Cout, L.nhwc_view(ref), BF)
+    torch.cuda.synchronize()
+    yg = torch.empty_like(ref)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=cap):
+        pg, _ = ops.conv_stats(L.CONV_S2, B, L.nhwc_view(x), Cin, w, Cout, L.nhwc_view(yg), BF)
+    for _ in range(4):
+        ye = torch.full_like(ref, float("nan"))
+        yg.fill_(float("nan"))
+        torch.cuda.synchronize()
+        other.wait_stream(torch.cuda.current_stream())
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(other):
+            graph.replay()
+        with torch.cuda.stream(cap):
+            pe, _ = ops.conv_stats(L.CONV_S2, B, L.nhwc_view(x), Cin, w, Cout, L.nhwc_view(ye), BF)
+        torch.cuda.synchronize()
+        assert torch.equal(ye, ref) and torch.equal(yg, ref)
+        assert torch.equal(pe, pref) and torch.equal(pg, pref)

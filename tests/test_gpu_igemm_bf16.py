@@ -162,6 +162,57 @@ def test_splitk_inlaunch_matches_reduction_launch(case):
     assert float(((v1 - v0).abs() / (v0 + 1e-12)).max()) <= 1e-4
 
 
+@pytest.mark.parametrize("case", [(L.CONV_S2, 32, 512, 1024, 8, 8), (L.CONVT_S2, 32, 512, 512, 2, 2),
+                                  (L.CONV_S2, 32, 1024, 512, 4, 4), (L.CONVT_S2, 32, 1024, 512, 4, 4)],
+                         ids=lambda c: "x".join(map(str, c)))
+def test_splitk_inlaunch_bn_backward_matches_reduction_launch(case):
+    """The fused BatchNorm-backward form of an input-gradient conv on an in-launch split-K plan (the last arriver's
+    epilogue writes the {dn, dn*xhat} partials, nphase * mtiles chunks) against the reduction launch (which computes
+    them itself): the conv output bit for bit, the BN input gradient bit for bit apart from fp32 rounding of the
+    per-channel sums, dgamma / dbeta within fp32 rounding."""
+    kind, B, Cin, Cout, Hg, Wg = case
+    _, _, plan = ops.conv_query(kind, B, Hg, Wg, Cin, Cout, BF)
+    if not 2 <= plan[2] <= 4:
+        pytest.skip(f"the automatic plan is not a 2-4 split plan here: {plan}")
+    gen = torch.Generator(device=DEV)
+    if kind == L.CONVT_S2:
+        wt = q(rnd(Cin, Cout, 4, 4, seed=61, scale=0.05))
+        w = ops.pack(L.PACK_CONVT_FWD, wt.to(DEV), Cout, Cin, BF)
+        dy = torch.randn((B, Hg, Wg, Cin), generator=gen.manual_seed(62), device=DEV).to(BF)
+        Ho, Wo = 2 * Hg, 2 * Wg
+    else:
+        wt = q(rnd(Cout, Cin, 4, 4, seed=61, scale=0.05))
+        w = ops.pack(L.PACK_CONV_FWD, wt.to(DEV), Cout, Cin, BF)
+        dy = torch.randn((B, 2 * Hg, 2 * Wg, Cin), generator=gen.manual_seed(62), device=DEV).to(BF)
+        Ho, Wo = Hg, Wg
+    C = Cout
+    x = torch.randn((B, Ho, Wo, C), generator=gen.manual_seed(63), device=DEV).to(BF)
+    go = torch.randn((B, Ho, Wo, C), generator=gen.manual_seed(64), device=DEV).to(BF)
+    g = torch.Generator().manual_seed(65)
+    st = tuple((torch.rand(C, generator=g) + 0.5).to(DEV) if i in (0, 3) else (torch.randn(C, generator=g) * 0.2).to(DEV)
+               for i in range(4))
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    res = []
+    old = ops.set_splitk_inlaunch(True)
+    try:
+        for mode in (True, False):
+            ops.set_splitk_inlaunch(mode)
+            out = torch.zeros((B, Ho, Wo, Cout), device=DEV, dtype=BF)
+            dx = torch.empty((B, Ho, Wo, C), device=DEV, dtype=BF)
+            dg, db = ops.conv_bn_backward(kind, B, L.nhwc_view(dy), Cin, w, Cout, L.nhwc_view(out), BF,
+                                          bn_x=L.nhwc_view(x), C=C, bn_state=st, gamma=gamma, s_self=0.2,
+                                          g_other=L.nhwc_view(go), s_other=0.0, dxv=L.nhwc_view(dx))
+            torch.cuda.synchronize()
+            res.append((out, dx.float(), dg, db))
+    finally:
+        ops.set_splitk_inlaunch(old)
+    (o1, dx1, g1, b1), (o0, dx0, g0, b0) = res
+    assert torch.equal(o1, o0)
+    for a, b in ((g1, g0), (b1, b0)):
+        assert float((a - b).abs().max()) <= 1e-5 * (float(b.abs().max()) + 1e-6)
+    assert float((dx1 - dx0).abs().max()) <= 1e-2 * (float(dx0.abs().max()) + 1e-6)
+
+
 def test_plan_query_consistent():
     for kind, gh in ((L.CONV_S2, 64), (L.CONVT_S2, 8), (L.CONV_S1, 31)):
         ws, nch, plan = ops.conv_query(kind, 32, gh, gh, 256, 512, BF)
