@@ -149,47 +149,6 @@ int stc_conv_fwd_act(int dtype, int kind, int B, stc_view x, int Cin, const void
                      stc_view y1, float slope1, stc_view y2, float slope2, const float* bias,
                      void* workspace, int64_t workspace_bytes, void* stream);
 
-/* ---- the U-Net's innermost levels, one launch per layer (bf16) --------------------------------------
- * Replaces, for the generator's innermost levels (STCGAN/networks.py:104-105 down convs, :119-121 / :126-128
- * up ConvTs: grids of 1x1 - 4x4 at 256x256), the four launches per layer of the im2col path --
- * stc_conv_fwd_ex (split K), its split-K reduction, stc_bn_finalize, stc_bn_apply -- by one: the A operand
- * is read RAW and each source's BatchNorm affine (its producer's table) + activation is applied as it is
- * staged; split-K slices are summed in-launch in split order by the last-arriving block of each tile (a
- * ticket per tile, agent-scope release / acquire); with an output BatchNorm (train mode) each tile's
- * (count, mean, M2) partials are merged by the last tile of its column of channels into the output's
- * mean / rstd / scale / shift tables and running statistics (num_batches_tracked + 1).  Tickets must be zero
- * before the first launch and are left zero.  kind: STC_CONV_S2 (GEMM grid = output grid) or STC_CONVT_S2
- * (GEMM grid = input grid, 4 phases); the sources' channels are concatenated in order (the U-Net concat
- * [skip | up] of a ConvT input), each a multiple of 64.
- * stc_deep_conv_query: workspace bytes (split-K slabs + statistics partials) and tickets of the plan;
- * plan_out[5] = {BM, BN, ksplit, taps kept, blocks}.                                                     */
-typedef struct {
-  stc_view x;             /* NHWC bf16 source (a raw conv output, or an activation: no table, slope 1)  */
-  int32_t C;              /* its channels (a multiple of 64)                                            */
-  float slope;            /* activation after the affine: 0 ReLU, 0.2 LeakyReLU, 1 none                 */
-  const float* scale;     /* (scale, shift) table of its BatchNorm (NULL: identity)                     */
-  const float* shift;
-} stc_deep_src;
-typedef struct {
-  const float* gamma;     /* the output's BatchNorm2d (train mode)                                      */
-  const float* beta;
-  float eps, momentum;
-  float* mean_out;        /* [Cout] outputs: batch mean, 1/sqrt(var + eps), the (scale, shift) table    */
-  float* rstd_out;
-  float* scale_out;
-  float* shift_out;
-  float* running_mean;    /* updated (NULL: not updated)                                                */
-  float* running_var;
-  int64_t* num_batches_tracked;
-} stc_deep_bn;
-int stc_deep_conv_query(int kind, int B, int Hg, int Wg, int IH, int IW, int Cin, int Cout,
-                        const int32_t* force_plan, int64_t* workspace_bytes, int32_t* ntickets, int32_t* plan_out);
-int stc_deep_conv(int kind, int B, int nsrc, const stc_deep_src* src, const void* w_packed, int Cout, stc_view y,
-                  const stc_deep_bn* bn, const int32_t* force_plan, uint32_t* tickets, int ntickets,
-                  void* workspace, int64_t workspace_bytes, void* stream);
-/* diagnostics (scripts/deep_tune.py --phases): the next stc_deep_conv launch writes 8 wall-clock stamps per block
- * (start, tables, K loop done, reduce, statistics, finalize, end) into stamps[blocks][8]; NULL clears.          */
-int stc_deep_debug_next(void* stamps);
 /* split-K forward / input-gradient GEMMs (bf16): 1 (default) = the slabs are combined inside the launch by each
  * tile's last-arriving block (a ticket per tile) and it runs the epilogue; 0 = a separate reduction launch (A/B).
  * on < 0 only queries.  Returns the previous setting.  Workspace sizes and statistics chunk counts

@@ -23,14 +23,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--deep", type=int, default=None, help="engine.DEEP (the innermost levels on stc_deep_conv)")
-    ap.add_argument("--levels", type=int, default=None, help="engine.DEEP_LEVELS")
     a = ap.parse_args()
-    from stcgan_amd import engine
-    if a.deep is not None:
-        engine.DEEP = bool(a.deep)
-    if a.levels is not None:
-        engine.DEEP_LEVELS = a.levels
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     g1 = networks.get_generator(3, 1).apply(networks.weights_init).to(dev).set_compute_dtype(a.dtype).train()

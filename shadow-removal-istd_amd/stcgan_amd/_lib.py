@@ -38,20 +38,6 @@ class BnbFuse(ctypes.Structure):
                 ("slope_other", ctypes.c_float), ("C", ctypes.c_int32), ("ch_off", ctypes.c_int32)]
 
 
-class DeepSrc(ctypes.Structure):
-    """stc_deep_src: one source of a stc_deep_conv launch (a raw tensor, its BatchNorm table, an activation)."""
-    _fields_ = [("x", View), ("C", ctypes.c_int32), ("slope", ctypes.c_float), ("scale", ctypes.c_void_p),
-                ("shift", ctypes.c_void_p)]
-
-
-class DeepBN(ctypes.Structure):
-    """stc_deep_bn: the output BatchNorm of a stc_deep_conv launch (tables and running statistics it writes)."""
-    _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("eps", ctypes.c_float),
-                ("momentum", ctypes.c_float), ("mean_out", ctypes.c_void_p), ("rstd_out", ctypes.c_void_p),
-                ("scale_out", ctypes.c_void_p), ("shift_out", ctypes.c_void_p), ("running_mean", ctypes.c_void_p),
-                ("running_var", ctypes.c_void_p), ("num_batches_tracked", ctypes.c_void_p)]
-
-
 class PackDesc(ctypes.Structure):
     """stc_pack_desc: one stc_pack_weight job of a multi-tensor stc_pack_weights launch."""
     _fields_ = [("mode", ctypes.c_int32), ("P", ctypes.c_int32), ("Q", ctypes.c_int32), ("N_pad", ctypes.c_int32),
@@ -73,10 +59,7 @@ _SIGS = {
                                _i64, _vp]),
     "stc_conv_fwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View]),
     "stc_conv_fwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _f32, View, _f32, _vp, _vp, _i64, _vp]),
-    "stc_deep_debug_next": (_i32, [_vp]),
     "stc_set_splitk_inlaunch": (_i32, [_i32]),
-    "stc_deep_conv_query": (_i32, [_i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
-    "stc_deep_conv": (_i32, [_i32, _i32, _i32, _vp, _vp, _i32, View, _vp, _vp, _vp, _i32, _vp, _i64, _vp]),
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
                               _f32, _vp, _vp, _i64, _vp]),
     "stc_conv_wgrad_workspace": (_i64, [_i32, _i32, _i32, _i32, _i32, _i32]),

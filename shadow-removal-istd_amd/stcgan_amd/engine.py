@@ -262,33 +262,11 @@ def _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev):
 # ----------------------------------------------------------------------------- generator
 
 
-# The generator's three innermost levels (grids of 1x1 - 4x4 at 256x256: 32-512 GEMM rows per phase at bs = 32) on
-# stc_deep_conv, one launch per layer (raw inputs with the BatchNorm + activation applied as they are staged,
-# in-launch split-K, the output's statistics partials), instead of four (conv, split-K reduction, BN finalize,
-# BN apply).  bf16 only; False: the per-layer path for every level (A/B).
-DEEP = False  # (enabled once validated on the GPU)
-DEEP_LEVELS = 3
-
-
-def _deep_from(plan, dt, B, S):
-    """First level k (conv_k and convT_k) that runs on stc_deep_conv, or None."""
-    Lv, co = plan.L, plan.co
-    if not DEEP or dt != torch.bfloat16 or Lv < DEEP_LEVELS + 2:
-        return None
-    kd = Lv - DEEP_LEVELS
-    if any(c % 64 for c in co[kd - 1:]) or co[kd - 1] > 1024 or any(2 * c > 1024 for c in co[kd:Lv - 1]):
-        return None
-    return kd
-
-
 def gen_forward(plan, sources, train, dt, cache, save):
     dev = sources[0].device
     B, _, H, W = sources[0].shape
     Lv, co = plan.L, plan.co
     S = _sizes(H, W, Lv)
-    kd = _deep_from(plan, dt, B, S)
-    if kd is not None:
-        return _gen_forward_deep(plan, sources, train, dt, cache, save, kd)
     assert S[Lv][0] >= 1 and S[Lv][1] >= 1, "input too small for the generator depth"
     cin = sum(s.shape[1] for s in sources)
     assert cin == plan.in_c, f"generator expects {plan.in_c} input channels, got {cin}"
@@ -344,133 +322,6 @@ def gen_forward(plan, sources, train, dt, cache, save):
     wt0 = ops.packed(cache, plan.convT[0].weight, L.PACK_CONVT_FWD, plan.out_c, 2 * co[0], dt)
     ops.conv(L.CONVT_S2, B, L.nhwc_view(cr[0]), 2 * co[0], wt0, plan.out_c, L.nchw_view(y), dt,
              bias=plan.convT[0].bias, tanh=True, out_f32=True)
-    saved = None
-    if save:
-        saved = dict(S=S, xin=xin, rd=rd, ad=ad, cr=cr, rq=rq, tab_d=tab_d, tab_u=tab_u, st_d=st_d, st_u=st_u,
-                     y=y, cin=cin, cin_pad=cin_pad, src_c=[s.shape[1] for s in sources])
-        if TRACE is not None:
-            _trace_new("G")
-            _trace("G", "saved", saved)
-    return y, saved
-
-
-def _gen_forward_deep(plan, sources, train, dt, cache, save, kd):
-    """gen_forward with levels kd .. L-1 on stc_deep_conv (see DEEP).  The deep levels' raw outputs rd / rq and their
-    BatchNorm tables / statistics are kept as on the per-layer path; their activations ad / cr (read only by the
-    backward's weight gradients) are materialised only when the call saves for a backward, on a side stream."""
-    dev = sources[0].device
-    B, _, H, W = sources[0].shape
-    Lv, co = plan.L, plan.co
-    S = _sizes(H, W, Lv)
-    assert S[Lv][0] >= 1 and S[Lv][1] >= 1, "input too small for the generator depth"
-    cin = sum(s.shape[1] for s in sources)
-    assert cin == plan.in_c, f"generator expects {plan.in_c} input channels, got {cin}"
-    cin_pad = ops.pad_channels(cin, dt)
-    xin = _nhwc(B, H, W, cin_pad, dt, dev)
-    ops.gather(sources, xin, dt)
-
-    def cin_t(k):
-        return co[k] if k == Lv - 1 else 2 * co[k]
-
-    rd = [None] + [_nhwc(B, *S[k + 1], co[k], dt, dev) for k in range(1, Lv)]
-    ad = [_nhwc(B, *S[k + 1], co[k], dt, dev) if (k < Lv - 1 and (k < kd or save)) else None for k in range(Lv)]
-    cr = [_nhwc(B, *S[k + 1], cin_t(k), dt, dev) if (k < kd or save) else None for k in range(Lv)]
-    rq = [None] + [_nhwc(B, *_pad2(S, k), co[k - 1], dt, dev) for k in range(1, Lv)]
-    tab_d, tab_u, st_d, st_u = {}, {}, {}, {}
-    tickets = cache.setdefault("__tickets__", {})
-
-    def conv_bn(kind, xv, cin_, w, cout, yv, bn):
-        return _conv_bn(kind, B, xv, cin_, w, cout, yv, dt, bn, train, dev)
-
-    # ---- down path: levels < kd as gen_forward
-    w0 = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_FWD, co[0], cin_pad, dt)
-    if ops.conv_act(L.CONV_S2, B, L.nhwc_view(xin), cin_pad, w0, co[0], L.nhwc_view(ad[0]), LRELU, dt,
-                    L.nhwc_view(cr[0], 0), 0.0):
-        rd[0] = ad[0]
-    else:
-        rd[0] = _nhwc(B, *S[1], co[0], dt, dev)
-        ops.conv(L.CONV_S2, B, L.nhwc_view(xin), cin_pad, w0, co[0], L.nhwc_view(rd[0]), dt)
-        ops.bn_apply(B, L.nhwc_view(rd[0]), co[0], dt, None, L.nhwc_view(ad[0]), LRELU, L.nhwc_view(cr[0], 0), 0.0)
-    for k in range(1, kd):
-        wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
-        tab_d[k], st_d[k] = conv_bn(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]),
-                                    plan.bnd[k])
-        ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]), LRELU,
-                     L.nhwc_view(cr[k], 0), 0.0)
-    # ---- deep levels: conv_k reads ad[kd - 1] (materialised above), then the raw rd[k - 1] through BN_d[k - 1]'s
-    # table, which conv_{k-1}'s launch wrote (train) or bn_eval_table made (eval); convT_k likewise
-    def table_of(k, up):
-        """(BN table, deep_bn descriptor for the launch that produces the level's raw output (train) or None)."""
-        bn = plan.bnu[k] if up else plan.bnd[k]
-        C = bn.num_features
-        tabs, sts = (tab_u, st_u) if up else (tab_d, st_d)
-        t = torch.empty((2, C), dtype=torch.float32, device=dev)
-        tabs[k] = t
-        if not train:
-            ops.bn_eval_table(C, bn, t[0], t[1])
-            sts[k] = None
-            return None
-        sts[k] = (torch.empty(C, dtype=torch.float32, device=dev), torch.empty(C, dtype=torch.float32, device=dev))
-        return ops.deep_bn(bn, t, sts[k])
-
-    for k in range(kd, Lv):
-        wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
-        if k == kd:
-            src = ops.deep_src(L.nhwc_view(ad[k - 1]), co[k - 1])
-        else:
-            src = ops.deep_src(L.nhwc_view(rd[k - 1]), co[k - 1], table=(tab_d[k - 1][0], tab_d[k - 1][1]), slope=LRELU)
-        # (the innermost level has no down-norm, STCGAN/networks.py:118-124)
-        dbn = table_of(k, False) if k < Lv - 1 else None
-        ops.deep_conv(L.CONV_S2, B, [src], wk, co[k], L.nhwc_view(rd[k]), tickets, ("c", k), bn=dbn)
-    # ---- deep up path: convT_k reads [ReLU(BN_d[k](rd[k])) | ReLU(BN_u[k + 1](rq[k + 1]))] (innermost: ReLU(rd))
-    for k in range(Lv - 1, kd - 1, -1):
-        wt = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_FWD, co[k - 1], cin_t(k), dt)
-        if k == Lv - 1:
-            srcs = [ops.deep_src(L.nhwc_view(rd[k]), co[k], slope=0.0)]
-        else:
-            srcs = [ops.deep_src(L.nhwc_view(rd[k]), co[k], table=(tab_d[k][0], tab_d[k][1]), slope=0.0),
-                    ops.deep_src(L.nhwc_view(rq[k + 1], 0, *S[k + 1]), co[k], table=(tab_u[k + 1][0], tab_u[k + 1][1]),
-                                 slope=0.0)]
-        ops.deep_conv(L.CONVT_S2, B, srcs, wt, co[k - 1], L.nhwc_view(rq[k]), tickets, ("t", k), bn=table_of(k, True))
-    # ---- BN_u[kd] (table from convT_kd) applied into cr[kd - 1]'s up half, read by the per-layer convT_{kd-1}
-    C = co[kd - 1]
-    t = tab_u[kd]
-    ops.bn_apply(B, L.nhwc_view(rq[kd], 0, *S[kd]), C, dt, (t[0], t[1]), L.nhwc_view(cr[kd - 1], C), 0.0)
-    # ---- the deep levels' activations for the backward's weight gradients (side stream, joined at the end)
-    side = None
-    if save:
-        main = torch.cuda.current_stream(dev)
-        side = cache.get("__deep_side__")
-        if side is None:
-            side = cache["__deep_side__"] = torch.cuda.Stream(dev)
-        wait_stream(side, main)
-        with torch.cuda.stream(side):
-            for k in range(kd, Lv):
-                for tns in (rd[k], cr[k], ad[k], rq[k + 1] if k + 1 < Lv else None):
-                    if tns is not None:
-                        tns.record_stream(side)
-                if k < Lv - 1:
-                    ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]),
-                                 LRELU, L.nhwc_view(cr[k], 0), 0.0)
-                    tu = tab_u[k + 1]
-                    ops.bn_apply(B, L.nhwc_view(rq[k + 1], 0, *S[k + 1]), co[k], dt, (tu[0], tu[1]),
-                                 L.nhwc_view(cr[k], co[k]), 0.0)
-                else:
-                    ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, None, L.nhwc_view(cr[k]), 0.0)
-    # ---- up path: levels < kd as gen_forward
-    for k in range(kd - 1, 0, -1):
-        wt = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_FWD, co[k - 1], cin_t(k), dt)
-        tab_u[k], st_u[k] = conv_bn(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
-                                    plan.bnu[k])
-        ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
-                     L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
-    Ho, Wo = 2 * S[1][0], 2 * S[1][1]
-    y = torch.empty((B, plan.out_c, Ho, Wo), dtype=torch.float32, device=dev)
-    wt0 = ops.packed(cache, plan.convT[0].weight, L.PACK_CONVT_FWD, plan.out_c, 2 * co[0], dt)
-    ops.conv(L.CONVT_S2, B, L.nhwc_view(cr[0]), 2 * co[0], wt0, plan.out_c, L.nchw_view(y), dt,
-             bias=plan.convT[0].bias, tanh=True, out_f32=True)
-    if side is not None:
-        wait_stream(torch.cuda.current_stream(dev), side)
     saved = None
     if save:
         saved = dict(S=S, xin=xin, rd=rd, ad=ad, cr=cr, rq=rq, tab_d=tab_d, tab_u=tab_u, st_d=st_d, st_u=st_u,

@@ -315,80 +315,6 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
     return dgamma, dbeta
 
 
-def deep_query(kind, B, gh, gw, ih, iw, cin, cout, force=None):
-    """(workspace bytes, tickets, plan) of stc_deep_conv for these shapes."""
-    key = ("dq", kind, B, gh, gw, ih, iw, cin, cout, None if force is None else tuple(force))
-    r = _MEMO.get(key)
-    if r is None:
-        ws, nt = ctypes.c_int64(), ctypes.c_int32()
-        po = (ctypes.c_int32 * 5)()
-        fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
-        check(lib().stc_deep_conv_query(kind, B, gh, gw, ih, iw, cin, cout, fp, ctypes.byref(ws), ctypes.byref(nt), po),
-              "stc_deep_conv_query")
-        r = _MEMO[key] = (ws.value, nt.value, tuple(po))
-    return r
-
-
-def deep_src(xv, C, table=None, slope=1.0):
-    """One stc_deep_conv source: the view ``xv`` (C channels), through its BatchNorm's (scale, shift) ``table``
-    (None: identity) and the activation ``slope``."""
-    s = L.DeepSrc()
-    s.x = xv
-    s.C = C
-    s.slope = float(slope)
-    s._keep = [xv]
-    if table is not None:
-        s.scale, s.shift = table[0].data_ptr(), table[1].data_ptr()
-        s._keep += list(table)
-    return s
-
-
-def deep_bn(bn, table, stats, running=True):
-    """The output BatchNorm of a stc_deep_conv launch: it writes ``table`` ((2, C): scale, shift) and ``stats``
-    ((mean, rstd)), and (``running``) updates bn's running statistics and batch count."""
-    d = L.DeepBN()
-    d.gamma, d.beta = bn.weight.data_ptr(), bn.bias.data_ptr()
-    d.eps = float(bn.eps)
-    d.momentum = float(bn.momentum if bn.momentum is not None else BN_MOMENTUM)
-    d.mean_out, d.rstd_out = stats[0].data_ptr(), stats[1].data_ptr()
-    d.scale_out, d.shift_out = table[0].data_ptr(), table[1].data_ptr()
-    if running:
-        d.running_mean, d.running_var = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
-        d.num_batches_tracked = bn.num_batches_tracked.data_ptr()
-    d._keep = [bn.weight, bn.bias, table, stats]
-    return d
-
-
-def deep_conv(kind, B, srcs, w_packed, cout, yv, tickets_cache, key, bn=None, force=None):
-    """The U-Net's innermost levels in one launch per layer (stc_deep_conv); ``bn``: a deep_bn() descriptor of the
-    output's BatchNorm (train mode) or None.  ``tickets_cache[key]``: the launch site's persistent tile tickets."""
-    dev = w_packed.device
-    ih, iw = srcs[0].x.H, srcs[0].x.W
-    gh, gw = (ih, iw) if kind == L.CONVT_S2 else (yv.H, yv.W)
-    cin = sum(s.C for s in srcs)
-    nbytes, ntk, plan = deep_query(kind, B, gh, gw, ih, iw, cin, cout, force)
-    tk = tickets_cache.get(key)
-    if tk is None or tk.numel() < ntk:
-        tk = tickets_cache[key] = torch.zeros(max(ntk, 1), dtype=torch.int32, device=dev)
-    ws, nb = _ws(nbytes, dev)
-    arr = (L.DeepSrc * len(srcs))(*srcs)
-    fp = (ctypes.c_int32 * 2)(*force) if force is not None else None
-    timer = _timer
-    if timer is not None:
-        e0, e1 = _main_events()
-    rc = lib().stc_deep_conv(kind, B, len(srcs), arr, ptr(w_packed), cout, yv,
-                             ctypes.byref(bn) if bn is not None else None, fp, ptr(tk), tk.numel(), ptr(ws), nb,
-                             stream())
-    if timer is not None:
-        _disarm()
-    check(rc, "stc_deep_conv")
-    if timer is not None:
-        outs = B * gh * gw * (4 if kind == L.CONVT_S2 else 1)
-        taps = 4 if kind == L.CONVT_S2 else 16  # (the conv's FLOPs, as every other launch counts them)
-        timer.append((f"deep_conv_kernel<{plan[0]}, {plan[1]}>", True, 2.0 * outs * cout * taps * cin, e0, e1,
-                      f"{['conv_s2', 'conv_s1', 'convT', 's1_dgrad'][kind]} B{B} grid{gh}x{gw} cin{cin} cout{cout}"))
-
-
 def bn_finalize_part(part, nch, C, bn, scale_out, shift_out, update_running=True):
     """mean/rstd + (scale, shift) table from conv_stats partials; updates running stats."""
     dev = scale_out.device
