@@ -3,7 +3,9 @@ world 8?  One bench-config train step (bs 32, bf16, 256x256) on one GPU with Buc
 parameter's gradient-ready event, on the stream that wrote it, and each network's finish), then a simulation of
 the RCCL ring all-reduce of the same buckets at world W on one communicator (collectives run one after another
 in ready order): cost = alpha + 2 (W - 1) / W * bytes / busbw.  Prints per network: gradient bytes, the window
-from its first gradient to its backward's end, the exposed time after it for each bucket size and bus bandwidth.
+from its first gradient to its backward's end, the exposed time after it for each bucket size and bus bandwidth,
+without and with overlap_optim (each bucket's share of the measured optimiser update right after its all-reduce;
+reported as the time past the one-GPU step's backward + update).
 usage: exchange_timeline.py [--world 8] [--alpha-us 25]"""
 import argparse
 import json
@@ -64,7 +66,16 @@ def main():
     t1.record()
     torch.cuda.synchronize()
     step_ms = t0.elapsed_time(t1)
-    res = {"step_ms": round(step_ms, 3), "world": a.world, "alpha_us": a.alpha_us, "nets": {}}
+    # the optimiser updates alone (one more step() each on the same gradients: timing only)
+    upd = {}
+    for phase, o in (("D", tr.optim_D), ("G", tr.optim_G)):
+        u0, u1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        u0.record()
+        o.step()
+        u1.record()
+        torch.cuda.synchronize()
+        upd[phase] = u0.elapsed_time(u1)
+    res = {"step_ms": round(step_ms, 3), "world": a.world, "alpha_us": a.alpha_us, "update_ms": upd, "nets": {}}
     ready, fin, flats = {}, {}, {}
     for n in NETS:
         ex = getattr(tr, n).grad_exchange
@@ -84,7 +95,8 @@ def main():
         first = min(ready[id(p)] for n in nets for p in flats[n].params)
         nbytes = sum(4 * flats[n].numel for n in nets)
         sims[phase] = {"grad_MB": round(nbytes / 1e6, 1), "first_ready_ms": round(first, 3),
-                       "backward_end_ms": round(end, 3), "window_ms": round(end - first, 3), "exposed_ms": {}}
+                       "backward_end_ms": round(end, 3), "window_ms": round(end - first, 3), "exposed_ms": {},
+                       "exposed_overlap_optim_ms": {}}
         for mb in (4, 8, 16, 32, 64, 128):
             bks = []
             for n in nets:
@@ -92,10 +104,15 @@ def main():
                     bks.append((max(ready[i] for i in ids), b))
             bks.sort()
             for bw in (150, 300, 600):
-                t = 0.0
+                t = u = 0.0
                 for r, b in bks:
                     t = max(t, r) + a.alpha_us * 1e-3 + 2 * (a.world - 1) / a.world * b / (bw * 1e9) * 1e3
+                    # overlap_optim: the bucket's share of the update right after its all-reduce, one bucket at a
+                    # time on the optimiser stream
+                    u = max(u, t) + upd[phase] * b / nbytes
                 sims[phase]["exposed_ms"][f"{mb}MB@{bw}GB/s"] = round(max(0.0, t - end), 3)
+                # time past the eager step (whose update follows its backward): (update done) - (end + update)
+                sims[phase]["exposed_overlap_optim_ms"][f"{mb}MB@{bw}GB/s"] = round(u - end - upd[phase], 3)
     res["phases"] = sims
     print(json.dumps(res, indent=1))
 

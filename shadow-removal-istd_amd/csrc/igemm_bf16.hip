@@ -667,10 +667,10 @@ struct Bf16Problem {
 // Ticket counters of the in-launch split-K.  A region belongs to one (device, stream, capture): launches on one stream
 // run one after another and every launch leaves its counters zero, so eager launches on a stream share its region; a
 // launch made while the stream is being captured gets a region of that capture (the graph's replays may run beside
-// eager work on the same stream handle, or on another stream), kept for the process lifetime.  A region is zeroed on
-// the stream that first uses it (hipMemsetAsync: ordered before that launch -- inside a capture it becomes the graph's
-// memset node), so no device-wide synchronisation.  The pool itself is allocated outside any capture (the eager
-// warm-up steps of STCGAN.capture make the first split-K launch).
+// eager work on the same stream handle, or on another stream), kept for the process lifetime.  The pool is allocated
+// and zeroed once, outside any capture, by the first split-K launch of the device (its stream waits for the zeroing:
+// no device-wide synchronisation); regions need no zeroing of their own.  (A per-region hipMemsetAsync captured into
+// the graph left a replay launched on another stream with stale counters on this ROCm -- no tile finished.)
 constexpr int kTicketRegion = 4096, kTicketRegions = 512;  // (8 MiB per device: streams are pooled)
 static unsigned* splitk_tickets(hipStream_t st, int tiles) {
   static std::mutex mu;
@@ -688,17 +688,17 @@ static unsigned* splitk_tickets(hipStream_t st, int tiles) {
   if (!pool[dev]) {
     if (cs != hipStreamCaptureStatusNone) return nullptr;
     void* q = nullptr;
-    if (hipMalloc(&q, (size_t)kTicketRegion * kTicketRegions * sizeof(unsigned)) != hipSuccess) return nullptr;
+    const size_t bytes = (size_t)kTicketRegion * kTicketRegions * sizeof(unsigned);
+    if (hipMalloc(&q, bytes) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(q, 0, bytes, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return nullptr;
     pool[dev] = (unsigned*)q;
   }
   const auto key = std::make_tuple(dev, (uintptr_t)st, cap);
   auto it = region.find(key);
   if (it != region.end()) return pool[dev] + (size_t)it->second * kTicketRegion;
   if (used[dev] >= kTicketRegions) return nullptr;
-  unsigned* r = pool[dev] + (size_t)used[dev] * kTicketRegion;
-  if (hipMemsetAsync(r, 0, (size_t)kTicketRegion * sizeof(unsigned), st) != hipSuccess) return nullptr;
-  region[key] = used[dev]++;
-  return r;
+  region[key] = used[dev];
+  return pool[dev] + (size_t)used[dev]++ * kTicketRegion;
 }
 
 // Shared planning for query and launch.

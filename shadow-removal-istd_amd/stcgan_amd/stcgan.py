@@ -118,14 +118,17 @@ class STCGAN(object):
         # each network's gradients live in one flat buffer (parallel.FlatGrads), cut into buckets that the
         # engine reports complete while the backward runs (parallel.BucketExchange): with data parallelism each
         # bucket is averaged over the ranks (RCCL) right then.  overlap_optim: the optimiser also updates each
-        # bucket right after (optim.Adam.overlap) -- bit-identical, but off by default: the step is GPU-bound,
-        # and the updates' HBM traffic only moved time into the backward's kernels (round-3 A/B, scripts/
-        # ab_overlap.py: 13.22 vs 13.05 ms/step)
+        # bucket right after (optim.Adam.overlap) -- bit-identical.  On by default with data parallelism: the
+        # update of the early buckets then runs while the last ones are still being exchanged, so the G step's
+        # tail after its backward is the last bucket's all-reduce + its update, not the whole exchange + the whole
+        # update (scripts/exchange_timeline.py).  Off at world 1, where there is nothing to hide: the updates' HBM
+        # traffic only moved time into the backward's kernels (round-3 A/B, scripts/ab_overlap.py: 13.22 vs 13.05
+        # ms/step).
         world = parallel.world()
         self.bucket_mb = float(getattr(args, "bucket_mb", 16 if world > 1 else 8))
         for net in (self.G1, self.G2, self.D1, self.D2):
             net.grad_exchange = parallel.BucketExchange(parallel.flat_grads(net), self.bucket_mb)
-        self.set_overlap_optim(bool(getattr(args, "overlap_optim", False)))
+        self.set_overlap_optim(bool(getattr(args, "overlap_optim", world > 1)))
         # discriminators on side HIP streams (train_step / _lanes); off for a strictly serial step
         self.streams = bool(getattr(args, "streams", True))
         self.lane_carry = bool(getattr(args, "lane_carry", True))
