@@ -516,13 +516,17 @@ struct WhGeom {
   static constexpr int TR = 64 / TC;                 // grid rows per K-step
   static constexpr int NR = S1 ? TR + 3 : 2 * TR + 2;  // patch rows
   static constexpr int NPL = S1 ? 1 : 2;             // column planes
-  static constexpr int NPOS = TC + 16;               // positions per plane line (>= TC + 3, whole 16-groups)
+  // positions per plane line: >= TC + 3, whole 16-groups -- TC = 8 (8 x 8 grids, a K-step = one whole image): 17, an
+  // odd count, so that the transposed reads of K rows q and q + 8 (grid rows ty and ty + 1: two patch rows = 4 lines
+  // apart) land 128 B apart mod 256 (different banks)
+  static constexpr int NPOS = TC == 8 ? 17 : TC + 16;
   static constexpr int SLOTS = NR * NPL * NPOS;      // 32-B slots
   static constexpr int PBR = (SLOTS + 31) / 32;      // 1 KiB pieces of the patch
   static constexpr int PB = (PBR + 3) / 4 * 4;       // padded to whole pieces per loader wave
   static constexpr int TILEA = 64 * 128 * 2, TILEB = PB * 1024, STAGE = TILEA + TILEB;
 };
-static_assert(4 * WhGeom<64>::STAGE <= 163840 && 4 * WhGeom<32>::STAGE <= 163840 && 4 * WhGeom<16>::STAGE <= 163840,
+static_assert(4 * WhGeom<64>::STAGE <= 163840 && 4 * WhGeom<32>::STAGE <= 163840 && 4 * WhGeom<16>::STAGE <= 163840 &&
+                  4 * WhGeom<8>::STAGE <= 163840,
               "halo wgrad LDS");
 __device__ __forceinline__ int wh_perm(int pos) { return pos ^ (((pos >> 3) & 1) << 2); }
 
@@ -762,7 +766,7 @@ static bool wb_halo_ok(int GH, int GW, int stride, int R, int Cg) {
   if (Cg % 16 != 0 || R < 96) return false;
   if (wb_halo_s1(GH, GW, stride)) return true;
   if (!(stride == 2 || stride == 0)) return false;
-  if (!(GW == 16 || GW == 32 || GW == 64 || GW == 128)) return false;
+  if (!(GW == 8 || GW == 16 || GW == 32 || GW == 64 || GW == 128)) return false;
   return GH % (64 / std::min(GW, 64)) == 0;
 }
 
@@ -787,7 +791,9 @@ static WbPlan wb_plan(int B, int GH, int GW, int stride, int R, int Cg, const in
     // (R <= 64: the 128 x 128 loader tile beats the 64 x 128 tile on the first layers' 524288-pixel problems even
     // with half its rows idle, 32-38 us against 40-45: profiles/r04/wgrad/tune_s1.log)
     else if (R <= 64 && P < 65536) cfg = 1;
-    else if (halo && P >= 4096) cfg = WB_HALO;
+    // (8 x 8 grids, P = 2048 at bs 32 -- the generator's 16 -> 8 conv and 8 -> 16 ConvT: the halo tile too, whose
+    // patch stages each G pixel once instead of once per tap: profiles/r06/wgrad8/)
+    else if (halo && (P >= 4096 || (GW == 8 && P >= 2048))) cfg = WB_HALO;
     else if (ncol >= 1024 && ((R >= 512 && P >= 16384) || (R >= 256 && P >= 65536))) cfg = 3;
     // 128x128 + 4 loader waves, 3-stage ring (96 KiB: a 64 KiB conv block still fits beside it): 5-13 % under
     // cfg 0 in isolation, -0.16 ms per train step in situ (profiles/r03/diag/plan_ab.log)
@@ -882,7 +888,8 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
   const int htc = std::min(p.GW, 64);
   const size_t lds = pl.cfg == WB_HALO
                          ? (size_t)4 * (hs1 ? WhGeom<32, true>::STAGE : htc == 64 ? WhGeom<64>::STAGE
-                                                                       : htc == 32 ? WhGeom<32>::STAGE : WhGeom<16>::STAGE)
+                                                                       : htc == 32 ? WhGeom<32>::STAGE
+                                                                       : htc == 16 ? WhGeom<16>::STAGE : WhGeom<8>::STAGE)
                          : (size_t)kWbCfg[pl.cfg].stages * WB_BK * (pl.BM + pl.BN) * 2;
   if (!pl.slab) {
     p.dW = dW;
@@ -913,7 +920,8 @@ int wgrad_bf16(int B, int stride, stc_view D, int R, stc_view G, int Cg, int Cg_
       if (hs1) hipLaunchKernelGGL((wgrad_halo_kernel<32, true>), grid, dim3(512), lds, st, p);
       else if (htc == 64) hipLaunchKernelGGL((wgrad_halo_kernel<64, false>), grid, dim3(512), lds, st, p);
       else if (htc == 32) hipLaunchKernelGGL((wgrad_halo_kernel<32, false>), grid, dim3(512), lds, st, p);
-      else hipLaunchKernelGGL((wgrad_halo_kernel<16, false>), grid, dim3(512), lds, st, p);
+      else if (htc == 16) hipLaunchKernelGGL((wgrad_halo_kernel<16, false>), grid, dim3(512), lds, st, p);
+      else hipLaunchKernelGGL((wgrad_halo_kernel<8, false>), grid, dim3(512), lds, st, p);
       break;
     default:
       if (p.pmode) hipLaunchKernelGGL((wgrad_bf16_ld_kernel<128, 128, 2, 2, false, true, 4, 3>), grid, dim3(512), lds, st, p);

@@ -472,6 +472,11 @@ WGRAD_FORCED = [  # (case, tile config, pixel splits): the 8-wave tiles on ragge
     (("convT", 2, 2, 128, 64, 16, 16), 8, 0),
     (("convT", 2, 3, 256, 32, 32, 32), 8, 4),
     (("convT", 2, 1, 128, 16, 64, 64), 8, 1),
+    # 8-wide grids (a K-step = one whole 8 x 8 image; 17-position plane lines): both roles, ragged R, splits
+    (("conv", 2, 4, 64, 128, 16, 16), 8, 0),
+    (("conv", 2, 5, 32, 96, 16, 16), 8, 2),
+    (("convT", 2, 3, 128, 64, 8, 8), 8, 0),
+    (("convT", 2, 2, 48, 128, 8, 8), 8, 3),
     # the stride-1 halo tile (PatchGAN layer 4: D = dy 31 x 31 run as 32 x 32, G = x 32 x 32)
     (("conv", 1, 2, 64, 128, 32, 32), 8, 0),
     (("conv", 1, 1, 256, 512, 32, 32), 8, 3),
@@ -531,10 +536,11 @@ def test_wgrad_rows_narrow_s1(B, Cin, H, W, rows, dt):
 
 
 def test_wgrad_halo_plan_automatic():
-    """The train step's stride-2 weight gradients with a 16..128-wide grid and 16-channel groups take the halo tile
-    (plan config 8); the narrow first layers (Cg = 8) and the deep 8x8 .. 1x1 grids keep the im2col tiles."""
+    """The train step's stride-2 weight gradients with an 8..128-wide grid and 16-channel groups take the halo tile
+    (plan config 8); the narrow first layers (Cg = 8) and the deep 4x4 .. 1x1 grids keep the im2col tiles."""
     for (B, gh, R, Cg) in ((32, 64, 128, 64), (32, 32, 256, 128), (32, 16, 512, 256), (32, 64, 256, 64),
-                           (32, 32, 512, 128), (32, 16, 1024, 256), (32, 31, 512, 256)):
+                           (32, 32, 512, 128), (32, 16, 1024, 256), (32, 31, 512, 256), (32, 8, 512, 512),
+                           (32, 8, 1024, 512)):
         assert ops.wgrad_query(B, gh, gh, R, Cg, BF)[1][0] == 8, (B, gh, R, Cg)
-    for (B, gh, R, Cg) in ((32, 128, 64, 8), (32, 8, 512, 512), (32, 2, 512, 512)):
+    for (B, gh, R, Cg) in ((32, 128, 64, 8), (32, 4, 512, 512), (32, 2, 512, 512)):
         assert ops.wgrad_query(B, gh, gh, R, Cg, BF)[1][0] != 8, (B, gh, R, Cg)
