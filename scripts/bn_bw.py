@@ -39,5 +39,5 @@ for H, C in ((128, 64), (64, 128), (32, 256), (16, 512)):
     g2 = torch.randn_like(x)
     us3 = timed(lambda: ops.bn_backward(B, L.nhwc_view(x), C, dt, L.nhwc_view(y1), g1=L.nhwc_view(g1), s1=0.2,
                                         g2=L.nhwc_view(g2), s2=0.0))
-    print(f"{H}x{H}x{C}: apply {us:6.1f} us {2 * n / us / 1e3:5.2f} TB/s | apply2 {us2:6.1f} us "
-          f"{3 * n / us2 / 1e3:5.2f} TB/s | bwd(no stats) {us3:6.1f} us {4 * n / us3 / 1e3:5.2f} TB/s", flush=True)
+    print(f"{H}x{H}x{C}: apply {us:6.1f} us {2 * n / us / 1e3:5.2f} GB/s | apply2 {us2:6.1f} us "
+          f"{3 * n / us2 / 1e3:5.2f} GB/s | bwd(no stats) {us3:6.1f} us {4 * n / us3 / 1e3:5.2f} GB/s", flush=True)
