@@ -136,6 +136,21 @@ int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin, const void
                     const stc_bnb_fuse* bnb, float* part2, int nchunks,
                     void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ---- input-gradient conv with the activation backward of a layer without BatchNorm ---------------
+ * The backward of the first conv's activation (no BatchNorm there): G's outermost level, whose output feeds
+ * the next conv through LeakyReLU(0.2) and the skip through ReLU (STCGAN/networks.py:99-106, the in-place skip
+ * activation), and the PatchGAN's first layer (networks.py:165-166: LeakyReLU(0.2)).  Replaces stc_conv_fwd into
+ * a gradient tensor followed by stc_bn_bwd_apply(no table): with this conv's output v (the gradient reaching the
+ * activation, slope_self) and the optional second gradient g_other (slope_other) at the same pixel,
+ *   out = g_other*act'(x, slope_other) + v*act'(x, slope_self)    (x = the activation's input)
+ * is stored in place of v, rounded to bf16 from the same fp32 values as the two-call form (bit-identical), with
+ * no intermediate gradient written or re-read.  stc_conv_bwd_act_ok: 1 when the layer takes the halo kernels
+ * with 16-byte NHWC bf16 views of one extent (else use the two-call form).                              */
+int stc_conv_bwd_act_ok(int dtype, int kind, int B, stc_view dy, int Cin, int Cout, stc_view out, stc_view x,
+                        stc_view g_other);
+int stc_conv_bwd_act(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout,
+                     stc_view out, stc_view x, float slope_self, stc_view g_other, float slope_other, void* stream);
+
 /* ---- conv with an activation epilogue (the layers without BatchNorm) -----------------------------
  * The outermost down conv of the generators (STCGAN/networks.py:99-101: conv, then LeakyReLU(0.2) for the
  * next conv and -- in-place on the skip -- ReLU for the up path) and the PatchGAN's first conv

@@ -497,7 +497,7 @@ int halo_launch(GParams& p, hipStream_t st, int shape) {
   const bool t2 = convt && bn == 64 && (shape == 6 || (shape != 5 && p.mtiles * p.ntiles * 2 >= 256));
   const int blocks = p.mtiles * p.ntiles * (t2 ? 2 : p.nphase);
   const dim3 grid((unsigned)blocks);
-  const bool bnb = p.part2 != nullptr;
+  const bool bnb = p.part2 != nullptr || p.bnb_act;
   // >= 512 blocks: the 4-wave 80 KiB block, two per CU; fewer: the 8-wave block (one per CU, all CUs busy)
 #ifndef STC_EXP_TWO_MIN
 #define STC_EXP_TWO_MIN 512

@@ -673,7 +673,8 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
                   const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr,
-                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f);
+                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f,
+                  int bnb_act = 0);
 bool bf16_conv_act_ok(int kind, int B, const stc_view& x, int Cin, int Cout, const stc_view& y1, const stc_view* y2);
 bool bf16_narrow_eligible(int kind, int Cin, int Cout);
 int64_t bf16_narrow_workspace(int kind, int B, int GH, int GW, int Cin, int Cout);
@@ -904,6 +905,33 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
   STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks_ex)", nchunks, need);
   return stc_bn_bwd_reduce(dtype, B, bnb->x, bnb->C, bnb->scale, bnb->shift, bnb->mean, bnb->rstd, g1, bnb->slope_self,
                            bnb->g_other, bnb->slope_other, part2, need, stream);
+}
+
+// ---- input-gradient conv + activation backward (layers without BatchNorm)
+namespace stc {
+bool bf16_conv_bwd_act_ok(int kind, int B, const stc_view& dy, int Cin, int Cout, const stc_view& out, const stc_view& x,
+                          const stc_view* g_other);
+}  // namespace stc
+extern "C" int stc_conv_bwd_act_ok(int dtype, int kind, int B, stc_view dy, int Cin, int Cout, stc_view out, stc_view x,
+                                   stc_view g_other) {
+  if (kind < 0 || kind > 3 || !bf16_path(dtype, kind, Cin, Cout)) return 0;
+  return bf16_conv_bwd_act_ok(kind, B, dy, Cin, Cout, out, x, &g_other) ? 1 : 0;
+}
+
+extern "C" int stc_conv_bwd_act(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout,
+                                stc_view out, stc_view x, float slope_self, stc_view g_other, float slope_other,
+                                void* stream) {
+  STC_REQUIRE(stc_conv_bwd_act_ok(dtype, kind, B, dy, Cin, Cout, out, x, g_other),
+              "stc_conv_bwd_act: no fused activation backward for this shape / view (check stc_conv_bwd_act_ok)");
+  stc_bnb_fuse f{};
+  f.x = x;
+  f.g_other = g_other;
+  f.slope_self = slope_self;
+  f.slope_other = slope_other;
+  f.C = Cout;
+  f.ch_off = 0;
+  return bf16_conv_fwd(kind, B, dy, Cin, w_packed, Cout, out, nullptr, 0, 0, nullptr, 0, nullptr, nullptr, 0,
+                       (hipStream_t)stream, &f, nullptr, nullptr, 0, 0.f, 0.f, 1);
 }
 
 // ---- conv + activation epilogue (layers without BatchNorm)

@@ -919,7 +919,8 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
                   const float* bias, int epi_tanh, int out_f32, float* stats, int stats_chunks,
                   const int32_t* force, void* ws, int64_t ws_bytes, hipStream_t st,
                   const stc_bnb_fuse* bnb = nullptr, float* part2 = nullptr,
-                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f) {
+                  const stc_view* act2 = nullptr, int act_n = 0, float act_s1 = 0.f, float act_s2 = 0.f,
+                  int bnb_act = 0) {
   const Geometry g = geometry(kind);
   const int taps = g.taps_lg_tw == 2 ? 16 : 4;
   GParams p{};
@@ -949,11 +950,12 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
   STC_REQUIRE(!epi_tanh, "bf16 conv: the MFMA tile kernel has no tanh epilogue");
   if (!p.vec_out) STC_REQUIRE(!stats || out_f32 == 0, "bf16 conv: stats need a bf16 output");
   if (bnb) {
-    STC_REQUIRE(p.vec_out && part2 && !stats, "bf16 conv: fused BN backward needs a 16-byte NHWC bf16 output");
+    STC_REQUIRE(p.vec_out && (part2 || bnb_act) && !stats, "bf16 conv: fused BN backward needs a 16-byte NHWC bf16 output");
     STC_REQUIRE(bnb->C % 8 == 0 && bnb->ch_off % 8 == 0 && bnb->x.cs == 1 && bnb->x.co % 8 == 0 && bnb->x.ps % 8 == 0 &&
                     (!bnb->g_other.p || (bnb->g_other.cs == 1 && bnb->g_other.co % 8 == 0 && bnb->g_other.ps % 8 == 0)) &&
-                    bnb->scale && bnb->shift && bnb->mean && bnb->rstd,
+                    (bnb_act || (bnb->scale && bnb->shift && bnb->mean && bnb->rstd)),
                 "bf16 conv: bad fused BN-backward arguments");
+    p.bnb_act = bnb_act;
     p.part2 = part2;
     p.bx = (const char*)bnb->x.p; p.bx_bs = bnb->x.bs; p.bx_rs = bnb->x.rs; p.bx_ps = bnb->x.ps; p.bx_co = bnb->x.co;
     p.bxH = bnb->x.H; p.bxW = bnb->x.W;
@@ -970,6 +972,13 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
     if (act_n == 2) {
       p.c2 = (char*)act2->p; p.c2_bs = act2->bs; p.c2_rs = act2->rs; p.c2_ps = act2->ps; p.c2_co = act2->co;
     }
+  }
+  if (bnb_act) {  // (the halo kernels' epilogue only: stc_conv_bwd_act_ok)
+    STC_REQUIRE(!force && !part2 && bnb->C == Cout && bnb->ch_off == 0 && halo_plan(nullptr, kind, B, p.GH, p.GW, Cin, Cout) &&
+                    halo_eligible(kind, B, x, Cin, Cout, y),
+                "bf16 conv: no fused activation backward for this shape / view (check stc_conv_bwd_act_ok)");
+    p.ws = nullptr;
+    return halo_launch(p, st, 0);
   }
   if (p.vec_out && !force && !stats && bnb && !bnb->g_other.p && stem_s1d_eligible(kind, B, x, Cin, Cout, y)) {
     p.ws = nullptr;
@@ -988,6 +997,20 @@ int bf16_conv_fwd(int kind, int B, stc_view x, int Cin, const void* w_packed, in
   }
   STC_REQUIRE(!(force && force[0] == HALO_CFG), "bf16 conv: the halo kernel does not take this shape / view");
   return bf16_igemm_launch(p, force, ws, ws_bytes, stats, stats_chunks, st);
+}
+
+// The fused activation backward (stc_conv_bwd_act) runs in the halo kernels' BN-backward epilogue: the layer takes
+// the halo route with 16-byte NHWC bf16 views of one extent.
+bool bf16_conv_bwd_act_ok(int kind, int B, const stc_view& dy, int Cin, int Cout, const stc_view& out, const stc_view& x,
+                          const stc_view* g_other) {
+  if (!bf16_conv_eligible(kind, B, dy, Cin, Cout) || !vec_out_ok(B, out, Cout, 0) || Cout % 8 != 0) return false;
+  const int Hg = kind == STC_CONVT_S2 ? dy.H : out.H, Wg = kind == STC_CONVT_S2 ? dy.W : out.W;
+  if (!halo_plan(nullptr, kind, B, Hg, Wg, Cin, Cout) || !halo_eligible(kind, B, dy, Cin, Cout, out)) return false;
+  auto vec = [&](const stc_view& v) {
+    return v.H == out.H && v.W == out.W && v.cs == 1 && v.co % 8 == 0 && v.ps % 8 == 0 && v.rs % 8 == 0 && v.bs % 8 == 0 &&
+           ((uintptr_t)v.p & 15) == 0 && (long long)B * v.bs < (1ll << 31);
+  };
+  return x.p && vec(x) && (!g_other || !g_other->p || vec(*g_other));
 }
 
 // Partial count of the fused BN-backward sums for these views: the route bf16_conv_fwd takes for a BN-backward

@@ -47,6 +47,10 @@ struct GParams {
   const float *bsc, *bsh, *bmu, *brs;
   float bs_self, bs_other;
   int bC, bch_off;
+  // bnb_act = 1 (stc_conv_bwd_act, layers with no BatchNorm): the BNB epilogue stores dn itself -- this conv's output
+  // v (gradient reaching an activation) through the activation, nn = x (the activation's input), plus the second
+  // gradient -- in place of v; no table, no sums (part2 unused).
+  int bnb_act;
   int phase_major;  // grid linear over (tile, phase), phase fastest (set by the launcher)
   // Activation epilogue (layers with no BatchNorm: the first conv of G / D, STCGAN/networks.py:99,165-166):
   // act_n = 1 or 2 activated copies of the bf16-rounded output, out1 = act(v, act_s1) into c (instead of the
@@ -106,6 +110,29 @@ __device__ __forceinline__ void bnb_accum(const GParams& p, int b, int oy, int o
     sa[e] += dn;
     sb[e] += dn * (xv[e] - p.bmu[ch + e]) * p.brs[ch + e];
   }
+}
+
+// 8 channels of the activation backward with no BatchNorm (stc_conv_bwd_act): dn = g * act'(x, s_other) +
+// v * act'(x, s_self), summed in stc_bn_bwd_apply's order (second gradient first), rounded to bf16 -- the values
+// conv + stc_bn_bwd_apply(no table) write, bit for bit
+__device__ __forceinline__ uint4 act_bwd_bf16x8(uint4 v, uint4 x, uint4 g, bool has_g, float s_self, float s_other) {
+  const unsigned wv[4] = {v.x, v.y, v.z, v.w}, wx[4] = {x.x, x.y, x.z, x.w}, wg[4] = {g.x, g.y, g.z, g.w};
+  unsigned o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float d[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float vv = __uint_as_float(h ? (wv[q] & 0xffff0000u) : (wv[q] << 16));
+      const float xx = __uint_as_float(h ? (wx[q] & 0xffff0000u) : (wx[q] << 16));
+      float dn = 0.f;
+      if (has_g) dn += __uint_as_float(h ? (wg[q] & 0xffff0000u) : (wg[q] << 16)) * dact(xx, s_other);
+      dn += vv * dact(xx, s_self);
+      d[h] = dn;
+    }
+    o[q] = pack_bf16x2(d[0], d[1]);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -510,9 +537,11 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
           if (p.vmask && (y >= p.vh || x >= p.vw)) continue;
           const int oy = y * p.os + p.oy0[ph], ox = x * p.os + p.ox0[ph];
           const long long off = (long long)b * p.c_bs + (long long)oy * p.c_rs + (long long)ox * p.c_ps + p.c_co + n;
-          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) = tv[u];
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(p.c) + off) =
+              p.bnb_act && ok[u] ? act_bwd_bf16x8(tv[u], xr[u], gr[u], p.bg != nullptr, p.bs_self, p.bs_other) : tv[u];
         }
       }
+      if (p.bnb_act) continue;  // (no BatchNorm: no sums)
 #pragma unroll
       for (int u = 0; u < G; ++u) {
         if (!ok[u]) continue;
@@ -531,6 +560,7 @@ __device__ __forceinline__ void igemm_epilogue(const GParams& p, floatx4 (&acc)[
         }
       }
     }
+    if (p.bnb_act) return;
     // per-tile reduction over the threads sharing a channel chunk (fixed order)
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [threads][16]

@@ -59,6 +59,8 @@ _SIGS = {
                                _i64, _vp]),
     "stc_conv_fwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View]),
     "stc_conv_fwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _f32, View, _f32, _vp, _vp, _i64, _vp]),
+    "stc_conv_bwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View, View]),
+    "stc_conv_bwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, View, _f32, View, _f32, _vp]),
     "stc_set_splitk_inlaunch": (_i32, [_i32]),
     "stc_conv_wgrad": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _vp, _i32, _f32, View, _i32, _i32, _vp, _vp, _i32,
                               _f32, _vp, _vp, _i64, _vp]),

@@ -437,10 +437,16 @@ def gen_backward(plan, saved, gy, dt, cache, need_src, W):
         xv = L.nhwc_view(rd[k - 1])
         g1 = L.nhwc_view(gcat[k - 1], 0, *S[k])
         if k - 1 == 0:
-            ops.conv(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt)
+            # r_0 has no BatchNorm: the activation backward (LeakyReLU into conv_1, ReLU into the skip) in the
+            # input-gradient conv's epilogue when it has one (no ga tensor), else conv + bn_backward
+            if TRACE is not None or (ga.shape[1], ga.shape[2]) != tuple(S[k]) or not ops.conv_act_backward(
+                    L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(dr), dt, act_x=xv, s_self=LRELU, g_other=g1,
+                    s_other=0.0):
+                ops.conv(L.CONVT_S2, B, drv, co[k], wd, cprev, L.nhwc_view(ga), dt)
+                ops.bn_backward(B, xv, cprev, dt, L.nhwc_view(dr), g1=g1, s1=0.0, g2=L.nhwc_view(ga, 0, *S[k]),
+                                s2=LRELU)
             if need_w:
                 W.done([plan.conv[k].weight], lane)
-            ops.bn_backward(B, xv, cprev, dt, L.nhwc_view(dr), g1=g1, s1=0.0, g2=L.nhwc_view(ga, 0, *S[k]), s2=LRELU)
         else:  # BN reduction fused into the input-gradient conv that produces ga
             mean, rstd = st_d[k - 1]
             t = tab_d[k - 1]
@@ -626,11 +632,13 @@ def disc_backward(plan, saved, gout, dt, cache, need_src, W):
         gn = _nhwc(B, ph, pw, cin, dt, dev)
         _trace("D", ("ga", i), ga)
         xv = L.nhwc_view(raw[i])
-        if tabs[i] is None:
-            ops.conv(dkind, B, gv, gch, wd, cin, L.nhwc_view(ga), dt)
+        if tabs[i] is None:  # (no BatchNorm: the LeakyReLU backward in the conv epilogue when it has one)
+            if TRACE is not None or not ops.conv_act_backward(dkind, B, gv, gch, wd, cin, L.nhwc_view(gn), dt, act_x=xv,
+                                                              s_self=LRELU):
+                ops.conv(dkind, B, gv, gch, wd, cin, L.nhwc_view(ga), dt)
+                ops.bn_backward(B, xv, cin, dt, L.nhwc_view(gn), g1=L.nhwc_view(ga), s1=LRELU)
             if need_w:
                 W.done(own, lane)
-            ops.bn_backward(B, xv, cin, dt, L.nhwc_view(gn), g1=L.nhwc_view(ga), s1=LRELU)
         else:
             mean, rstd = stats[i]
             bn = plan.bns[i - 2]

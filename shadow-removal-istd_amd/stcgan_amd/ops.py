@@ -149,6 +149,9 @@ FORCE_WGRAD = {}
 # conv + activation epilogue for the layers without BatchNorm (stc_conv_fwd_act); False (A/B scripts): conv +
 # bn_apply
 FUSE_ACT = True
+# input-gradient conv + activation backward for the same layers (stc_conv_bwd_act); False (A/B, tests): conv +
+# bn_backward(no table)
+FUSE_ACT_BWD = True
 
 
 def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bias=None):
@@ -179,6 +182,36 @@ def conv_act(kind, B, xv, cin, w_packed, cout, y1v, s1, dt, y2v=None, s2=0.0, bi
                 and xv.H == 2 * gh and gh % 8 == 0)
         _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1,
                     name=f"stem_conv_kernel<{xv.W}, {2 if y2v is not None else 1}>" if stem else None)
+    return True
+
+
+def conv_act_backward(kind, B, xv, cin, w_packed, cout, yv, dt, act_x, s_self, g_other=None, s_other=0.0):
+    """Input-gradient conv (output yv) whose output reaches an activation with no BatchNorm: yv receives
+    g_other*act'(x, s_other) + out*act'(x, s_self) (x = ``act_x``, the activation's input) from the conv epilogue,
+    bit-identical to conv + bn_backward(no table) without the intermediate gradient tensor.  Returns False (nothing
+    launched) when the layer has no such epilogue: the caller then runs the two-call form."""
+    if not FUSE_ACT_BWD or dt != torch.bfloat16:
+        return False
+    l = lib()
+    g2 = g_other if g_other is not None else L.NULL_VIEW
+    key = ("actb", kind, B, cin, cout, L.layout_key(xv), L.layout_key(yv), L.layout_key(act_x),
+           L.layout_key(g2) if g_other is not None else None)
+    ok = _MEMO.get(key)
+    if ok is None:
+        ok = _MEMO[key] = bool(l.stc_conv_bwd_act_ok(L.dtype_code(dt), kind, B, xv, cin, cout, yv, act_x, g2))
+    if not ok:
+        return False
+    timer = _timer
+    if timer is not None:
+        e0, e1 = _main_events()
+    rc = l.stc_conv_bwd_act(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, act_x, float(s_self), g2,
+                            float(s_other), stream())
+    if timer is not None:
+        _disarm()
+    check(rc, "stc_conv_bwd_act")
+    if timer is not None:
+        gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
+        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=True)
     return True
 
 
