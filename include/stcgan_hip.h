@@ -135,6 +135,24 @@ int stc_conv_bwd_bn_chunks_ex(int dtype, int kind, int B, stc_view dy, int Cin, 
 int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout, stc_view out,
                     const stc_bnb_fuse* bnb, float* part2, int nchunks,
                     void* workspace, int64_t workspace_bytes, void* stream);
+/* stc_conv_bwd_bn + stc_bn_bwd_apply from one call: the BN layer's input gradient dx (and dgamma / dbeta), with the
+ * conv output at channels ch_off.. over x's extent as the gradient reaching the BN output (through slope_self).  */
+int stc_conv_bwd_bn_apply(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout,
+                          stc_view out, const stc_bnb_fuse* bnb, float* part2, int nchunks, const float* gamma,
+                          stc_view dx, float* dgamma, float* dbeta, void* workspace, int64_t workspace_bytes,
+                          void* stream);
+
+/* ---- conv + train-mode BatchNorm + activation in one call -----------------------------------------
+ * A BN layer's forward (STCGAN/networks.py:104-109,118-128,167-171: conv -> BatchNorm2d (batch statistics, running
+ * statistics update) -> LeakyReLU / ReLU): stc_conv_fwd_ex with the statistics into fws, stc_bn_finalize, then
+ * stc_bn_apply of apply_x (the conv output, or its cropped extent) into y1 [and y2] -- the same three launches,
+ * enqueued by one call.  fws (fp32) = [nchunks*Cout*4 partials | mean | rstd | scale | shift], nchunks from
+ * stc_conv_fwd_query; y1.p == NULL skips the apply.                                                       */
+int stc_conv_bn_fwd(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout, stc_view y,
+                    float* fws, int nchunks, const float* gamma, const float* beta, float* running_mean,
+                    float* running_var, int64_t* num_batches_tracked, float momentum, float eps, stc_view apply_x,
+                    stc_view y1, float slope1, stc_view y2, float slope2, void* workspace, int64_t workspace_bytes,
+                    void* stream);
 
 /* ---- input-gradient conv with the activation backward of a layer without BatchNorm ---------------
  * The backward of the first conv's activation (no BatchNorm there): G's outermost level, whose output feeds
@@ -443,6 +461,10 @@ int stc_grad_accumulate(int ntensors, float* const* dst, const float* const* src
  * -- not around the split-K / split-pixel reduction it may enqueue afterwards -- then disarms.  Both
  * NULL disarms.  Thread-local one-shot state: calls on other threads are unaffected.               */
 int stc_time_next_main_kernel(void* ev_begin, void* ev_end);
+/* waiter (hipStream_t) waits for everything enqueued so far on src: a pooled event (never destroyed, so it also
+ * outlives a graph capture) recorded on src and waited on by waiter -- the host schedule's stream forks and joins
+ * (the reference's implicit single stream has none; STCGAN/stcgan.py:203-312 runs the same work serially).     */
+int stc_stream_wait(void* waiter, void* src);
 const char* stc_last_error(void);
 int stc_version(void);
 

@@ -770,6 +770,26 @@ extern "C" int stc_conv_fwd_ex(int dtype, int kind, int B, stc_view x, int Cin, 
   return stc_chan_stats(dtype, B, y, Cout, stats_part, stats_chunks, stream);
 }
 
+// conv + BatchNorm (train mode) + activation as one call: stc_conv_fwd_ex with the batch statistics, stc_bn_finalize,
+// stc_bn_apply -- the three launches of a BN layer's forward, enqueued by one host call (the train step makes ~50
+// of them; each separate call costs host time the GPU then waits for).  fws = [stats partials nchunks*Cout*4 |
+// mean | rstd | scale | shift] (Cout each); y1.p == NULL: no apply (the caller only needs the statistics).
+extern "C" int stc_conv_bn_fwd(int dtype, int kind, int B, stc_view x, int Cin, const void* w_packed, int Cout,
+                               stc_view y, float* fws, int nchunks, const float* gamma, const float* beta,
+                               float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum,
+                               float eps, stc_view apply_x, stc_view y1, float slope1, stc_view y2, float slope2,
+                               void* workspace, int64_t workspace_bytes, void* stream) {
+  STC_REQUIRE(fws && nchunks > 0 && gamma && beta, "stc_conv_bn_fwd: statistics workspace and BN affine required");
+  int rc = stc_conv_fwd_ex(dtype, kind, B, x, Cin, w_packed, Cout, y, nullptr, 0, 0, fws, nchunks, nullptr, workspace,
+                           workspace_bytes, stream);
+  if (rc) return rc;
+  float* tab = fws + (int64_t)nchunks * Cout * 4;
+  rc = stc_bn_finalize(fws, nchunks, Cout, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
+                       tab, tab + Cout, tab + 2 * Cout, tab + 3 * Cout, stream);
+  if (rc || !y1.p) return rc;
+  return stc_bn_apply(dtype, B, apply_x, Cout, tab + 2 * Cout, tab + 3 * Cout, y1, slope1, y2, slope2, stream);
+}
+
 extern "C" int stc_conv_fwd(int dtype, int kind, int B, stc_view x, int Cin,
                             const float* pro_scale, const float* pro_shift, int pro_act, float pro_slope,
                             const void* w_packed, int Cout, stc_view y,
@@ -905,6 +925,23 @@ extern "C" int stc_conv_bwd_bn(int dtype, int kind, int B, stc_view dy, int Cin,
   STC_REQUIRE(nchunks == need, "stc_conv_bwd_bn: %d chunks != %d (use stc_conv_bwd_bn_chunks_ex)", nchunks, need);
   return stc_bn_bwd_reduce(dtype, B, bnb->x, bnb->C, bnb->scale, bnb->shift, bnb->mean, bnb->rstd, g1, bnb->slope_self,
                            bnb->g_other, bnb->slope_other, part2, need, stream);
+}
+
+// stc_conv_bwd_bn followed by its stc_bn_bwd_apply (the conv output at the BN channels over the BN extent as the
+// first gradient): a BN layer's whole input-gradient step from one host call
+extern "C" int stc_conv_bwd_bn_apply(int dtype, int kind, int B, stc_view dy, int Cin, const void* w_packed, int Cout,
+                                     stc_view out, const stc_bnb_fuse* bnb, float* part2, int nchunks,
+                                     const float* gamma, stc_view dx, float* dgamma, float* dbeta, void* workspace,
+                                     int64_t workspace_bytes, void* stream) {
+  int rc = stc_conv_bwd_bn(dtype, kind, B, dy, Cin, w_packed, Cout, out, bnb, part2, nchunks, workspace,
+                           workspace_bytes, stream);
+  if (rc) return rc;
+  stc_view g1 = out;
+  g1.co += bnb->ch_off;
+  g1.H = bnb->x.H;
+  g1.W = bnb->x.W;
+  return stc_bn_bwd_apply(dtype, B, bnb->x, bnb->C, bnb->scale, bnb->shift, bnb->mean, bnb->rstd, gamma, g1,
+                          bnb->slope_self, bnb->g_other, bnb->slope_other, part2, nchunks, dx, dgamma, dbeta, stream);
 }
 
 // ---- input-gradient conv + activation backward (layers without BatchNorm)

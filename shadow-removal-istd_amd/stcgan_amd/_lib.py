@@ -59,6 +59,10 @@ _SIGS = {
                                _i64, _vp]),
     "stc_conv_fwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View]),
     "stc_conv_fwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _f32, View, _f32, _vp, _vp, _i64, _vp]),
+    "stc_conv_bwd_bn_apply": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _vp, _i32, _vp, View, _vp,
+                                     _vp, _vp, _i64, _vp]),
+    "stc_conv_bn_fwd": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _f32,
+                               _f32, View, View, _f32, View, _f32, _vp, _i64, _vp]),
     "stc_conv_bwd_act_ok": (_i32, [_i32, _i32, _i32, View, _i32, _i32, View, View, View]),
     "stc_conv_bwd_act": (_i32, [_i32, _i32, _i32, View, _i32, _vp, _i32, View, View, _f32, View, _f32, _vp]),
     "stc_set_splitk_inlaunch": (_i32, [_i32]),
@@ -112,6 +116,7 @@ _SIGS = {
     "stc_warp_affine": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "stc_resize_area": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "stc_time_next_main_kernel": (_i32, [_vp, _vp]),
+    "stc_stream_wait": (_i32, [_vp, _vp]),
     "stc_last_error": (ctypes.c_char_p, []),
     "stc_version": (_i32, []),
 }

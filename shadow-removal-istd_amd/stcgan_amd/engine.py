@@ -69,6 +69,10 @@ SIDE_IN_CAPTURE = False
 
 _set_stream = torch._C._cuda_setStream
 
+
+def _stream_wait(waiter_h, src_h):
+    return L.lib().stc_stream_wait(waiter_h, src_h)
+
 # Events recorded or waited on while a HIP graph is being captured, kept alive until the capture has ended
 # (STCGAN.capture sets a list here and drops it after capture_end).  torch's Stream.wait_stream and a fork's local
 # event are otherwise destroyed inside the open capture, while capture edges still refer to them: the first suspect
@@ -84,11 +88,9 @@ def hold(ev):
 
 
 def wait_stream(waiter, src):
-    """waiter.wait_stream(src) whose event outlives an open capture."""
-    ev = torch.cuda.Event()
-    ev.record(src)
-    waiter.wait_event(ev)
-    hold(ev)
+    """waiter.wait_stream(src), through one library call (stc_stream_wait: a pooled event that outlives an open
+    capture)."""
+    L.check(L.lib().stc_stream_wait(waiter.cuda_stream, src.cuda_stream), "stc_stream_wait")
 
 
 class _WgradLane:
@@ -102,24 +104,24 @@ class _WgradLane:
         if self.cur is not None:
             ent = _WG_SIDE.get(self.cur.cuda_stream)
             if ent is None:
-                ent = _WG_SIDE[self.cur.cuda_stream] = (torch.cuda.Stream(self.cur.device), torch.cuda.Event())
-            self.side, self._ev = ent
+                side = torch.cuda.Stream(self.cur.device)
+                ent = _WG_SIDE[self.cur.cuda_stream] = (side, side.cuda_stream, self.cur.cuda_stream)
+            self.side, self._side_h, self._cur_h = ent
 
     def run(self, fn, *reads, pixels=0):
         """fn() on the side stream, after everything queued so far on the calling stream; ``reads``: the
         calling stream's tensors fn reads that may be freed before the backward ends.  Only layers of at
         most WGRAD_OVERLAP_MAX_PIX output pixels per image go to the side (the big ones fill the GPU alone;
-        overlapping them measured slower).  (The fork is one reused event and a direct current-stream switch:
-        ``Stream.wait_stream`` creates an event per call and ``torch.cuda.stream()`` queries the current stream
-        twice -- together ~15 us of host time per call, 50 calls per step.)"""
+        overlapping them measured slower).  (The fork is one library call on raw stream handles (stc_stream_wait, a
+        pooled event) and a direct current-stream switch: ``Stream.wait_stream`` creates an event per call and
+        ``torch.cuda.stream()`` queries the current stream twice -- together ~15 us of host time per call, 50 calls
+        per step.)"""
         if self.side is None or pixels > WGRAD_OVERLAP_MAX_PIX:
             self.last_side = False
             return fn()
         self.last_side = True
         side, cur = self.side, self.cur
-        ev = self._ev if not SIDE_IN_CAPTURE else hold(torch.cuda.Event())  # (capture probe: a fresh event per fork)
-        ev.record(cur)
-        side.wait_event(ev)
+        L.check(_stream_wait(self._side_h, self._cur_h), "stc_stream_wait")
         for t in reads:
             t.record_stream(side)
         _set_stream(side.stream_id, side.device_index, side.device_type)
@@ -130,7 +132,7 @@ class _WgradLane:
 
     def join(self):
         if self.side is not None:
-            wait_stream(self.cur, self.side)
+            L.check(_stream_wait(self._cur_h, self._side_h), "stc_stream_wait")
 
 
 class GradWriter:
@@ -259,6 +261,17 @@ def _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev):
     return t, st
 
 
+def _conv_bn_act(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev, apply_x, y1, s1, y2=None, s2=0.0):
+    """Conv -> BatchNorm2d -> activation pass of ``apply_x`` into y1 [and y2] (y1 None: none); returns _conv_bn's
+    (table, (mean, rstd) or None).  Train mode: one library call (ops.conv_bn_act)."""
+    if train:
+        return ops.conv_bn_act(kind, B, xv, cin, w, cout, yv, dt, bn, apply_x, y1, s1, y2, s2)
+    t, st = _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev)
+    if y1 is not None:
+        ops.bn_apply(B, apply_x, cout, dt, (t[0], t[1]), y1, s1, y2, s2)
+    return t, st
+
+
 # ----------------------------------------------------------------------------- generator
 
 
@@ -283,9 +296,9 @@ def gen_forward(plan, sources, train, dt, cache, save):
     rq = [None] + [_nhwc(B, *_pad2(S, k), co[k - 1], dt, dev) for k in range(1, Lv)]
     tab_d, tab_u, st_d, st_u = {}, {}, {}, {}
 
-    def conv_bn(kind, xv, cin_, w, cout, yv, bn):
-        """conv -> BatchNorm table (batch statistics fused into the conv in train mode)."""
-        return _conv_bn(kind, B, xv, cin_, w, cout, yv, dt, bn, train, dev)
+    def conv_bn_act(kind, xv, cin_, w, cout, yv, bn, apply_x, y1, s1, y2=None, s2=0.0):
+        """conv -> BatchNorm (batch statistics fused into the conv in train mode) -> activation pass."""
+        return _conv_bn_act(kind, B, xv, cin_, w, cout, yv, dt, bn, train, dev, apply_x, y1, s1, y2, s2)
 
     # ---- down path
     w0 = ops.packed(cache, plan.conv[0].weight, L.PACK_CONV_FWD, co[0], cin_pad, dt)
@@ -301,10 +314,9 @@ def gen_forward(plan, sources, train, dt, cache, save):
     for k in range(1, Lv):
         wk = ops.packed(cache, plan.conv[k].weight, L.PACK_CONV_FWD, co[k], co[k - 1], dt)
         if k <= Lv - 2:
-            tab_d[k], st_d[k] = conv_bn(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k],
-                                        L.nhwc_view(rd[k]), plan.bnd[k])
-            ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, (tab_d[k][0], tab_d[k][1]), L.nhwc_view(ad[k]),
-                         LRELU, L.nhwc_view(cr[k], 0), 0.0)
+            rv = L.nhwc_view(rd[k])
+            tab_d[k], st_d[k] = conv_bn_act(L.CONV_S2, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], rv, plan.bnd[k],
+                                            rv, L.nhwc_view(ad[k]), LRELU, L.nhwc_view(cr[k], 0), 0.0)
         else:  # innermost: no down-norm (STCGAN/networks.py:118-124)
             ops.conv(L.CONV_S2, B, L.nhwc_view(ad[k - 1]), co[k - 1], wk, co[k], L.nhwc_view(rd[k]), dt)
             ops.bn_apply(B, L.nhwc_view(rd[k]), co[k], dt, None, L.nhwc_view(cr[k]), 0.0)
@@ -312,10 +324,9 @@ def gen_forward(plan, sources, train, dt, cache, save):
     for k in range(Lv - 1, 0, -1):
         wt = ops.packed(cache, plan.convT[k].weight, L.PACK_CONVT_FWD, co[k - 1], cin_t(k), dt)
         # statistics over the full ConvT extent (before the crop of an odd level)
-        tab_u[k], st_u[k] = conv_bn(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
-                                    plan.bnu[k])
-        ops.bn_apply(B, L.nhwc_view(rq[k], 0, *S[k]), co[k - 1], dt, (tab_u[k][0], tab_u[k][1]),
-                     L.nhwc_view(cr[k - 1], co[k - 1]), 0.0)
+        tab_u[k], st_u[k] = conv_bn_act(L.CONVT_S2, L.nhwc_view(cr[k]), cin_t(k), wt, co[k - 1], L.nhwc_view(rq[k]),
+                                        plan.bnu[k], L.nhwc_view(rq[k], 0, *S[k]), L.nhwc_view(cr[k - 1], co[k - 1]),
+                                        0.0)
     # ---- outermost: tanh(convT_0(cr[0]) + bias) -> NCHW fp32
     Ho, Wo = 2 * S[1][0], 2 * S[1][1]
     y = torch.empty((B, plan.out_c, Ho, Wo), dtype=torch.float32, device=dev)
@@ -534,11 +545,11 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None, stats_only=
         if i >= 1:  # conv -> BatchNorm -> LeakyReLU (networks.py:167-180); no conv bias there
             assert cv.bias is None
             o = _nhwc(B, h, w, cout, dt, dev)
-            t, st = _conv_bn(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(o), dt,
-                             plan.bns[i - 1], train, dev)
+            ov = L.nhwc_view(o)
+            # (stats_only: only the logits layer reads the last activation -- no pass)
+            t, st = _conv_bn_act(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, ov, dt, plan.bns[i - 1], train,
+                                 dev, ov, None if (stats_only and i == n - 2) else L.nhwc_view(a), LRELU)
             tab = (t[0], t[1])
-            if not (stats_only and i == n - 2):  # (stats_only: only the logits layer reads this activation)
-                ops.bn_apply(B, L.nhwc_view(o), cout, dt, tab, L.nhwc_view(a), LRELU)
         elif ops.conv_act(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(a), LRELU, dt, bias=cv.bias):
             o = a  # no raw output: the backward's LeakyReLU test sees the same signs in the activation
         else:

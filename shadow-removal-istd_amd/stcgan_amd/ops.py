@@ -239,6 +239,35 @@ def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
     return part, nch
 
 
+def conv_bn_act(kind, B, xv, cin, w_packed, cout, yv, dt, bn, apply_x, y1, s1, y2=None, s2=0.0):
+    """A BatchNorm layer's train-mode forward: conv into ``yv`` with the batch statistics, the BN finalize (running
+    statistics updated) and the activation pass of ``apply_x`` into y1 [and y2] (y1 None: no pass) -- one library call
+    (stc_conv_bn_fwd; the instrumented / forced-plan runs take the three separate calls).  Returns ((2, cout) scale /
+    shift table, (mean, rstd)), views of one fp32 buffer."""
+    dev = w_packed.device
+    gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
+    if _timer is not None or (FORCE_CONV and (kind, B, gh, gw, cin, cout) in FORCE_CONV):
+        t = torch.empty((2, cout), dtype=torch.float32, device=dev)
+        part, nch = conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt)
+        st = bn_finalize_part(part, nch, cout, bn, t[0], t[1])
+        if y1 is not None:
+            bn_apply(B, apply_x, cout, dt, (t[0], t[1]), y1, s1, y2, s2)
+        return t, st
+    nbytes, nch, _ = conv_query(kind, B, gh, gw, cin, cout, dt)
+    ws, nb = _ws(nbytes, dev)
+    P = nch * cout * 4
+    fws = torch.empty(P + 4 * cout, dtype=torch.float32, device=dev)
+    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+    check(lib().stc_conv_bn_fwd(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ptr(fws), nch,
+                                ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
+                                ptr(bn.num_batches_tracked), float(mom), float(bn.eps),
+                                apply_x if y1 is not None else L.NULL_VIEW, y1 if y1 is not None else L.NULL_VIEW,
+                                float(s1), y2 if y2 is not None else L.NULL_VIEW, float(s2), ptr(ws), nb, stream()),
+          "stc_conv_bn_fwd")
+    tab = fws[P:]
+    return tab[2 * cout:].view(2, cout), (tab[:cout], tab[cout:2 * cout])
+
+
 # bf16 LDS-DMA tile configurations (csrc/igemm_bf16.hip kTiles): cfg -> (BM, BN, WM, WN, stages, BK[, loader waves])
 _BF16_TILES = [(128, 128, 2, 2, 2, 64), (256, 128, 2, 2, 2, 64), (128, 64, 2, 2, 2, 64), (256, 64, 4, 1, 2, 64),
                (64, 128, 1, 4, 2, 64), (64, 64, 2, 2, 2, 64), (256, 256, 2, 4, 2, 64), (128, 256, 2, 4, 2, 64),
@@ -327,17 +356,19 @@ def conv_bn_backward(kind, B, xv, cin, w_packed, cout, yv, dt, bn_x, C, bn_state
         check(0 if nch > 0 else -1, "stc_conv_bwd_bn_chunks_ex")
     part = torch.empty((nch, C, 2), dtype=torch.float32, device=dev)
     timer = _timer
-    if timer is not None:
-        e0, e1 = _main_events()
     dgamma = _out1(dgamma, C, dev)
     dbeta = _out1(dbeta, C, dev)
+    if timer is None:  # (both launches from one call)
+        check(l.stc_conv_bwd_bn_apply(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse),
+                                      ptr(part), nch, ptr(gamma), dxv, ptr(dgamma), ptr(dbeta), ptr(ws), nb, stream()),
+              "stc_conv_bwd_bn_apply")
+        return dgamma, dbeta
+    e0, e1 = _main_events()
     rc = l.stc_conv_bwd_bn(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ctypes.byref(fuse),
                            ptr(part), nch, ptr(ws), nb, stream())
-    if timer is not None:
-        _disarm()
+    _disarm()
     check(rc, "stc_conv_bwd_bn")
-    if timer is not None:
-        _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=yv.cs == 1)
+    _time_entry(timer, kind, B, gh, gw, cin, cout, dt, e0, e1, bnb=yv.cs == 1)
     # apply: g1 = the conv output at the BN channels over the BN extent
     g1 = L.View(yv.p, bn_x.H, bn_x.W, yv.bs, yv.rs, yv.ps, yv.co + ch_off, yv.cs, 0)
     g1._keep = yv
