@@ -94,14 +94,13 @@ struct ChanTab {
   long long bs[16];    // image stride of channel c's source
   int n;               // real channels (the rest of Cpad is zero)
 };
-template <typename T>
+template <typename T, typename I>  // I: the quad index type (int when B * HW / 4 < 2^31: no 64-bit division)
 __global__ void __launch_bounds__(256) gather4_kernel(int B, int HW, int W, ChanTab t, View d, int Cpad) {
   constexpr int N = 16 / sizeof(T);
-  const long long quads = (long long)B * (HW >> 2);
-  for (long long qd = (long long)blockIdx.x * blockDim.x + threadIdx.x; qd < quads;
-       qd += (long long)gridDim.x * blockDim.x) {
-    const int b = (int)(qd / (HW >> 2));
-    const int hw = (int)(qd - (long long)b * (HW >> 2)) << 2;
+  const I quads = (I)B * (I)(HW >> 2);
+  for (I qd = (I)blockIdx.x * blockDim.x + threadIdx.x; qd < quads; qd += (I)gridDim.x * blockDim.x) {
+    const int b = (int)(qd / (I)(HW >> 2));
+    const int hw = (int)(qd - (I)b * (HW >> 2)) << 2;
     float4 v[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -176,6 +175,61 @@ __global__ void tanh_bwd_kernel(int B, int C, int H, int W, const float* y, cons
         acc[c] += v;
       }
       st1<T>(out + (long long)c * dq.cs, v);
+    }
+  }
+  __shared__ float red[4][256];
+  for (int c = 0; c < 4; ++c) red[c][threadIdx.x] = acc[c];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s)
+      for (int c = 0; c < 4; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x < C) part[(long long)blockIdx.x * C + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// The same with 4 consecutive pixels per thread (W % 4 == 0, 16-byte NHWC dq pixels, 32-bit indices): float4 loads of
+// y / gy per channel plane and one 16-byte store per pixel instead of Cpad element stores; chunks of whole quads.
+// part is summed per thread in pixel order, then over the block in a fixed tree order (deterministic).
+template <typename T>
+__global__ void __launch_bounds__(256) tanh_bwd4_kernel(int B, int C, int HW, int W, const float* y, const float* gy,
+                                                        View dq, int per4, float* part) {
+  const int P = B * HW;
+  const int p0 = blockIdx.x * per4, p1 = min(P, p0 + per4);
+  float acc[4] = {0, 0, 0, 0};
+  for (int q = p0 + 4 * (int)threadIdx.x; q < p1; q += 4 * (int)blockDim.x) {
+    const int b = q / HW, hw = q - b * HW;
+    const int yy = hw / W, xx = hw - yy * W;
+    float v[4][4];  // [channel][pixel]
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[c][i] = 0.f;
+      if (c < C) {
+        const int o = (b * C + c) * HW + hw;
+        const float4 t = *reinterpret_cast<const float4*>(y + o);
+        const float4 g = *reinterpret_cast<const float4*>(gy + o);
+        v[c][0] = g.x * (1.f - t.x * t.x);
+        v[c][1] = g.y * (1.f - t.y * t.y);
+        v[c][2] = g.z * (1.f - t.z * t.z);
+        v[c][3] = g.w * (1.f - t.w * t.w);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[c] += v[c][i];
+      }
+    }
+    T* out = reinterpret_cast<T*>(dq.p) + vidx(dq, b, yy, xx, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float4*>(out + (long long)i * dq.ps) = make_float4(v[0][i], v[1][i], v[2][i], v[3][i]);
+      } else {
+        uint4 w;
+        w.x = pack_bf16x2(v[0][i], v[1][i]);
+        w.y = pack_bf16x2(v[2][i], v[3][i]);
+        w.z = 0u;
+        w.w = 0u;
+        *reinterpret_cast<uint4*>(out + (long long)i * dq.ps) = w;
+      }
     }
   }
   __shared__ float red[4][256];
@@ -326,8 +380,13 @@ extern "C" int stc_gather_nchw(int dtype, int B, int H, int W, int nsrc, const f
         for (int j = 0; j < src_c[k]; ++j, ++c) { t.p[c] = src[k] + j * HW; t.bs[c] = src_c[k] * HW; }
       t.n = tot;
       const int blocks = (int)std::max<long long>(1, std::min<long long>((P / 4 + 255) / 256, 4096));
-      if (dtype == STC_F32) hipLaunchKernelGGL(gather4_kernel<float>, dim3(blocks), dim3(256), 0, st, B, (int)HW, W, t, d, Cpad);
-      else hipLaunchKernelGGL(gather4_kernel<bf16>, dim3(blocks), dim3(256), 0, st, B, (int)HW, W, t, d, Cpad);
+      if (P / 4 < (1ll << 31)) {
+        if (dtype == STC_F32) hipLaunchKernelGGL((gather4_kernel<float, int>), dim3(blocks), dim3(256), 0, st, B, (int)HW, W, t, d, Cpad);
+        else hipLaunchKernelGGL((gather4_kernel<bf16, int>), dim3(blocks), dim3(256), 0, st, B, (int)HW, W, t, d, Cpad);
+      } else {
+        if (dtype == STC_F32) hipLaunchKernelGGL((gather4_kernel<float, long long>), dim3(blocks), dim3(256), 0, st, B, (int)HW, W, t, d, Cpad);
+        else hipLaunchKernelGGL((gather4_kernel<bf16, long long>), dim3(blocks), dim3(256), 0, st, B, (int)HW, W, t, d, Cpad);
+      }
       STC_CHECK_LAUNCH();
       return 0;
     }
@@ -362,7 +421,17 @@ extern "C" int stc_tanh_bias_bwd(int dtype, int B, int C, int H, int W, const fl
   hipStream_t st = (hipStream_t)stream;
   const int Cpad = dtype == STC_F32 ? 4 : 8;
   View d = mkview(dq);
-  if (dtype == STC_F32)
+  const long long P = (long long)B * H * W;
+  const bool quad = W % 4 == 0 && P * 4 < (1ll << 31) && dq.cs == 1 && dq.co == 0 && dq.ps == Cpad &&
+                    dq.rs % Cpad == 0 && dq.bs % Cpad == 0 && ((uintptr_t)dq.p & 15) == 0 &&
+                    ((uintptr_t)y & 15) == 0 && ((uintptr_t)gy & 15) == 0;
+  if (quad) {
+    const int per4 = (int)((((P + nchunks - 1) / nchunks) + 3) & ~3ll);
+    if (dtype == STC_F32)
+      hipLaunchKernelGGL(tanh_bwd4_kernel<float>, dim3(nchunks), dim3(256), 0, st, B, C, H * W, W, y, gy, d, per4, part);
+    else
+      hipLaunchKernelGGL(tanh_bwd4_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, B, C, H * W, W, y, gy, d, per4, part);
+  } else if (dtype == STC_F32)
     hipLaunchKernelGGL(tanh_bwd_kernel<float>, dim3(nchunks), dim3(256), 0, st, B, C, H, W, y, gy, d, Cpad, part, nchunks);
   else
     hipLaunchKernelGGL(tanh_bwd_kernel<bf16>, dim3(nchunks), dim3(256), 0, st, B, C, H, W, y, gy, d, Cpad, part, nchunks);

@@ -347,6 +347,27 @@ def test_tanh_bias_bwd_and_chan_sum():
     close(s, ref.sum(dim=(0, 2, 3)), tol=1e-6, what="chan_sum")
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("B,C,H,W", [(32, 3, 256, 256), (32, 1, 256, 256), (3, 3, 10, 12), (2, 1, 6, 10)],
+                         ids=["c3_256", "c1_256", "quad_small", "scalar_w10"])
+def test_tanh_bias_bwd_paths(dt, B, C, H, W):
+    """The output layer's tanh + bias backward (4 pixels per thread where W % 4 == 0, else per pixel): dq to the
+    per-element formula within fp32 rounding (bf16: the output cast), padding channels zero, dbias within fp32
+    reordering of the per-channel sum."""
+    g = torch.Generator().manual_seed(B * 7 + C)
+    y = torch.tanh(torch.randn(B, C, H, W, generator=g)).to(DEV)
+    gy = torch.randn(B, C, H, W, generator=g).to(DEV)
+    cpad = 4 if dt == torch.float32 else 8
+    dq = torch.full((B, H, W, cpad), float("nan"), device=DEV, dtype=dt)
+    db = ops.tanh_bias_bwd(y, gy, L.nhwc_view(dq), dt)
+    ref = gy * (1 - y * y)
+    err = float((nchw(dq)[:, :C].float() - ref).abs().max())
+    assert err <= (2e-6 if dt == torch.float32 else 8e-3) * float(ref.abs().max()), err  # (bf16: the output cast)
+    assert float(dq[..., C:].float().abs().max()) == 0.0
+    rs = ref.double().sum(dim=(0, 2, 3))
+    assert float((db.double() - rs).abs().max()) <= 1e-5 * float(ref.abs().sum(dim=(0, 2, 3)).max())
+
+
 @pytest.mark.parametrize("n", [1, 1000, 393216])
 def test_losses(n):
     from stcgan_amd import loss as sl
