@@ -37,6 +37,8 @@ a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2
                           streams=bool(args.streams), fused_objectives=bool(args.fused))
 torch.manual_seed(1234)
 tr = STCGAN(a)
+import stcgan_amd.stcgan as _st  # noqa: E402
+tr.set_early = lambda v: setattr(_st, "EARLY_REAL_BACKWARD", bool(v))  # (--ab-attr early=0,1)
 if args.host_sleep_us:
     _ts = tr.train_step
 

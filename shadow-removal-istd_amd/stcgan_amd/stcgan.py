@@ -18,6 +18,7 @@ loader passed, the reference's two ISTD loaders (STCGAN/stcgan.py:73-104) are bu
 on data.ISTDLoader (decode on the host, Resize / RandomScale / RandomRotate / flip /
 crop on the device), each rank taking its shard of the global ``args.batch_size``.
 """
+import contextlib
 import datetime
 import logging
 import os
@@ -30,7 +31,7 @@ import torch.nn as nn
 from . import engine
 from . import networks
 from . import parallel
-from .loss import AdversarialLoss, DataLoss, d_objective, g_objective
+from .loss import AdversarialLoss, DataLoss, d_objective, d_real_grad, g_objective
 from .optim import Adam
 
 
@@ -81,6 +82,10 @@ def accumulate(acc, vals, d_out, weight=1.0):
     for k, c in zip(("D1_real", "D1_fake", "D2_real", "D2_fake"), d_out):
         acc[k] = acc[k] + c.mean().double() * weight
 
+
+# loss type "normal": run the discriminators' real-input backward right after their forward (STCGAN._real_backward);
+# False (A/B, tests): one D-objective backward after the fake forwards, as the reference
+EARLY_REAL_BACKWARD = True
 
 class STCGAN(object):
 
@@ -294,6 +299,19 @@ class STCGAN(object):
         out.record_stream(torch.cuda.current_stream(self.device))
         return out
 
+    def _real_backward(self, lane, C_real, lam, weight):
+        """Back-propagate the D objective's real term of one discriminator from its logits (on its lane)."""
+        with (torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext()):
+            if weight == 1.0:  # (the objective's incoming gradient: one fp32 1, made once per stream that reads it)
+                key = lane.cuda_stream if lane is not None else None
+                gout = self._gout_one.get(key) if hasattr(self, "_gout_one") else None
+                if gout is None:
+                    gout = torch.ones((), dtype=torch.float32, device=self.device)
+                    self.__dict__.setdefault("_gout_one", {})[key] = gout
+            else:  # (weighted_loss: loss * weight, whose backward hands the objective fp32(weight))
+                gout = torch.full((), weight, dtype=torch.float32, device=self.device)
+            torch.autograd.backward(C_real, d_real_grad(self.adv_loss, C_real, lam, gout))
+
     def train_step(self, x, m, y, training=True, acc=None, inputs_ready=None, weight=1.0):
         """One iteration of STCGAN.run_epoch (STCGAN/stcgan.py:208-312): D step then G step.
         Returns the on-device loss scalars (no host sync).  The call order of every network
@@ -345,8 +363,20 @@ class STCGAN(object):
             self.optim_D.zero_grad()
             self.D1.requires_grad_(True)
             self.D2.requires_grad_(True)
+            # loss type "normal": each real-input call's backward runs right after its forward (its gradient from
+            # the objective does not involve the fake logits, loss.d_real_grad) -- off the D step's critical path,
+            # overlapping the generators' forwards (and, carried over on the lanes, the previous step's G update);
+            # the objective below then takes the real logits detached.  The D gradients' real + fake sum is the
+            # same fp32 addition in the other order: bit-identical.
+            early = training and EARLY_REAL_BACKWARD and self.d_loss_type == "normal" and self.fused_objectives
+            if early:
+                self._exchange(("D1", "D2"), 2)  # real + fake calls
             C1_real = self._on(l1, self.D1, [x, m])
+            if early:
+                self._real_backward(l1, C1_real, self.lambda2, weight)
             C2_real = self._on(l2, self.D2, [x, m, y])
+            if early:
+                self._real_backward(l2, C2_real, self.lambda3, weight)
             m_pred = self.G1(x)
             ev_m = engine.hold(main.record_event()) if l1 is not None else None
             C1_fake = self._on(l1, self.D1, [x, m_pred.detach()], after=ev_m)
@@ -357,13 +387,15 @@ class STCGAN(object):
                 engine.wait_stream(main, l1)
                 engine.wait_stream(main, l2)
             if self.d_loss_type == "normal" and self.fused_objectives:  # one node (loss.d_objective)
-                D_loss, D1_loss, D2_loss = d_objective(self.adv_loss, C1_fake, C1_real, C2_fake, C2_real,
+                D_loss, D1_loss, D2_loss = d_objective(self.adv_loss, C1_fake, C1_real.detach() if early else C1_real,
+                                                       C2_fake, C2_real.detach() if early else C2_real,
                                                        self.lambda2, self.lambda3)
             else:
                 D1_loss, D2_loss = self._d_losses(C1_real, C1_fake, C2_real, C2_fake)
                 D_loss = self.lambda2 * D1_loss + self.lambda3 * D2_loss
             if training:
-                self._exchange(("D1", "D2"), 2)  # real + fake calls
+                if not early:
+                    self._exchange(("D1", "D2"), 2)  # real + fake calls
                 weighted_loss(D_loss, weight).backward()
                 self._finish_exchange(("D2", "D1"))
                 self.optim_D.step()

@@ -67,3 +67,22 @@ def test_run_epoch_input_stream_bit_identical():
     for n in NETS:
         for k, v in ref_state[n].items():
             assert torch.equal(state[n][k], v), (n, k)
+
+
+@pytest.mark.parametrize("streams", [False, True], ids=["one_stream", "lanes"])
+def test_early_real_backward_bit_identical(streams):
+    """The discriminators' real-input backward run right after their forward (stcgan.EARLY_REAL_BACKWARD, loss type
+    normal) against one D-objective backward after the fake forwards: every parameter, buffer and loss identical."""
+    from stcgan_amd import stcgan as st
+    prev = st.EARLY_REAL_BACKWARD
+    try:
+        st.EARLY_REAL_BACKWARD = False
+        ref_state, ref_losses = _run(streams, streams, streams, "normal")
+        st.EARLY_REAL_BACKWARD = True
+        state, losses = _run(streams, streams, streams, "normal")
+    finally:
+        st.EARLY_REAL_BACKWARD = prev
+    assert losses == ref_losses
+    for n in NETS:
+        for k, v in ref_state[n].items():
+            assert torch.equal(state[n][k], v), (n, k)
