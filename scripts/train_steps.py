@@ -38,7 +38,7 @@ a = types.SimpleNamespace(devices=["cuda:0"], tasks=["train"], lr_G=5e-5, lr_D=2
 torch.manual_seed(1234)
 tr = STCGAN(a)
 import stcgan_amd.stcgan as _st  # noqa: E402
-tr.set_early = lambda v: setattr(_st, "EARLY_REAL_BACKWARD", bool(v))  # (--ab-attr early=0,1)
+tr.set_early = lambda v: setattr(_st, "EARLY_D_BACKWARD", int(v))  # (--ab-attr early=0,1,2)
 if args.host_sleep_us:
     _ts = tr.train_step
 

@@ -110,18 +110,19 @@ def d_objective(adv, C1_fake, C1_real, C2_fake, C2_real, lambda2, lambda3):
     return total, parts[4], parts[5]
 
 
-def d_real_grad(adv, C_real, lam, gout):
-    """d_objective's gradient with respect to one real-input logits tensor, lam * 0.5 * adv'(C_real, real) scaled by
-    the objective's incoming gradient ``gout`` (fp32 device scalar) -- the same per-term kernel arithmetic as that
-    node's backward (stc_loss_multi_bwd), available as soon as C_real is: the real branch's backward need not wait
-    for the fake logits (STCGAN.train_step runs it early; the objective then takes C_real detached)."""
-    real = adv._labels[0]
+def d_term_grad(adv, C, lam, gout, real=True):
+    """d_objective's gradient with respect to one of its four logits tensors, lam * 0.5 * adv'(C, label) (label: real
+    or fake) scaled by the objective's incoming gradient ``gout`` (fp32 device scalar) -- the same per-term kernel
+    arithmetic as that node's backward (stc_loss_multi_bwd), available as soon as C is: with loss type normal each
+    term involves one logits tensor only, so each discriminator call's backward need not wait for the other calls
+    (STCGAN.train_step runs them early; the objective then takes the logits detached)."""
+    label = adv._labels[0] if real else adv._labels[1]
     k = L.LOSS_BCE_CONST if adv.ls else L.LOSS_MSE_CONST
-    p_ = C_real.contiguous()
+    p_ = C.contiguous()
     if p_.dtype != torch.float32 or not p_.is_cuda:
         raise TypeError("stcgan_amd losses take fp32 CUDA inputs")
     g = torch.empty_like(p_)
-    check(lib().stc_loss_multi_bwd(1, _arr(ctypes.c_int32, [k]), _arr(ctypes.c_float, [real]),
+    check(lib().stc_loss_multi_bwd(1, _arr(ctypes.c_int32, [k]), _arr(ctypes.c_float, [label]),
                                    _arr(ctypes.c_void_p, [p_.data_ptr()]), _arr(ctypes.c_void_p, [None]),
                                    _arr(ctypes.c_int64, [p_.numel()]), _arr(ctypes.c_float, [lam]),
                                    _arr(ctypes.c_float, [0.5]), ptr(gout), _arr(ctypes.c_void_p, [g.data_ptr()]),

@@ -31,7 +31,7 @@ import torch.nn as nn
 from . import engine
 from . import networks
 from . import parallel
-from .loss import AdversarialLoss, DataLoss, d_objective, d_real_grad, g_objective
+from .loss import AdversarialLoss, DataLoss, d_objective, d_term_grad, g_objective
 from .optim import Adam
 
 
@@ -83,9 +83,10 @@ def accumulate(acc, vals, d_out, weight=1.0):
         acc[k] = acc[k] + c.mean().double() * weight
 
 
-# loss type "normal": run the discriminators' real-input backward right after their forward (STCGAN._real_backward);
-# False (A/B, tests): one D-objective backward after the fake forwards, as the reference
-EARLY_REAL_BACKWARD = True
+# loss type "normal": each discriminator call's D-step backward right after its forward (STCGAN._term_backward):
+# 1 = the real-input calls', 2 = every call's; 0 (A/B, tests): one D-objective backward after the fake forwards, as
+# the reference does
+EARLY_D_BACKWARD = 2
 
 class STCGAN(object):
 
@@ -299,8 +300,8 @@ class STCGAN(object):
         out.record_stream(torch.cuda.current_stream(self.device))
         return out
 
-    def _real_backward(self, lane, C_real, lam, weight):
-        """Back-propagate the D objective's real term of one discriminator from its logits (on its lane)."""
+    def _term_backward(self, lane, C, lam, weight, real):
+        """Back-propagate one term of the D objective (loss type normal) from its logits (on its lane)."""
         with (torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext()):
             if weight == 1.0:  # (the objective's incoming gradient: one fp32 1, made once per stream that reads it)
                 key = lane.cuda_stream if lane is not None else None
@@ -310,7 +311,7 @@ class STCGAN(object):
                     self.__dict__.setdefault("_gout_one", {})[key] = gout
             else:  # (weighted_loss: loss * weight, whose backward hands the objective fp32(weight))
                 gout = torch.full((), weight, dtype=torch.float32, device=self.device)
-            torch.autograd.backward(C_real, d_real_grad(self.adv_loss, C_real, lam, gout))
+            torch.autograd.backward(C, d_term_grad(self.adv_loss, C, lam, gout, real))
 
     def train_step(self, x, m, y, training=True, acc=None, inputs_ready=None, weight=1.0):
         """One iteration of STCGAN.run_epoch (STCGAN/stcgan.py:208-312): D step then G step.
@@ -363,32 +364,39 @@ class STCGAN(object):
             self.optim_D.zero_grad()
             self.D1.requires_grad_(True)
             self.D2.requires_grad_(True)
-            # loss type "normal": each real-input call's backward runs right after its forward (its gradient from
-            # the objective does not involve the fake logits, loss.d_real_grad) -- off the D step's critical path,
-            # overlapping the generators' forwards (and, carried over on the lanes, the previous step's G update);
-            # the objective below then takes the real logits detached.  The D gradients' real + fake sum is the
-            # same fp32 addition in the other order: bit-identical.
-            early = training and EARLY_REAL_BACKWARD and self.d_loss_type == "normal" and self.fused_objectives
+            # loss type "normal": each discriminator call's backward runs right after its forward (each term of the
+            # objective involves one logits tensor, loss.d_term_grad) -- the real-input ones off the D step's
+            # critical path, overlapping the generators' forwards (and, carried over on the lanes, the previous
+            # step's G update), D1's fake-input one overlapping G2's forward; the objective below then takes the
+            # logits detached.  The D gradients' real + fake sum is the same fp32 addition: bit-identical.
+            early = training and EARLY_D_BACKWARD and self.d_loss_type == "normal" and self.fused_objectives
             if early:
                 self._exchange(("D1", "D2"), 2)  # real + fake calls
             C1_real = self._on(l1, self.D1, [x, m])
             if early:
-                self._real_backward(l1, C1_real, self.lambda2, weight)
+                self._term_backward(l1, C1_real, self.lambda2, weight, True)
             C2_real = self._on(l2, self.D2, [x, m, y])
             if early:
-                self._real_backward(l2, C2_real, self.lambda3, weight)
+                self._term_backward(l2, C2_real, self.lambda3, weight, True)
             m_pred = self.G1(x)
             ev_m = engine.hold(main.record_event()) if l1 is not None else None
             C1_fake = self._on(l1, self.D1, [x, m_pred.detach()], after=ev_m)
             y_pred = self.G2([x, m_pred])
             ev_y = engine.hold(main.record_event()) if l1 is not None else None
+            if early and EARLY_D_BACKWARD > 1:
+                self._term_backward(l1, C1_fake, self.lambda2, weight, False)
             C2_fake = self._on(l2, self.D2, [x, m_pred.detach(), y_pred.detach()], after=ev_y)
+            if early and EARLY_D_BACKWARD > 1:
+                self._term_backward(l2, C2_fake, self.lambda3, weight, False)
             if l1 is not None:
                 engine.wait_stream(main, l1)
                 engine.wait_stream(main, l2)
             if self.d_loss_type == "normal" and self.fused_objectives:  # one node (loss.d_objective)
-                D_loss, D1_loss, D2_loss = d_objective(self.adv_loss, C1_fake, C1_real.detach() if early else C1_real,
-                                                       C2_fake, C2_real.detach() if early else C2_real,
+                full = early and EARLY_D_BACKWARD > 1  # (every term back-propagated above: values only here)
+                D_loss, D1_loss, D2_loss = d_objective(self.adv_loss, C1_fake.detach() if full else C1_fake,
+                                                       C1_real.detach() if early else C1_real,
+                                                       C2_fake.detach() if full else C2_fake,
+                                                       C2_real.detach() if early else C2_real,
                                                        self.lambda2, self.lambda3)
             else:
                 D1_loss, D2_loss = self._d_losses(C1_real, C1_fake, C2_real, C2_fake)
@@ -396,7 +404,8 @@ class STCGAN(object):
             if training:
                 if not early:
                     self._exchange(("D1", "D2"), 2)  # real + fake calls
-                weighted_loss(D_loss, weight).backward()
+                if not (early and EARLY_D_BACKWARD > 1):
+                    weighted_loss(D_loss, weight).backward()
                 self._finish_exchange(("D2", "D1"))
                 self.optim_D.step()
             d_out = (C1_real.detach(), C1_fake.detach(), C2_real.detach(), C2_fake.detach())

@@ -69,19 +69,20 @@ def test_run_epoch_input_stream_bit_identical():
             assert torch.equal(state[n][k], v), (n, k)
 
 
+@pytest.mark.parametrize("early", [1, 2], ids=["real_calls", "every_call"])
 @pytest.mark.parametrize("streams", [False, True], ids=["one_stream", "lanes"])
-def test_early_real_backward_bit_identical(streams):
-    """The discriminators' real-input backward run right after their forward (stcgan.EARLY_REAL_BACKWARD, loss type
+def test_early_d_backward_bit_identical(streams, early):
+    """The discriminators' D-step backward run right after each call's forward (stcgan.EARLY_D_BACKWARD, loss type
     normal) against one D-objective backward after the fake forwards: every parameter, buffer and loss identical."""
     from stcgan_amd import stcgan as st
-    prev = st.EARLY_REAL_BACKWARD
+    prev = st.EARLY_D_BACKWARD
     try:
-        st.EARLY_REAL_BACKWARD = False
+        st.EARLY_D_BACKWARD = 0
         ref_state, ref_losses = _run(streams, streams, streams, "normal")
-        st.EARLY_REAL_BACKWARD = True
+        st.EARLY_D_BACKWARD = early
         state, losses = _run(streams, streams, streams, "normal")
     finally:
-        st.EARLY_REAL_BACKWARD = prev
+        st.EARLY_D_BACKWARD = prev
     assert losses == ref_losses
     for n in NETS:
         for k, v in ref_state[n].items():
