@@ -39,6 +39,7 @@ torch.manual_seed(1234)
 tr = STCGAN(a)
 import stcgan_amd.stcgan as _st  # noqa: E402
 tr.set_early = lambda v: setattr(_st, "EARLY_D_BACKWARD", int(v))  # (--ab-attr early=0,1,2)
+tr.set_late = lambda v: setattr(_st, "LATE_STATS_CALLS", bool(v))  # (--ab-attr late=0,1)
 if args.host_sleep_us:
     _ts = tr.train_step
 

@@ -261,11 +261,12 @@ def _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev):
     return t, st
 
 
-def _conv_bn_act(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev, apply_x, y1, s1, y2=None, s2=0.0):
+def _conv_bn_act(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev, apply_x, y1, s1, y2=None, s2=0.0, defer=None):
     """Conv -> BatchNorm2d -> activation pass of ``apply_x`` into y1 [and y2] (y1 None: none); returns _conv_bn's
-    (table, (mean, rstd) or None).  Train mode: one library call (ops.conv_bn_act)."""
+    (table, (mean, rstd) or None).  Train mode: one library call (ops.conv_bn_act); ``defer`` (a list): the running
+    statistics are not updated, the update's inputs are appended (ops.bn_running_update)."""
     if train:
-        return ops.conv_bn_act(kind, B, xv, cin, w, cout, yv, dt, bn, apply_x, y1, s1, y2, s2)
+        return ops.conv_bn_act(kind, B, xv, cin, w, cout, yv, dt, bn, apply_x, y1, s1, y2, s2, defer=defer)
     t, st = _conv_bn(kind, B, xv, cin, w, cout, yv, dt, bn, train, dev)
     if y1 is not None:
         ops.bn_apply(B, apply_x, cout, dt, (t[0], t[1]), y1, s1, y2, s2)
@@ -497,7 +498,7 @@ def _conv_out(h, s):
     return (h + 2 - 4) // s + 1
 
 
-def disc_forward(plan, sources, train, dt, cache, save, inputs=None, stats_only=False):
+def disc_forward(plan, sources, train, dt, cache, save, inputs=None, stats_only=False, defer=None):
     """raw[i] = conv_{i-1} raw output (raw[0] = padded input); act[i] = input of conv_i.
     inputs: optional dict reusing the gathered NHWC input across calls on the same source tensors
     (the trainer's real/fake pairs are fed to each discriminator twice per step, STCGAN/stcgan.py:215-280;
@@ -548,7 +549,7 @@ def disc_forward(plan, sources, train, dt, cache, save, inputs=None, stats_only=
             ov = L.nhwc_view(o)
             # (stats_only: only the logits layer reads the last activation -- no pass)
             t, st = _conv_bn_act(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, ov, dt, plan.bns[i - 1], train,
-                                 dev, ov, None if (stats_only and i == n - 2) else L.nhwc_view(a), LRELU)
+                                 dev, ov, None if (stats_only and i == n - 2) else L.nhwc_view(a), LRELU, defer=defer)
             tab = (t[0], t[1])
         elif ops.conv_act(kind, B, L.nhwc_view(act[i]), chans[i], wp, cout, L.nhwc_view(a), LRELU, dt, bias=cv.bias):
             o = a  # no raw output: the backward's LeakyReLU test sees the same signs in the activation
@@ -679,19 +680,19 @@ class NetFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, ctrl, *tensors):
-        plan, kind, train, dt, cache, nsrc, inputs, _, stats_only = ctrl
+        plan, kind, train, dt, cache, nsrc, inputs, _, stats_only, defer = ctrl
         sources = [t.contiguous().float() for t in tensors[:nsrc]]
         save = train and any(ctx.needs_input_grad[1:])
         ops.refresh_packs(cache)  # all operands packed since the last optimiser step, one launch
         out, saved = (gen_forward(plan, sources, train, dt, cache, save) if kind == "G" else
-                      disc_forward(plan, sources, train, dt, cache, save, inputs, stats_only and not save))
+                      disc_forward(plan, sources, train, dt, cache, save, inputs, stats_only and not save, defer))
         ctx.ctrl = ctrl
         ctx.saved_net = saved
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        plan, kind, train, dt, cache, nsrc, _, consumer, _ = ctx.ctrl
+        plan, kind, train, dt, cache, nsrc, _, consumer, _, _ = ctx.ctrl
         saved = ctx.saved_net
         if saved is None:
             raise RuntimeError("stcgan_amd: backward through a network called in eval mode is not supported")

@@ -68,6 +68,10 @@ class _HipNet(nn.Module):
         # G-step real-input discriminator calls with loss type "normal"): the layers after the last
         # BatchNorm are skipped and the output is left unwritten
         self.stats_only = False
+        # a list (set by the trainer for one call): the call's BatchNorm layers leave their running statistics
+        # alone and append what ops.bn_running_update needs to apply the update later (the trainer orders it after
+        # another call's, as the reference's call order has it)
+        self.defer_running = None
 
     def set_compute_dtype(self, dtype):
         """'fp32' (default, parity path) or 'bf16' (bf16 operands, fp32 accumulation/BN/master weights)."""
@@ -86,7 +90,7 @@ class _HipNet(nn.Module):
             self._plan = self._make_plan()
         params = self._plan.params
         ctrl = (self._plan, self.kind, self.training, self.compute_dtype, self._pack_cache, len(sources),
-                self.input_cache, self.grad_consumer, self.stats_only)
+                self.input_cache, self.grad_consumer, self.stats_only, self.defer_running)
         return engine.NetFn.apply(ctrl, *sources, *params)
 
     def _apply(self, fn, *args, **kwargs):

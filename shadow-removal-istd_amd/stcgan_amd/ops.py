@@ -239,17 +239,21 @@ def conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt, bias=None, force=None):
     return part, nch
 
 
-def conv_bn_act(kind, B, xv, cin, w_packed, cout, yv, dt, bn, apply_x, y1, s1, y2=None, s2=0.0):
+def conv_bn_act(kind, B, xv, cin, w_packed, cout, yv, dt, bn, apply_x, y1, s1, y2=None, s2=0.0, defer=None):
     """A BatchNorm layer's train-mode forward: conv into ``yv`` with the batch statistics, the BN finalize (running
     statistics updated) and the activation pass of ``apply_x`` into y1 [and y2] (y1 None: no pass) -- one library call
     (stc_conv_bn_fwd; the instrumented / forced-plan runs take the three separate calls).  Returns ((2, cout) scale /
-    shift table, (mean, rstd)), views of one fp32 buffer."""
+    shift table, (mean, rstd)), views of one fp32 buffer.  defer (a list): the running statistics are left alone and
+    (partials, chunks, cout, bn) is appended for bn_running_update."""
     dev = w_packed.device
     gh, gw = (xv.H, xv.W) if kind == L.CONVT_S2 else (yv.H, yv.W)
+    upd = defer is None
     if _timer is not None or (FORCE_CONV and (kind, B, gh, gw, cin, cout) in FORCE_CONV):
         t = torch.empty((2, cout), dtype=torch.float32, device=dev)
         part, nch = conv_stats(kind, B, xv, cin, w_packed, cout, yv, dt)
-        st = bn_finalize_part(part, nch, cout, bn, t[0], t[1])
+        st = bn_finalize_part(part, nch, cout, bn, t[0], t[1], update_running=upd)
+        if not upd:
+            defer.append((part, nch, cout, bn))
         if y1 is not None:
             bn_apply(B, apply_x, cout, dt, (t[0], t[1]), y1, s1, y2, s2)
         return t, st
@@ -259,13 +263,28 @@ def conv_bn_act(kind, B, xv, cin, w_packed, cout, yv, dt, bn, apply_x, y1, s1, y
     fws = torch.empty(P + 4 * cout, dtype=torch.float32, device=dev)
     mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
     check(lib().stc_conv_bn_fwd(L.dtype_code(dt), kind, B, xv, cin, ptr(w_packed), cout, yv, ptr(fws), nch,
-                                ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var),
-                                ptr(bn.num_batches_tracked), float(mom), float(bn.eps),
+                                ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean) if upd else None,
+                                ptr(bn.running_var) if upd else None, ptr(bn.num_batches_tracked) if upd else None,
+                                float(mom), float(bn.eps),
                                 apply_x if y1 is not None else L.NULL_VIEW, y1 if y1 is not None else L.NULL_VIEW,
                                 float(s1), y2 if y2 is not None else L.NULL_VIEW, float(s2), ptr(ws), nb, stream()),
           "stc_conv_bn_fwd")
+    if not upd:
+        defer.append((fws, nch, cout, bn))
     tab = fws[P:]
     return tab[2 * cout:].view(2, cout), (tab[:cout], tab[cout:2 * cout])
+
+
+def bn_running_update(part, nch, C, bn):
+    """The running-statistics update a train-mode BatchNorm call left for later (conv_bn_act(defer=...)): the same
+    finalize launch on the same partials (so the same mean / variance, bit for bit) with the running buffers this
+    time, its table output discarded."""
+    dev = part.device
+    scratch = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    mom = bn.momentum if bn.momentum is not None else BN_MOMENTUM
+    check(lib().stc_bn_finalize(ptr(part), nch, C, ptr(bn.weight), ptr(bn.bias), ptr(bn.running_mean),
+                                ptr(bn.running_var), ptr(bn.num_batches_tracked), float(mom), float(bn.eps), None, None,
+                                ptr(scratch), ptr(scratch[C:]), stream()), "stc_bn_finalize")
 
 
 # bf16 LDS-DMA tile configurations (csrc/igemm_bf16.hip kTiles): cfg -> (BM, BN, WM, WN, stages, BK[, loader waves])

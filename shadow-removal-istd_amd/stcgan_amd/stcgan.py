@@ -29,6 +29,7 @@ import torch
 import torch.nn as nn
 
 from . import engine
+from . import ops
 from . import networks
 from . import parallel
 from .loss import AdversarialLoss, DataLoss, d_objective, d_term_grad, g_objective
@@ -83,6 +84,9 @@ def accumulate(acc, vals, d_out, weight=1.0):
         acc[k] = acc[k] + c.mean().double() * weight
 
 
+# loss type "normal": the G step's statistics-only real-input discriminator calls after the fake-input ones (their
+# running-statistics updates applied in the reference's order); False (A/B, tests): before them, as the reference
+LATE_STATS_CALLS = True
 # loss type "normal": each discriminator call's D-step backward right after its forward (STCGAN._term_backward):
 # 1 = the real-input calls', 2 = every call's; 0 (A/B, tests): one D-objective backward after the fake forwards, as
 # the reference does
@@ -421,14 +425,26 @@ class STCGAN(object):
                 # makes them, STCGAN/stcgan.py:269-272) for their BatchNorm running statistics, minus the
                 # logits layer (engine: stats_only)
                 unused = self.d_loss_type == "normal"
-                self.D1.stats_only = self.D2.stats_only = unused
-                C1_real = self._on(l1, self.D1, [x, m])
-                C2_real = self._on(l2, self.D2, [x, m, y])
-                self.D1.stats_only = self.D2.stats_only = False
+                # ... and, with LATE_STATS_CALLS, after the fake-input calls (whose running-statistics updates are
+                # held back and applied after theirs, in the reference's order: real then fake per BatchNorm) -- the
+                # G step's critical path (D update -> fake-input forwards -> their input gradients -> G backward)
+                # no longer waits for two forwards whose outputs nothing reads
+                late = unused and LATE_STATS_CALLS
+                if not late:
+                    self.D1.stats_only = self.D2.stats_only = unused
+                    C1_real = self._on(l1, self.D1, [x, m])
+                    C2_real = self._on(l2, self.D2, [x, m, y])
+                    self.D1.stats_only = self.D2.stats_only = False
                 if unused:  # (zero-element placeholders: the logits were not computed)
                     C1_real = C2_real = None
-                C1_fake = self._on(l1, self.D1, [x, m_pred])
-                C2_fake = self._on(l2, self.D2, [x, m_pred, y_pred])
+                if late:
+                    held = ([], [])
+                    self.D1.defer_running, self.D2.defer_running = held
+                try:
+                    C1_fake = self._on(l1, self.D1, [x, m_pred])
+                    C2_fake = self._on(l2, self.D2, [x, m_pred, y_pred])
+                finally:
+                    self.D1.defer_running = self.D2.defer_running = None
                 if l1 is not None:
                     engine.wait_stream(main, l1)
                     engine.wait_stream(main, l2)
@@ -443,6 +459,17 @@ class STCGAN(object):
             if training:
                 self._exchange(("G1", "G2"), 1)
                 weighted_loss(G_loss, weight).backward()
+                if late:  # the statistics-only real-input calls, then the fake calls' held running updates
+                    self.D1.stats_only = self.D2.stats_only = True
+                    try:
+                        self._on(l1, self.D1, [x, m])
+                        self._on(l2, self.D2, [x, m, y])
+                    finally:
+                        self.D1.stats_only = self.D2.stats_only = False
+                    for lane, lst in zip((l1, l2), held):
+                        with (torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext()):
+                            for item in lst:
+                                ops.bn_running_update(*item)
                 self._finish_exchange(("G2", "G1"))
                 self.optim_G.step()
         if l1 is not None:  # nothing on the side lanes outlives the step

@@ -87,3 +87,23 @@ def test_early_d_backward_bit_identical(streams, early):
     for n in NETS:
         for k, v in ref_state[n].items():
             assert torch.equal(state[n][k], v), (n, k)
+
+
+@pytest.mark.parametrize("streams", [False, True], ids=["one_stream", "lanes"])
+def test_late_stats_calls_bit_identical(streams):
+    """The G step's statistics-only real-input discriminator calls after the fake-input ones, the fake calls' running-
+    statistics updates held back and applied after theirs (stcgan.LATE_STATS_CALLS), against the reference's call
+    order: every parameter and BatchNorm buffer (running statistics, num_batches_tracked) and loss identical."""
+    from stcgan_amd import stcgan as st
+    prev = st.LATE_STATS_CALLS
+    try:
+        st.LATE_STATS_CALLS = False
+        ref_state, ref_losses = _run(streams, streams, streams, "normal")
+        st.LATE_STATS_CALLS = True
+        state, losses = _run(streams, streams, streams, "normal")
+    finally:
+        st.LATE_STATS_CALLS = prev
+    assert losses == ref_losses
+    for n in NETS:
+        for k, v in ref_state[n].items():
+            assert torch.equal(state[n][k], v), (n, k)
