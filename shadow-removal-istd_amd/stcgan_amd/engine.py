@@ -53,8 +53,10 @@ def _trace_new(kind):
 # stream and overlap the rest of the chain -- most of the deep (1x1-8x8) layers' kernels are latency-bound
 # small grids.  Joined before the backward returns its gradients.
 WGRAD_OVERLAP = True
-# interleaved A/B (scripts/train_steps.py --ab): none 13.74, <= 32x32 13.45, <= 64x64 13.64, all 13.75 ms/step
-WGRAD_OVERLAP_MAX_PIX = 32 * 32
+# interleaved A/B (scripts/train_steps.py --ab): round 2: none 13.74, <= 32x32 13.45, <= 64x64 13.64, all 13.75
+# ms/step; round 6 (the D-step backward of each discriminator call right after its forward,
+# profiles/r06/wgrad_lane/): <= 32x32 10.57, <= 64x64 10.47, all 10.52 ms/step
+WGRAD_OVERLAP_MAX_PIX = 64 * 64
 _WG_SIDE = {}
 # streams (raw handles) whose backward keeps its weight gradients on the stream itself while a HIP graph
 # is being captured: the discriminator lanes (STCGAN.capture).  A weight-gradient side stream forked from a
