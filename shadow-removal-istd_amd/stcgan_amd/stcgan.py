@@ -146,6 +146,7 @@ class STCGAN(object):
         self._lanes_stale = True  # the side lanes must wait for the main stream before their next work
         # loss type "normal": the D and G objectives as one fused node each (loss.d_objective / g_objective)
         self.fused_objectives = bool(getattr(args, "fused_objectives", True))
+        self._gout_one = {}  # stream handle -> fp32 1 made on that stream (_term_backward)
         self._side = None
 
         data_dir = getattr(args, "data_dir", None)
@@ -309,10 +310,9 @@ class STCGAN(object):
         with (torch.cuda.stream(lane) if lane is not None else contextlib.nullcontext()):
             if weight == 1.0:  # (the objective's incoming gradient: one fp32 1, made once per stream that reads it)
                 key = lane.cuda_stream if lane is not None else None
-                gout = self._gout_one.get(key) if hasattr(self, "_gout_one") else None
+                gout = self._gout_one.get(key)
                 if gout is None:
-                    gout = torch.ones((), dtype=torch.float32, device=self.device)
-                    self.__dict__.setdefault("_gout_one", {})[key] = gout
+                    gout = self._gout_one[key] = torch.ones((), dtype=torch.float32, device=self.device)
             else:  # (weighted_loss: loss * weight, whose backward hands the objective fp32(weight))
                 gout = torch.full((), weight, dtype=torch.float32, device=self.device)
             torch.autograd.backward(C, d_term_grad(self.adv_loss, C, lam, gout, real))
